@@ -1,0 +1,140 @@
+"""Model hyper-parameters, read from GGUF metadata, plus presets for the architectures the reference
+advertises (reference `README.md:43-59`: Llama 2 7B/13B/70B, Mistral, Phi-2, Mixtral ...) and the
+BASELINE.json configs (Llama-2-7B Q4_K_M, Mistral-7B, Llama-2-70B, Mixtral-8x7B, Phi-2).
+"""
+from __future__ import annotations
+
+from dataclasses import asdict, dataclass, field, replace
+from typing import Any
+
+ROPE_NORM = 0   # rotate adjacent pairs (x[2i], x[2i+1]) -- llama.cpp "normal" mode (llama GGUF)
+ROPE_NEOX = 2   # rotate halves (x[i], x[i + n_rot/2]) -- phi2 / gpt-neox
+
+
+@dataclass
+class ModelConfig:
+    arch: str = "llama"            # "llama" (also Mistral / Mixtral / CodeLlama / Vicuna), "phi2"
+    n_vocab: int = 32000
+    n_embd: int = 4096
+    n_layer: int = 32
+    n_head: int = 32
+    n_head_kv: int = 32
+    n_ff: int = 11008
+    n_rot: int = 128
+    rope_base: float = 10000.0
+    rope_mode: int = ROPE_NORM
+    norm_eps: float = 1e-5
+    ctx_len: int = 4096
+    n_expert: int = 0
+    n_expert_used: int = 0
+    sliding_window: int = 0
+    bos_id: int = 1
+    eos_id: int = 2
+    name: str = ""
+    extra: dict[str, Any] = field(default_factory=dict)
+
+    @property
+    def head_dim(self) -> int:
+        return self.n_embd // self.n_head
+
+    @property
+    def n_embd_kv(self) -> int:
+        return self.head_dim * self.n_head_kv
+
+    @property
+    def gqa(self) -> int:
+        return self.n_head // self.n_head_kv
+
+    @property
+    def uses_layernorm(self) -> bool:
+        return self.arch == "phi2"
+
+    def to_dict(self) -> dict:
+        return asdict(self)
+
+    @classmethod
+    def from_gguf_metadata(cls, md: dict[str, Any]) -> "ModelConfig":
+        arch = str(md.get("general.architecture", "llama"))
+        p = arch + "."
+
+        def g(k, default=None):
+            return md.get(p + k, default)
+
+        tokens = md.get("tokenizer.ggml.tokens")
+        n_embd = int(g("embedding_length"))
+        n_head = int(g("attention.head_count"))
+        cfg = cls(
+            arch="phi2" if arch == "phi2" else "llama",
+            n_vocab=int(g("vocab_size", len(tokens) if tokens is not None else 32000)),
+            n_embd=n_embd,
+            n_layer=int(g("block_count")),
+            n_head=n_head,
+            n_head_kv=int(g("attention.head_count_kv", n_head)),
+            n_ff=int(g("feed_forward_length")),
+            n_rot=int(g("rope.dimension_count", n_embd // n_head)),
+            rope_base=float(g("rope.freq_base", 10000.0)),
+            rope_mode=ROPE_NEOX if arch == "phi2" else ROPE_NORM,
+            norm_eps=float(g("attention.layer_norm_rms_epsilon", g("attention.layer_norm_epsilon", 1e-5))),
+            ctx_len=int(g("context_length", 4096)),
+            n_expert=int(g("expert_count", 0)),
+            n_expert_used=int(g("expert_used_count", 0)),
+            sliding_window=int(g("attention.sliding_window", 0) or 0),
+            bos_id=int(md.get("tokenizer.ggml.bos_token_id", 1)),
+            eos_id=int(md.get("tokenizer.ggml.eos_token_id", 2)),
+            name=str(md.get("general.name", "")),
+        )
+        return cfg
+
+    def to_gguf_metadata(self) -> dict[str, Any]:
+        a = "phi2" if self.arch == "phi2" else "llama"
+        p = a + "."
+        md: dict[str, Any] = {
+            "general.architecture": a,
+            "general.name": self.name or a,
+            p + "context_length": self.ctx_len,
+            p + "embedding_length": self.n_embd,
+            p + "block_count": self.n_layer,
+            p + "feed_forward_length": self.n_ff,
+            p + "rope.dimension_count": self.n_rot,
+            p + "attention.head_count": self.n_head,
+            p + "attention.head_count_kv": self.n_head_kv,
+        }
+        if a == "phi2":
+            md[p + "attention.layer_norm_epsilon"] = float(self.norm_eps)
+        else:
+            md[p + "attention.layer_norm_rms_epsilon"] = float(self.norm_eps)
+            md[p + "rope.freq_base"] = float(self.rope_base)
+        if self.n_expert:
+            md[p + "expert_count"] = self.n_expert
+            md[p + "expert_used_count"] = self.n_expert_used
+        return md
+
+
+PRESETS: dict[str, ModelConfig] = {
+    # BASELINE headline: Llama-2-7B Q4_K_M
+    "llama2-7b": ModelConfig(name="llama2-7b"),
+    "llama2-13b": ModelConfig(name="llama2-13b", n_embd=5120, n_layer=40, n_head=40, n_head_kv=40,
+                              n_ff=13824),
+    "llama2-70b": ModelConfig(name="llama2-70b", n_embd=8192, n_layer=80, n_head=64, n_head_kv=8,
+                              n_ff=28672),
+    "mistral-7b": ModelConfig(name="mistral-7b", n_head_kv=8, n_ff=14336, ctx_len=32768,
+                              rope_base=1000000.0),
+    "mixtral-8x7b": ModelConfig(name="mixtral-8x7b", n_head_kv=8, n_ff=14336, ctx_len=32768,
+                                rope_base=1000000.0, n_expert=8, n_expert_used=2),
+    "phi2": ModelConfig(name="phi2", arch="phi2", n_vocab=51200, n_embd=2560, n_layer=32, n_head=32,
+                        n_head_kv=32, n_ff=10240, n_rot=32, rope_mode=ROPE_NEOX, norm_eps=1e-5,
+                        ctx_len=2048, bos_id=50256, eos_id=50256),
+    # small shapes of the same families for tests (K multiples of 256 so every quant type applies)
+    "tiny-llama": ModelConfig(name="tiny-llama", n_vocab=512, n_embd=256, n_layer=2, n_head=4,
+                              n_head_kv=2, n_ff=512, n_rot=64, ctx_len=256),
+    "tiny-mixtral": ModelConfig(name="tiny-mixtral", n_vocab=512, n_embd=256, n_layer=2, n_head=4,
+                                n_head_kv=2, n_ff=512, n_rot=64, ctx_len=256, n_expert=4,
+                                n_expert_used=2),
+    "tiny-phi2": ModelConfig(name="tiny-phi2", arch="phi2", n_vocab=512, n_embd=256, n_layer=2,
+                             n_head=4, n_head_kv=4, n_ff=1024, n_rot=32, rope_mode=ROPE_NEOX,
+                             ctx_len=256, bos_id=0, eos_id=0),
+}
+
+
+def preset(name: str, **overrides) -> ModelConfig:
+    return replace(PRESETS[name], **overrides)

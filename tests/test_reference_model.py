@@ -1,0 +1,44 @@
+import numpy as np
+import torch
+
+from ollama_operator_amd.gguf import read_gguf
+from ollama_operator_amd.models.config import ModelConfig
+from ollama_operator_amd.models.reference import KVCacheRef, ReferenceModel
+
+
+def test_config_from_gguf(tiny_models):
+    g = read_gguf(tiny_models["tiny-llama"])
+    cfg = ModelConfig.from_gguf_metadata(g.metadata)
+    assert (cfg.n_embd, cfg.n_layer, cfg.n_head, cfg.n_head_kv) == (256, 2, 4, 2)
+    assert cfg.head_dim == 64
+    g2 = read_gguf(tiny_models["tiny-mixtral"])
+    assert ModelConfig.from_gguf_metadata(g2.metadata).n_expert == 4
+    g3 = read_gguf(tiny_models["tiny-phi2"])
+    assert ModelConfig.from_gguf_metadata(g3.metadata).arch == "phi2"
+
+
+def _check_incremental(path):
+    g = read_gguf(path)
+    m = ReferenceModel(g)
+    toks = torch.tensor([1, 5, 9, 33, 2, 7, 100, 4])
+    full = m.forward(toks, KVCacheRef(m.cfg, 64), start=0)
+    c = KVCacheRef(m.cfg, 64)
+    part = [m.forward(toks[:5], c)]
+    for t in toks[5:]:
+        part.append(m.forward(t[None], c))
+    inc = torch.cat(part)
+    assert torch.isfinite(full).all()
+    np.testing.assert_allclose(inc.numpy(), full.numpy(), rtol=1e-4, atol=1e-4)
+    return full
+
+
+def test_reference_llama_incremental_matches_full(tiny_models):
+    _check_incremental(tiny_models["tiny-llama"])
+
+
+def test_reference_mixtral_incremental_matches_full(tiny_models):
+    _check_incremental(tiny_models["tiny-mixtral"])
+
+
+def test_reference_phi2_incremental_matches_full(tiny_models):
+    _check_incremental(tiny_models["tiny-phi2"])
