@@ -1,0 +1,311 @@
+// Python bindings for the gfx950 kernels, the native GGUF loader and the step executor.
+// Deliberately torch-header-free: device pointers and HIP streams cross the boundary as integers
+// (tensor.data_ptr(), torch.cuda.current_stream().cuda_stream), which keeps the build to seconds
+// and lets the executor's launches be captured by torch.cuda.CUDAGraph (hipGraph) unchanged.
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <memory>
+#include <stdexcept>
+
+#include "gguf/gguf.h"
+#include "kernels/ops.h"
+#include "runtime/executor.h"
+
+namespace py = pybind11;
+using namespace omx;
+
+static inline hipStream_t S(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
+template <class T>
+static inline T* Pp(uintptr_t p) { return reinterpret_cast<T*>(p); }
+
+static QMat qmat(py::object o) {
+  QMat m{};
+  if (o.is_none()) return m;
+  auto t = o.cast<py::tuple>();
+  if (t.size() != 7) throw std::runtime_error("qmat tuple must be (s0, s1, s2, s3, N, K, qtype)");
+  m.s0 = Pp<const uint8_t>(t[0].cast<uintptr_t>());
+  m.s1 = Pp<const uint8_t>(t[1].cast<uintptr_t>());
+  m.s2 = Pp<const uint8_t>(t[2].cast<uintptr_t>());
+  m.s3 = Pp<const uint8_t>(t[3].cast<uintptr_t>());
+  m.N = t[4].cast<int>();
+  m.K = t[5].cast<int>();
+  m.qtype = t[6].cast<int>();
+  if (m.qtype != QT_Q4_0 && m.qtype != QT_Q8_0 && m.qtype != QT_Q4_K && m.qtype != QT_Q6_K)
+    throw std::runtime_error("unsupported device quant type " + std::to_string(m.qtype));
+  const int blk = (m.qtype == QT_Q4_K || m.qtype == QT_Q6_K) ? 256 : 32;
+  if (m.K % blk || m.K <= 0 || m.N <= 0) throw std::runtime_error("bad qmat geometry");
+  return m;
+}
+
+static void check_attn(int H, int n_kv, int D) {
+  if (n_kv <= 0 || H % n_kv) throw std::runtime_error("H must be a multiple of n_kv");
+  const int G = H / n_kv;
+  if (G != 1 && G != 2 && G != 4 && G != 8) throw std::runtime_error("unsupported GQA group size");
+  if (D != 64 && D != 80 && D != 96 && D != 128) throw std::runtime_error("unsupported head dim");
+}
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "ollama-operator-amd native core: gfx950 HIP kernels, GGUF loader, step executor";
+
+  // ------------------------------------------------------------------ GGUF
+  py::class_<GGUFMap>(m, "GGUFMap")
+      .def(py::init<const std::string&>())
+      .def_property_readonly("size", &GGUFMap::size)
+      .def_property_readonly("version", &GGUFMap::version)
+      .def("tensors", [](const GGUFMap& g) {
+        py::list out;
+        for (const auto& e : g.tensors()) {
+          py::dict d;
+          d["name"] = e.name;
+          d["dims"] = e.dims;
+          d["type"] = e.type;
+          d["offset"] = e.offset;
+          d["nbytes"] = e.nbytes;
+          out.append(d);
+        }
+        return out;
+      })
+      .def("data_ptr", [](const GGUFMap& g, const std::string& name) {
+        return reinterpret_cast<uintptr_t>(g.data(g.get(name)));
+      })
+      .def("repack", [](const GGUFMap& g, const std::string& name, py::array_t<int64_t> rows,
+                        py::array_t<int64_t> dst_rows, int64_t K_src, int64_t kb0, int64_t kb1,
+                        std::vector<uintptr_t> dst, int n_threads) {
+        const auto& e = g.get(name);
+        uint8_t* d[4] = {nullptr, nullptr, nullptr, nullptr};
+        for (size_t i = 0; i < dst.size() && i < 4; ++i) d[i] = Pp<uint8_t>(dst[i]);
+        auto r = rows.unchecked<1>();
+        const int64_t n_src_rows = e.n_elements / K_src;
+        for (py::ssize_t i = 0; i < r.shape(0); ++i)
+          if (r(i) < 0 || r(i) >= n_src_rows) throw std::runtime_error("repack: row out of range");
+        if (dst_rows.shape(0) != rows.shape(0)) throw std::runtime_error("repack: rows/dst_rows length");
+        py::gil_scoped_release nogil;
+        repack_rows(g.data(e), e.type, K_src, rows.data(), dst_rows.data(), rows.shape(0), kb0, kb1, d, n_threads);
+      });
+  m.def("repack_ptr", [](uintptr_t src, int qtype, int64_t K_src, py::array_t<int64_t> rows,
+                         py::array_t<int64_t> dst_rows, int64_t kb0, int64_t kb1, std::vector<uintptr_t> dst,
+                         int n_threads) {
+    uint8_t* d[4] = {nullptr, nullptr, nullptr, nullptr};
+    for (size_t i = 0; i < dst.size() && i < 4; ++i) d[i] = Pp<uint8_t>(dst[i]);
+    if (dst_rows.shape(0) != rows.shape(0)) throw std::runtime_error("repack: rows/dst_rows length");
+    py::gil_scoped_release nogil;
+    repack_rows(Pp<const uint8_t>(src), qtype, K_src, rows.data(), dst_rows.data(), rows.shape(0), kb0, kb1, d,
+                n_threads);
+  });
+
+  // ------------------------------------------------------------------ single ops (tests, prefill)
+  m.def("gemv", [](py::object w, int B, uintptr_t x, int ldx, int norm, uintptr_t norm_w, uintptr_t norm_b,
+                   float eps, int epi, uintptr_t y, int ldy, uintptr_t bias, int row_offset, py::dict qkv,
+                   uintptr_t stream) {
+    GemvParams P{};
+    P.w = qmat(w);
+    P.B = B;
+    P.x = Pp<const float>(x);
+    P.ldx = ldx;
+    P.norm = norm;
+    P.norm_w = Pp<const float>(norm_w);
+    P.norm_b = Pp<const float>(norm_b);
+    P.eps = eps;
+    P.epi = epi;
+    P.y = Pp<float>(y);
+    P.ldy = ldy;
+    P.bias = Pp<const float>(bias);
+    P.row_offset = row_offset;
+    P.n_sel = 1;
+    if (epi == EPI_QKV) {
+      P.pos = Pp<const int>(qkv["pos"].cast<uintptr_t>());
+      P.slot = Pp<const int>(qkv["slot"].cast<uintptr_t>());
+      P.kc = Pp<void>(qkv["kc"].cast<uintptr_t>());
+      P.vc = Pp<void>(qkv["vc"].cast<uintptr_t>());
+      P.inv_freq = Pp<const float>(qkv["inv_freq"].cast<uintptr_t>());
+      P.Eq = qkv["Eq"].cast<int>();
+      P.Ekv = qkv["Ekv"].cast<int>();
+      P.D = qkv["D"].cast<int>();
+      P.n_rot = qkv["n_rot"].cast<int>();
+      P.n_kv = qkv["n_kv"].cast<int>();
+      P.bs = qkv["bs"].cast<int>();
+    }
+    if (qkv.contains("expert_ids")) {
+      P.expert_ids = Pp<const int>(qkv["expert_ids"].cast<uintptr_t>());
+      P.expert_w = Pp<const float>(qkv.contains("expert_w") ? qkv["expert_w"].cast<uintptr_t>() : 0);
+      P.n_sel = qkv["n_sel"].cast<int>();
+      P.x_per_sel = qkv.contains("x_sel_stride") ? 1 : 0;
+      P.x_sel_stride = qkv.contains("x_sel_stride") ? qkv["x_sel_stride"].cast<long long>() : 0;
+      P.y_sel_stride = qkv.contains("y_sel_stride") ? qkv["y_sel_stride"].cast<long long>() : 0;
+    }
+    gemv(P, S(stream));
+  });
+  m.def("attention", [](uintptr_t q, int ldq, uintptr_t kc, uintptr_t vc, uintptr_t block_table, int max_blocks,
+                        uintptr_t q_seq, uintptr_t q_len, int NQ, int H, int n_kv, int D, int bs, float scale,
+                        int window, uintptr_t out, int ldo, uintptr_t ws, int n_splits, uintptr_t stream) {
+    check_attn(H, n_kv, D);
+    AttnParams A{};
+    A.q = Pp<const float>(q);
+    A.ldq = ldq;
+    A.kc = Pp<const void>(kc);
+    A.vc = Pp<const void>(vc);
+    A.block_table = Pp<const int>(block_table);
+    A.max_blocks = max_blocks;
+    A.q_seq = Pp<const int>(q_seq);
+    A.q_len = Pp<const int>(q_len);
+    A.NQ = NQ;
+    A.H = H;
+    A.n_kv = n_kv;
+    A.D = D;
+    A.bs = bs;
+    A.scale = scale;
+    A.window = window;
+    A.out = Pp<float>(out);
+    A.ldo = ldo;
+    A.ws = Pp<float>(ws);
+    A.n_splits = n_splits;
+    attention_decode(A, S(stream));
+  });
+  m.def("attention_ws_floats", &attention_ws_floats);
+  m.def("embed_rows", [](py::object w, uintptr_t rows, int n, uintptr_t out, int ldo, uintptr_t stream) {
+    embed_rows(qmat(w), Pp<const int>(rows), n, Pp<float>(out), ldo, S(stream));
+  });
+  m.def("dequant_f16", [](py::object w, uintptr_t out, uintptr_t stream) {
+    dequant_f16(qmat(w), Pp<void>(out), S(stream));
+  });
+  m.def("argmax", [](uintptr_t logits, int B, int V, int ld, uintptr_t out, uintptr_t stream) {
+    argmax(Pp<const float>(logits), B, V, ld, Pp<int>(out), S(stream));
+  });
+  m.def("moe_route", [](uintptr_t logits, int B, int X, int k, uintptr_t ids, uintptr_t w, uintptr_t stream) {
+    moe_route(Pp<const float>(logits), B, X, k, Pp<int>(ids), Pp<float>(w), S(stream));
+  });
+  m.def("add_inplace", [](uintptr_t y, uintptr_t x, long long n, uintptr_t stream) {
+    add_inplace(Pp<float>(y), Pp<const float>(x), n, S(stream));
+  });
+  m.def("sample", [](py::dict d, uintptr_t stream) {
+    SampleParams P{};
+    P.logits = Pp<const float>(d["logits"].cast<uintptr_t>());
+    P.B = d["B"].cast<int>();
+    P.V = d["V"].cast<int>();
+    P.ld = d["ld"].cast<int>();
+    P.temperature = Pp<const float>(d["temperature"].cast<uintptr_t>());
+    P.top_k = Pp<const int>(d["top_k"].cast<uintptr_t>());
+    P.top_p = Pp<const float>(d["top_p"].cast<uintptr_t>());
+    P.min_p = Pp<const float>(d["min_p"].cast<uintptr_t>());
+    P.repeat_penalty = Pp<const float>(d["repeat_penalty"].cast<uintptr_t>());
+    P.presence_penalty = Pp<const float>(d["presence_penalty"].cast<uintptr_t>());
+    P.frequency_penalty = Pp<const float>(d["frequency_penalty"].cast<uintptr_t>());
+    P.history = Pp<int>(d["history"].cast<uintptr_t>());
+    P.hist_count = Pp<int>(d["hist_count"].cast<uintptr_t>());
+    P.hist_cap = d["hist_cap"].cast<int>();
+    P.repeat_last_n = Pp<const int>(d["repeat_last_n"].cast<uintptr_t>());
+    P.seed = Pp<const unsigned long long>(d["seed"].cast<uintptr_t>());
+    P.step = Pp<int>(d["step"].cast<uintptr_t>());
+    P.out = Pp<int>(d["out"].cast<uintptr_t>());
+    P.out_logprob = Pp<float>(d.contains("out_logprob") ? d["out_logprob"].cast<uintptr_t>() : 0);
+    sample(P, S(stream));
+  });
+
+  // ------------------------------------------------------------------ executor
+  py::class_<Executor>(m, "Executor")
+      .def(py::init<>())
+      .def("configure", [](Executor& e, py::dict c) {
+        ExecConfig& k = e.cfg;
+        k.arch = c["arch"].cast<int>();
+        k.E = c["E"].cast<int>();
+        k.H = c["H"].cast<int>();
+        k.Hkv = c["Hkv"].cast<int>();
+        k.D = c["D"].cast<int>();
+        k.n_rot = c["n_rot"].cast<int>();
+        k.F = c["F"].cast<int>();
+        k.n_layer = c["n_layer"].cast<int>();
+        k.V = c["V"].cast<int>();
+        k.eps = c["eps"].cast<float>();
+        k.n_expert = c["n_expert"].cast<int>();
+        k.n_expert_used = c["n_expert_used"].cast<int>();
+        k.window = c["window"].cast<int>();
+        k.tp = c["tp"].cast<int>();
+        check_attn(k.H, k.Hkv, k.D);
+        e.layers.assign(k.n_layer, LayerW{});
+      })
+      .def("set_globals", [](Executor& e, py::object tok_embd, uintptr_t out_norm, uintptr_t out_norm_b,
+                             py::object lm_head, uintptr_t lm_bias, uintptr_t inv_freq) {
+        e.tok_embd = qmat(tok_embd);
+        e.out_norm = Pp<const float>(out_norm);
+        e.out_norm_b = Pp<const float>(out_norm_b);
+        e.lm_head = qmat(lm_head);
+        e.lm_bias = Pp<const float>(lm_bias);
+        e.inv_freq = Pp<const float>(inv_freq);
+      })
+      .def("set_layer", [](Executor& e, int i, py::dict d) {
+        if (i < 0 || i >= (int)e.layers.size()) throw std::runtime_error("layer index");
+        LayerW& L = e.layers[i];
+        auto ptr = [&](const char* k) -> uintptr_t { return d.contains(k) ? d[k].cast<uintptr_t>() : 0; };
+        auto qm = [&](const char* k) { return d.contains(k) ? qmat(d[k]) : QMat{}; };
+        L.attn_norm = Pp<const float>(ptr("attn_norm"));
+        L.attn_norm_b = Pp<const float>(ptr("attn_norm_b"));
+        L.ffn_norm = Pp<const float>(ptr("ffn_norm"));
+        L.wqk = qm("wqk");
+        L.wv = qm("wv");
+        L.qkv_fused = d.contains("wv") ? 0 : 1;
+        L.qkv_bias = Pp<const float>(ptr("qkv_bias"));
+        L.wo = qm("wo");
+        L.bo = Pp<const float>(ptr("bo"));
+        L.wgu = qm("wgu");
+        L.bup = Pp<const float>(ptr("bup"));
+        L.wdown = qm("wdown");
+        L.bdown = Pp<const float>(ptr("bdown"));
+        L.router = qm("router");
+        L.gu_exps = qm("gu_exps");
+        L.down_exps = qm("down_exps");
+        L.kc = Pp<void>(ptr("kc"));
+        L.vc = Pp<void>(ptr("vc"));
+      })
+      .def("set_workspace", [](Executor& e, py::dict d) {
+        auto ptr = [&](const char* k) -> uintptr_t { return d.contains(k) ? d[k].cast<uintptr_t>() : 0; };
+        Workspace& w = e.ws;
+        w.resid = Pp<float>(ptr("resid"));
+        w.qbuf = Pp<float>(ptr("qbuf"));
+        w.abuf = Pp<float>(ptr("abuf"));
+        w.hbuf = Pp<float>(ptr("hbuf"));
+        w.ypart = Pp<float>(ptr("ypart"));
+        w.lbuf = Pp<float>(ptr("lbuf"));
+        w.rlogits = Pp<float>(ptr("rlogits"));
+        w.eids = Pp<int>(ptr("eids"));
+        w.ew = Pp<float>(ptr("ew"));
+        w.attn_ws = Pp<float>(ptr("attn_ws"));
+        w.max_B = d["max_B"].cast<int>();
+        w.n_splits = d["n_splits"].cast<int>();
+      })
+      .def("set_splits", [](Executor& e, int n) { e.ws.n_splits = n; })
+      .def("run", [](Executor& e, const std::string& what, int layer, py::dict d, uintptr_t stream) {
+        StepInputs in;
+        auto ptr = [&](const char* k) -> uintptr_t { return d.contains(k) ? d[k].cast<uintptr_t>() : 0; };
+        in.B = d["B"].cast<int>();
+        in.tokens = Pp<const int>(ptr("tokens"));
+        in.pos = Pp<const int>(ptr("pos"));
+        in.slot = Pp<const int>(ptr("slot"));
+        in.q_len = Pp<const int>(ptr("q_len"));
+        in.q_seq = Pp<const int>(ptr("q_seq"));
+        in.block_table = Pp<const int>(ptr("block_table"));
+        in.max_blocks = d["max_blocks"].cast<int>();
+        in.bs = d["bs"].cast<int>();
+        in.n_logits = d.contains("n_logits") ? d["n_logits"].cast<int>() : 0;
+        in.logit_idx = Pp<const int>(ptr("logit_idx"));
+        in.logits = Pp<float>(ptr("logits"));
+        if (in.B > e.ws.max_B) throw std::runtime_error("batch exceeds workspace max_B");
+        hipStream_t s = S(stream);
+        if (what == "forward") e.forward(in, s);
+        else if (what == "embed") e.embed(in, s);
+        else if (what == "attn") e.attn_block(layer, in, s);
+        else if (what == "ffn") e.ffn_block(layer, in, s);
+        else if (what == "head") e.head(in, s);
+        else throw std::runtime_error("unknown stage " + what);
+      });
+
+  m.attr("NORM_NONE") = (int)NORM_NONE;
+  m.attr("NORM_RMS") = (int)NORM_RMS;
+  m.attr("NORM_LAYER") = (int)NORM_LAYER;
+  m.attr("EPI_STORE") = (int)EPI_STORE;
+  m.attr("EPI_ADD") = (int)EPI_ADD;
+  m.attr("EPI_GLU") = (int)EPI_GLU;
+  m.attr("EPI_GELU") = (int)EPI_GELU;
+  m.attr("EPI_QKV") = (int)EPI_QKV;
+}

@@ -1,0 +1,220 @@
+// Native GGUF loader: mmap + bounds-checked tensor index + multi-threaded
+// repack of ggml quant blocks into the 16-B-aligned device streams of csrc/kernels/qmat.h, with
+// row selection/permutation (q/k NEOX pairing, gate/up interleave, TP row shards) and K-block
+// slicing (TP column shards) fused into the same pass over the mapped file.
+#include "gguf.h"
+
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cstring>
+#include <stdexcept>
+#include <thread>
+
+namespace omx {
+
+namespace {
+
+struct Cur {
+  const uint8_t* p;
+  size_t n, pos = 0;
+  void need(size_t k) {
+    if (k > n || pos + k > n) throw std::runtime_error("truncated GGUF header");
+  }
+  template <class T>
+  T get() {
+    need(sizeof(T));
+    T v;
+    std::memcpy(&v, p + pos, sizeof(T));
+    pos += sizeof(T);
+    return v;
+  }
+  std::string str() {
+    const uint64_t len = get<uint64_t>();
+    if (len > (1u << 24)) throw std::runtime_error("GGUF string too long");
+    need(len);
+    std::string s((const char*)p + pos, len);
+    pos += len;
+    return s;
+  }
+  void skip_value(uint32_t t, int depth = 0) {
+    static const int sz[] = {1, 1, 2, 2, 4, 4, 4, 1, -1, -1, 8, 8, 8};
+    if (t > 12) throw std::runtime_error("bad GGUF value type");
+    if (t == 8) { (void)str(); return; }
+    if (t == 9) {
+      if (depth > 2) throw std::runtime_error("GGUF arrays nested too deep");
+      const uint32_t et = get<uint32_t>();
+      const uint64_t cnt = get<uint64_t>();
+      if (cnt > (1ull << 28)) throw std::runtime_error("GGUF array too long");
+      if (et == 8 || et == 9) {
+        for (uint64_t i = 0; i < cnt; ++i) skip_value(et, depth + 1);
+      } else {
+        if (et > 12) throw std::runtime_error("bad GGUF array type");
+        need(cnt * sz[et]);
+        pos += cnt * sz[et];
+      }
+      return;
+    }
+    need(sz[t]);
+    pos += sz[t];
+  }
+};
+
+void block_geom(int t, int& blk, int& nb) {
+  switch (t) {
+    case 0: blk = 1; nb = 4; return;
+    case 1: case 30: blk = 1; nb = 2; return;
+    case 2: blk = 32; nb = 18; return;
+    case 3: blk = 32; nb = 20; return;
+    case 6: blk = 32; nb = 22; return;
+    case 7: blk = 32; nb = 24; return;
+    case 8: blk = 32; nb = 34; return;
+    case 10: blk = 256; nb = 84; return;
+    case 11: blk = 256; nb = 110; return;
+    case 12: blk = 256; nb = 144; return;
+    case 13: blk = 256; nb = 176; return;
+    case 14: blk = 256; nb = 210; return;
+    case 15: blk = 256; nb = 292; return;
+    default: throw std::runtime_error("unsupported ggml type " + std::to_string(t));
+  }
+}
+
+}  // namespace
+
+GGUFMap::GGUFMap(const std::string& path) {
+  fd_ = ::open(path.c_str(), O_RDONLY);
+  if (fd_ < 0) throw std::runtime_error("cannot open " + path);
+  struct stat st;
+  if (fstat(fd_, &st) != 0) throw std::runtime_error("stat failed");
+  size_ = (size_t)st.st_size;
+  base_ = (const uint8_t*)mmap(nullptr, size_, PROT_READ, MAP_SHARED, fd_, 0);
+  if (base_ == MAP_FAILED) throw std::runtime_error("mmap failed");
+  Cur c{base_, size_};
+  if (c.get<uint32_t>() != 0x46554747u) throw std::runtime_error("not a GGUF file");
+  version_ = c.get<uint32_t>();
+  if (version_ != 2 && version_ != 3) throw std::runtime_error("unsupported GGUF version");
+  const uint64_t nt = c.get<uint64_t>(), nkv = c.get<uint64_t>();
+  if (nt > (1u << 20) || nkv > (1u << 20)) throw std::runtime_error("implausible GGUF counts");
+  uint64_t align = 32;
+  for (uint64_t i = 0; i < nkv; ++i) {
+    const std::string key = c.str();
+    const uint32_t t = c.get<uint32_t>();
+    if (key == "general.alignment" && t == 4) {
+      align = c.get<uint32_t>();
+      if (align == 0 || (align & (align - 1))) throw std::runtime_error("bad alignment");
+    } else {
+      c.skip_value(t);
+    }
+  }
+  std::vector<TensorEntry> tmp;
+  for (uint64_t i = 0; i < nt; ++i) {
+    TensorEntry e;
+    e.name = c.str();
+    const uint32_t nd = c.get<uint32_t>();
+    if (nd == 0 || nd > 4) throw std::runtime_error("bad n_dims for " + e.name);
+    e.n_elements = 1;
+    for (uint32_t d = 0; d < nd; ++d) {
+      e.dims.push_back((int64_t)c.get<uint64_t>());
+      if (e.dims.back() <= 0) throw std::runtime_error("bad dim for " + e.name);
+      e.n_elements *= e.dims.back();
+    }
+    e.type = (int)c.get<uint32_t>();
+    e.offset = c.get<uint64_t>();
+    int blk, nb;
+    block_geom(e.type, blk, nb);
+    if (e.n_elements % blk) throw std::runtime_error("tensor not block aligned: " + e.name);
+    e.nbytes = e.n_elements / blk * nb;
+    tmp.push_back(e);
+  }
+  data_offset_ = (c.pos + align - 1) / align * align;
+  for (auto& e : tmp) {
+    e.offset += data_offset_;
+    if (e.offset + e.nbytes > size_) throw std::runtime_error("tensor data out of file: " + e.name);
+    index_[e.name] = tensors_.size();
+    tensors_.push_back(e);
+  }
+}
+
+GGUFMap::~GGUFMap() {
+  if (base_ && base_ != MAP_FAILED) munmap((void*)base_, size_);
+  if (fd_ >= 0) ::close(fd_);
+}
+
+const TensorEntry& GGUFMap::get(const std::string& name) const {
+  auto it = index_.find(name);
+  if (it == index_.end()) throw std::runtime_error("no tensor " + name);
+  return tensors_[it->second];
+}
+
+// stream geometry per row for K weights: bytes per row of each stream
+static void stream_bytes(int qt, int64_t K, int64_t out[4]) {
+  out[0] = out[1] = out[2] = out[3] = 0;
+  switch (qt) {
+    case 12: out[0] = K / 2; out[1] = K / 16; break;
+    case 14: out[0] = K / 2; out[1] = K / 4; out[2] = K / 16; out[3] = K / 128; break;
+    case 2: out[0] = K / 2; out[1] = K / 16; break;
+    case 8: out[0] = K; out[1] = K / 16; break;
+    default: throw std::runtime_error("repack: unsupported type");
+  }
+}
+
+void repack_rows(const uint8_t* src, int qtype, int64_t K_src, const int64_t* rows, const int64_t* dst_rows,
+                 int64_t n_rows, int64_t kb0, int64_t kb1, uint8_t* const dst[4], int n_threads) {
+  int blk, nb;
+  block_geom(qtype, blk, nb);
+  const int64_t nblk_src = K_src / blk;
+  if (kb0 < 0 || kb1 > nblk_src || kb0 >= kb1) throw std::runtime_error("repack: bad K block range");
+  const int64_t K = (kb1 - kb0) * blk;
+  int64_t sb[4];
+  stream_bytes(qtype, K, sb);
+  const int64_t row_bytes = nblk_src * nb;
+  auto work = [&](int64_t r0, int64_t r1) {
+    for (int64_t r = r0; r < r1; ++r) {
+      const uint8_t* s = src + rows[r] * row_bytes + kb0 * nb;
+      const int64_t o = dst_rows ? dst_rows[r] : r;
+      uint8_t* d0 = dst[0] + o * sb[0];
+      uint8_t* d1 = dst[1] + o * sb[1];
+      uint8_t* d2 = dst[2] ? dst[2] + o * sb[2] : nullptr;
+      uint8_t* d3 = dst[3] ? dst[3] + o * sb[3] : nullptr;
+      for (int64_t b = 0; b < kb1 - kb0; ++b, s += nb) {
+        switch (qtype) {
+          case 12:  // d,dmin,scales | qs
+            std::memcpy(d1 + 16 * b, s, 16);
+            std::memcpy(d0 + 128 * b, s + 16, 128);
+            break;
+          case 14:  // ql | qh | sc | d
+            std::memcpy(d0 + 128 * b, s, 128);
+            std::memcpy(d1 + 64 * b, s + 128, 64);
+            std::memcpy(d2 + 16 * b, s + 192, 16);
+            std::memcpy(d3 + 2 * b, s + 208, 2);
+            break;
+          case 2:  // d | qs
+            std::memcpy(d1 + 2 * b, s, 2);
+            std::memcpy(d0 + 16 * b, s + 2, 16);
+            break;
+          case 8:  // d | qs
+            std::memcpy(d1 + 2 * b, s, 2);
+            std::memcpy(d0 + 32 * b, s + 2, 32);
+            break;
+        }
+      }
+    }
+  };
+  n_threads = std::max(1, std::min<int>(n_threads, (int)std::min<int64_t>(n_rows, 64)));
+  if (n_threads == 1) {
+    work(0, n_rows);
+    return;
+  }
+  std::vector<std::thread> th;
+  const int64_t per = (n_rows + n_threads - 1) / n_threads;
+  for (int t = 0; t < n_threads; ++t) {
+    const int64_t a = t * per, b = std::min(n_rows, a + per);
+    if (a < b) th.emplace_back(work, a, b);
+  }
+  for (auto& t : th) t.join();
+}
+
+}  // namespace omx

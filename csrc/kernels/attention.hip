@@ -1,0 +1,194 @@
+// Paged-KV grouped-query attention for decode and chunked prefill.
+//
+// Grid (query, kv_head, split). One 256-thread block serves the G = H/H_kv query heads that share a
+// KV head, so each K/V row is read from HBM once per group (GQA reuse). 16 lanes cooperate on one
+// key (D/16 dims each, one 16-B load for D = 128), so a wave streams 4 keys per load instruction
+// and the 4 waves 16 keys per step; scores reduce inside the 16-lane group with xor-shuffles.
+// Online softmax per lane group, merged across groups/waves at the end. The key range of a query
+// is cut into `n_splits` equal chunks computed ON DEVICE from its length (flash-decode), so the
+// grid is fixed and the launch is hipGraph-capturable for any context length; a tiny combine
+// kernel merges split partials (skipped when n_splits == 1).
+// Causal prefill uses the same kernel: each prompt token is a query with length pos + 1.
+#include "common.h"
+#include "ops.h"
+
+namespace omx {
+
+template <int DPL>
+__device__ __forceinline__ void load_row(const f16* p, float* v) {
+  if constexpr (DPL == 8) {
+    const f16x8 t = *(const f16x8*)p;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (float)t[j];
+  } else if constexpr (DPL == 4) {
+    const f16x4 t = *(const f16x4*)p;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = (float)t[j];
+  } else {
+#pragma unroll
+    for (int j = 0; j < DPL; ++j) v[j] = (float)p[j];
+  }
+}
+
+template <int D, int G>
+__global__ __launch_bounds__(256) void attn_partial_kernel(AttnParams P) {
+  constexpr int DPL = D / 16;
+  __shared__ float sm[4][G][D + 2];
+  const int qi = blockIdx.x, kvh = blockIdx.y, split = blockIdx.z, S = gridDim.z;
+  const int seq = P.q_seq ? P.q_seq[qi] : qi;
+  const int len = P.q_len[qi];
+  const int kstart = P.window > 0 ? max(0, len - P.window) : 0;
+  const int nk = len - kstart;
+  const int chunk = (nk + S - 1) / S;
+  const int t0 = kstart + split * chunk;
+  const int t1 = min(len, t0 + chunk);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, tg = lane >> 4, li = lane & 15;
+
+  float q[G][DPL];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const float* qp = P.q + (long long)qi * P.ldq + (kvh * G + g) * D + li * DPL;
+#pragma unroll
+    for (int j = 0; j < DPL; ++j) q[g][j] = qp[j] * P.scale;
+  }
+  float m[G], l[G], acc[G][DPL];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    m[g] = -INFINITY;
+    l[g] = 0.f;
+#pragma unroll
+    for (int j = 0; j < DPL; ++j) acc[g][j] = 0.f;
+  }
+  const int* bt = P.block_table + (long long)seq * P.max_blocks;
+  const f16* kc = (const f16*)P.kc;
+  const f16* vc = (const f16*)P.vc;
+  for (int t = t0 + wave * 4 + tg; t < t1; t += 16) {
+    const long long blk = bt[t / P.bs];
+    const long long base = ((blk * P.n_kv + kvh) * P.bs + (t % P.bs)) * D + li * DPL;
+    float k[DPL], v[DPL];
+    load_row<DPL>(kc + base, k);
+    load_row<DPL>(vc + base, v);
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      float s = 0.f;
+#pragma unroll
+      for (int j = 0; j < DPL; ++j) s += q[g][j] * k[j];
+      s = group_sum<16>(s);
+      const float mn = fmaxf(m[g], s);
+      const float corr = __expf(m[g] - mn);
+      const float p = __expf(s - mn);
+      l[g] = l[g] * corr + p;
+#pragma unroll
+      for (int j = 0; j < DPL; ++j) acc[g][j] = acc[g][j] * corr + p * v[j];
+      m[g] = mn;
+    }
+  }
+  // merge the 4 token groups of the wave (lanes li, li+16, li+32, li+48)
+#pragma unroll
+  for (int sh = 16; sh <= 32; sh <<= 1) {
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const float mo = __shfl_xor(m[g], sh, 64), lo = __shfl_xor(l[g], sh, 64);
+      const float mn = fmaxf(m[g], mo);
+      const float c0 = mn == -INFINITY ? 0.f : __expf(m[g] - mn);
+      const float c1 = mn == -INFINITY ? 0.f : __expf(mo - mn);
+      l[g] = l[g] * c0 + lo * c1;
+#pragma unroll
+      for (int j = 0; j < DPL; ++j) acc[g][j] = acc[g][j] * c0 + __shfl_xor(acc[g][j], sh, 64) * c1;
+      m[g] = mn;
+    }
+  }
+  if (lane < 16) {
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+#pragma unroll
+      for (int j = 0; j < DPL; ++j) sm[wave][g][li * DPL + j] = acc[g][j];
+      if (li == 0) {
+        sm[wave][g][D] = m[g];
+        sm[wave][g][D + 1] = l[g];
+      }
+    }
+  }
+  __syncthreads();
+  // 4 waves merge: threads (g, d) over G*D outputs
+  for (int i = threadIdx.x; i < G * D; i += 256) {
+    const int g = i / D, d = i % D;
+    float M = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) M = fmaxf(M, sm[w][g][D]);
+    float L = 0.f, A = 0.f;
+    if (M != -INFINITY) {
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        const float c = __expf(sm[w][g][D] - M);
+        L += sm[w][g][D + 1] * c;
+        A += sm[w][g][d] * c;
+      }
+    }
+    const int h = kvh * G + g;
+    if (S == 1) {
+      P.out[(long long)qi * P.ldo + h * D + d] = L > 0.f ? A / L : 0.f;
+    } else {
+      float* ws = P.ws + (((long long)qi * P.H + h) * S + split) * (D + 2);
+      ws[d] = A;
+      if (d == 0) {
+        ws[D] = M;
+        ws[D + 1] = L;
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(128) void attn_combine_kernel(AttnParams P) {
+  const int qi = blockIdx.x, h = blockIdx.y, S = P.n_splits, D = P.D;
+  const float* ws = P.ws + ((long long)qi * P.H + h) * S * (D + 2);
+  float M = -INFINITY;
+  for (int s = 0; s < S; ++s)
+    if (ws[s * (D + 2) + D + 1] > 0.f) M = fmaxf(M, ws[s * (D + 2) + D]);
+  for (int d = threadIdx.x; d < D; d += blockDim.x) {
+    float L = 0.f, A = 0.f;
+    if (M != -INFINITY) {
+      for (int s = 0; s < S; ++s) {
+        const float* w = ws + s * (D + 2);
+        if (w[D + 1] > 0.f) {
+          const float c = __expf(w[D] - M);
+          L += w[D + 1] * c;
+          A += w[d] * c;
+        }
+      }
+    }
+    P.out[(long long)qi * P.ldo + h * D + d] = L > 0.f ? A / L : 0.f;
+  }
+}
+
+template <int D>
+static void launch_d(const AttnParams& P, hipStream_t s) {
+  const int G = P.H / P.n_kv;
+  dim3 grid(P.NQ, P.n_kv, P.n_splits);
+  switch (G) {
+    case 1: hipLaunchKernelGGL((attn_partial_kernel<D, 1>), grid, dim3(256), 0, s, P); break;
+    case 2: hipLaunchKernelGGL((attn_partial_kernel<D, 2>), grid, dim3(256), 0, s, P); break;
+    case 4: hipLaunchKernelGGL((attn_partial_kernel<D, 4>), grid, dim3(256), 0, s, P); break;
+    case 8: hipLaunchKernelGGL((attn_partial_kernel<D, 8>), grid, dim3(256), 0, s, P); break;
+    default: break;
+  }
+}
+
+void attention_decode(const AttnParams& P, hipStream_t s) {
+  if (P.NQ <= 0) return;
+  switch (P.D) {
+    case 64: launch_d<64>(P, s); break;
+    case 80: launch_d<80>(P, s); break;
+    case 96: launch_d<96>(P, s); break;
+    case 128: launch_d<128>(P, s); break;
+    default: break;
+  }
+  if (P.n_splits > 1)
+    hipLaunchKernelGGL(attn_combine_kernel, dim3(P.NQ, P.H), dim3(128), 0, s, P);
+}
+
+size_t attention_ws_floats(int NQ, int H, int D, int n_splits) {
+  return n_splits > 1 ? (size_t)NQ * H * n_splits * (D + 2) : 0;
+}
+
+}  // namespace omx

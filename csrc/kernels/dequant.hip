@@ -1,0 +1,86 @@
+// Row gather + dequantisation from the repacked quant streams (SURVEY.md §2.2 N15 embedding
+// gather) and whole-matrix dequantisation to fp16 (resident fp16 copies for MFMA prefill GEMMs).
+#include "common.h"
+#include "ops.h"
+
+namespace omx {
+
+// one block per gathered row; each thread dequantises 32-weight pieces
+__global__ __launch_bounds__(256) void embed_rows_kernel(QMat w, const int* rows, float* out, int ldo) {
+  const int b = blockIdx.x;
+  const long long row = rows[b];
+  const int P = w.K / 32;
+  float* o = out + (long long)b * ldo;
+  for (int p = threadIdx.x; p < P; p += blockDim.x) {
+    float lo[16], hi[16];
+    int olo, ohi;
+    dequant_piece(w, row, p, lo, hi, olo, ohi);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      *(f32x4*)(o + olo + 4 * j) = (f32x4){lo[4 * j], lo[4 * j + 1], lo[4 * j + 2], lo[4 * j + 3]};
+      *(f32x4*)(o + ohi + 4 * j) = (f32x4){hi[4 * j], hi[4 * j + 1], hi[4 * j + 2], hi[4 * j + 3]};
+    }
+  }
+}
+
+void embed_rows(const QMat& w, const int* rows, int n, float* out, int ldo, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(embed_rows_kernel, dim3(n), dim3(256), 0, s, w, rows, out, ldo);
+}
+
+// grid-stride over (row, piece)
+__global__ __launch_bounds__(256) void dequant_f16_kernel(QMat w, f16* out) {
+  const int P = w.K / 32;
+  const long long total = (long long)w.N * P;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long row = i / P;
+    const int p = (int)(i % P);
+    float lo[16], hi[16];
+    int olo, ohi;
+    dequant_piece(w, row, p, lo, hi, olo, ohi);
+    f16* o = out + row * w.K;
+    f16x8 a, b, c, d;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      a[j] = (f16)lo[j]; b[j] = (f16)lo[8 + j];
+      c[j] = (f16)hi[j]; d[j] = (f16)hi[8 + j];
+    }
+    *(f16x8*)(o + olo) = a;
+    *(f16x8*)(o + olo + 8) = b;
+    *(f16x8*)(o + ohi) = c;
+    *(f16x8*)(o + ohi + 8) = d;
+  }
+}
+
+void dequant_f16(const QMat& w, void* out, hipStream_t s) {
+  const long long total = (long long)w.N * (w.K / 32);
+  const int blocks = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
+  hipLaunchKernelGGL(dequant_f16_kernel, dim3(blocks), dim3(256), 0, s, w, (f16*)out);
+}
+
+__global__ void add_inplace_kernel(float* y, const float* x, long long n) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    y[i] += x[i];
+}
+
+void add_inplace(float* y, const float* x, long long n, hipStream_t s) {
+  const int blocks = (int)((n + 255) / 256 < 2048 ? (n + 255) / 256 : 2048);
+  hipLaunchKernelGGL(add_inplace_kernel, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, s, y, x, n);
+}
+
+__global__ __launch_bounds__(256) void rmsnorm_kernel(const float* x, const float* w, float eps, int n, float* out) {
+  __shared__ float red[4];
+  const float* xr = x + (long long)blockIdx.x * n;
+  float ss = 0.f;
+  for (int i = threadIdx.x; i < n; i += 256) ss += xr[i] * xr[i];
+  ss = block_sum<256>(ss, red);
+  const float r = rsqrtf(ss / n + eps);
+  for (int i = threadIdx.x; i < n; i += 256) out[(long long)blockIdx.x * n + i] = xr[i] * r * w[i];
+}
+
+void rmsnorm(const float* x, const float* w, float eps, int rows, int n, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(rmsnorm_kernel, dim3(rows), dim3(256), 0, s, x, w, eps, n, out);
+}
+
+}  // namespace omx

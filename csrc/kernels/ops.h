@@ -1,0 +1,100 @@
+// Host-visible interface of the gfx950 kernels. Plain C++ types only: this header is included by
+// the HIP kernel sources (hipcc) and by the torch bindings / executor (host compiler).
+#pragma once
+#include <hip/hip_runtime_api.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "qmat.h"
+
+namespace omx {
+
+enum { NORM_NONE = 0, NORM_RMS = 1, NORM_LAYER = 2 };
+enum { EPI_STORE = 0, EPI_ADD = 1, EPI_GLU = 2, EPI_GELU = 3, EPI_QKV = 4 };
+
+struct GemvParams {
+  QMat w;
+  int B;                       // activation rows
+  const float* x;              // [B][ldx] fp32
+  int ldx;
+  int norm;                    // NORM_*
+  const float* norm_w;
+  const float* norm_b;
+  float eps;
+  int epi;                     // EPI_*
+  float* y;                    // output / residual (EPI_QKV: q output [B][ldy])
+  int ldy;
+  const float* bias;           // [virtual N] or null
+  int row_offset;              // row index of w's row 0 in the virtual concatenated matrix
+  // EPI_QKV
+  const int* pos;              // [B]
+  const int* slot;             // [B] flat KV slot (block * bs + offset)
+  void* kc;                    // fp16 [nblk][n_kv][bs][D] (this layer)
+  void* vc;
+  const float* inv_freq;       // [n_rot/2]
+  int Eq, Ekv, D, n_rot, n_kv, bs;
+  // MoE: blockIdx.z = k-th selected expert of batch row b
+  const int* expert_ids;       // [B][n_sel] or null
+  const float* expert_w;       // [B][n_sel] routing weights (EPI_ADD scale) or null
+  int n_sel;
+  int x_per_sel;               // x has one row-block per selected expert (down proj)
+  long long x_sel_stride;      // elements between experts' x (within batch row b)
+  long long y_sel_stride;      // elements between experts' y (EPI_GLU output)
+};
+
+void gemv(const GemvParams& P, hipStream_t s);
+
+// Dequantize rows of a repacked matrix (embedding gather / fp16 copies)
+void embed_rows(const QMat& w, const int* rows, int n, float* out, int ldo, hipStream_t s);
+void dequant_f16(const QMat& w, void* out_f16, hipStream_t s);
+
+struct AttnParams {
+  const float* q;              // [NQ][ldq] fp32 (roped)
+  int ldq;
+  const void* kc;              // fp16 [nblk][n_kv][bs][D]
+  const void* vc;
+  const int* block_table;      // [nseq][max_blocks]
+  int max_blocks;
+  const int* q_seq;            // [NQ] sequence row of each query (null -> identity)
+  const int* q_len;            // [NQ] visible keys (= pos + 1)
+  int NQ, H, n_kv, D, bs;
+  float scale;
+  int window;                  // sliding window (0 = none)
+  float* out;                  // [NQ][ldo] fp32
+  int ldo;
+  float* ws;                   // split workspace: [NQ][H][S][D + 2] fp32
+  int n_splits;
+};
+void attention_decode(const AttnParams& P, hipStream_t s);
+size_t attention_ws_floats(int NQ, int H, int D, int n_splits);
+
+struct SampleParams {
+  const float* logits;         // [B][V] (modified in place by penalties)
+  int B, V, ld;
+  const float* temperature;    // [B]
+  const int* top_k;            // [B]
+  const float* top_p;          // [B]
+  const float* min_p;          // [B]
+  const float* repeat_penalty; // [B]
+  const float* presence_penalty;   // [B]
+  const float* frequency_penalty;  // [B]
+  int* history;                // [B][hist_cap] ring of recent tokens
+  int* hist_count;             // [B] tokens seen so far (ring write index)
+  int hist_cap;
+  const int* repeat_last_n;    // [B]
+  const unsigned long long* seed;  // [B]
+  int* step;                   // [B] RNG counter, incremented per sample
+  int* out;                    // [B] sampled token
+  float* out_logprob;          // [B] or null
+};
+void sample(const SampleParams& P, hipStream_t s);
+void argmax(const float* logits, int B, int V, int ld, int* out, hipStream_t s);
+
+void moe_route(const float* logits, int B, int X, int k, int* ids, float* w, hipStream_t s);
+void gather_rows(const float* x, int ld, const int* idx, int rows, int n, float* out, hipStream_t s);
+
+// small elementwise helpers
+void add_inplace(float* y, const float* x, long long n, hipStream_t s);
+void rmsnorm(const float* x, const float* w, float eps, int rows, int n, float* out, hipStream_t s);
+
+}  // namespace omx

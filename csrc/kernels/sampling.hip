@@ -1,0 +1,231 @@
+// On-device token sampling, one 1024-thread block per sequence, so the whole
+// decode step -- forward + sampling + history update -- stays inside one hipGraph replay.
+// Order follows Ollama's (llama.cpp) default chain: repeat/presence/frequency penalties over the
+// last `repeat_last_n` tokens -> top-k -> top-p -> min-p (on T = 1 probabilities) -> temperature
+// -> categorical draw. temperature <= 0 is greedy argmax. Top-k uses a 4-pass 8-bit radix select
+// over order-preserving float keys, then a bitonic sort of the survivors in LDS.
+#include "common.h"
+#include "ops.h"
+
+namespace omx {
+
+constexpr int SAMPLE_NT = 1024;
+constexpr int SAMPLE_CAP = 1024;
+
+__device__ __forceinline__ unsigned fkey(float f) {
+  const unsigned u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+__device__ __forceinline__ unsigned long long splitmix64(unsigned long long x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+__device__ void block_argmax(const float* lg, int V, float* sv, int* si, float& best, int& bi) {
+  float bv = -INFINITY;
+  int bidx = 0x7FFFFFFF;
+  for (int i = threadIdx.x; i < V; i += SAMPLE_NT) {
+    const float v = lg[i];
+    if (v > bv) { bv = v; bidx = i; }
+  }
+  for (int m = 32; m >= 1; m >>= 1) {
+    const float ov = __shfl_xor(bv, m, 64);
+    const int oi = __shfl_xor(bidx, m, 64);
+    if (ov > bv || (ov == bv && oi < bidx)) { bv = ov; bidx = oi; }
+  }
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) { sv[w] = bv; si[w] = bidx; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int k = 1; k < SAMPLE_NT / 64; ++k)
+      if (sv[k] > sv[0] || (sv[k] == sv[0] && si[k] < si[0])) { sv[0] = sv[k]; si[0] = si[k]; }
+  }
+  __syncthreads();
+  best = sv[0];
+  bi = si[0];
+}
+
+__global__ __launch_bounds__(SAMPLE_NT) void sample_kernel(SampleParams P) {
+  __shared__ float cval[SAMPLE_CAP];
+  __shared__ int cidx[SAMPLE_CAP];
+  __shared__ unsigned hist[256];
+  __shared__ float redv[SAMPLE_NT / 64];
+  __shared__ int redi[SAMPLE_NT / 64];
+  __shared__ unsigned s_prefix, s_mask, s_remaining;
+  __shared__ int s_count;
+  const int b = blockIdx.x;
+  float* lg = (float*)P.logits + (long long)b * P.ld;
+  const int V = P.V;
+
+  // ---- penalties over the recent-token window (each distinct token once, with its count)
+  const int seen = P.hist_count[b];
+  int win = min(seen, P.repeat_last_n[b]);
+  win = min(win, P.hist_cap);
+  const float rp = P.repeat_penalty[b], pp = P.presence_penalty[b], fp = P.frequency_penalty[b];
+  if (win > 0 && (rp != 1.f || pp != 0.f || fp != 0.f)) {
+    const int* h = P.history + (long long)b * P.hist_cap;
+    for (int i = threadIdx.x; i < win; i += SAMPLE_NT) {
+      const int tok = h[(seen - 1 - i) % P.hist_cap];
+      bool first = true;
+      int cnt = 1;
+      for (int j = 0; j < win; ++j) {
+        if (j == i) continue;
+        const int o = h[(seen - 1 - j) % P.hist_cap];
+        if (o == tok) {
+          ++cnt;
+          if (j < i) first = false;
+        }
+      }
+      if (first && tok >= 0 && tok < V) {
+        float v = lg[tok];
+        if (rp != 1.f) v = v > 0.f ? v / rp : v * rp;
+        v -= (float)cnt * fp + pp;
+        lg[tok] = v;
+      }
+    }
+    __syncthreads();
+  }
+
+  const float temp = P.temperature[b];
+  int chosen = 0;
+  float chosen_lp = 0.f;
+  if (temp <= 0.f) {
+    float best;
+    block_argmax(lg, V, redv, redi, best, chosen);
+  } else {
+    int k = P.top_k[b];
+    if (k <= 0 || k > SAMPLE_CAP) k = SAMPLE_CAP;
+    if (k > V) k = V;
+    // ---- radix select: key of the k-th largest logit
+    if (threadIdx.x == 0) { s_prefix = 0; s_mask = 0; s_remaining = k; }
+    __syncthreads();
+    for (int pass = 0; pass < 4; ++pass) {
+      const int shift = 24 - 8 * pass;
+      for (int i = threadIdx.x; i < 256; i += SAMPLE_NT) hist[i] = 0;
+      __syncthreads();
+      const unsigned prefix = s_prefix, mask = s_mask;
+      for (int i = threadIdx.x; i < V; i += SAMPLE_NT) {
+        const unsigned key = fkey(lg[i]);
+        if ((key & mask) == prefix) atomicAdd(&hist[(key >> shift) & 0xFF], 1u);
+      }
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        unsigned rem = s_remaining, cum = 0;
+        int bin = 255;
+        for (; bin > 0; --bin) {
+          if (cum + hist[bin] >= rem) break;
+          cum += hist[bin];
+        }
+        s_prefix = prefix | ((unsigned)bin << shift);
+        s_mask = mask | (0xFFu << shift);
+        s_remaining = rem - cum;
+      }
+      __syncthreads();
+    }
+    const unsigned thr = s_prefix;
+    if (threadIdx.x == 0) s_count = 0;
+    __syncthreads();
+    for (int i = threadIdx.x; i < V; i += SAMPLE_NT) {
+      const float v = lg[i];
+      if (fkey(v) >= thr) {
+        const int slot = atomicAdd(&s_count, 1);
+        if (slot < SAMPLE_CAP) { cval[slot] = v; cidx[slot] = i; }
+      }
+    }
+    __syncthreads();
+    const int cnt = min(s_count, SAMPLE_CAP);
+    int n2 = 1;
+    while (n2 < cnt) n2 <<= 1;
+    for (int i = cnt + threadIdx.x; i < n2; i += SAMPLE_NT) { cval[i] = -INFINITY; cidx[i] = 0x7FFFFFFF; }
+    __syncthreads();
+    // bitonic sort, descending by value (ties: lower index first)
+    for (int size = 2; size <= n2; size <<= 1) {
+      for (int stride = size >> 1; stride > 0; stride >>= 1) {
+        for (int i = threadIdx.x; i < n2; i += SAMPLE_NT) {
+          const int j = i ^ stride;
+          if (j > i) {
+            const bool desc = (i & size) == 0;
+            const float a = cval[i], c = cval[j];
+            const int ai = cidx[i], ci = cidx[j];
+            const bool a_first = a > c || (a == c && ai < ci);
+            if (desc != a_first) {
+              cval[i] = c; cval[j] = a; cidx[i] = ci; cidx[j] = ai;
+            }
+          }
+        }
+        __syncthreads();
+      }
+    }
+    if (threadIdx.x == 0) {
+      const int n = min(k, cnt);
+      const float top = cval[0];
+      // T = 1 probabilities for top-p / min-p
+      float z = 0.f;
+      for (int i = 0; i < n; ++i) z += __expf(cval[i] - top);
+      const float topp = P.top_p[b], minp = P.min_p[b];
+      int keep = n;
+      if (topp < 1.f) {
+        float c = 0.f;
+        for (int i = 0; i < n; ++i) {
+          c += __expf(cval[i] - top) / z;
+          if (c >= topp) { keep = i + 1; break; }
+        }
+      }
+      if (minp > 0.f) {
+        int j = 1;
+        while (j < keep && __expf(cval[j] - top) >= minp) ++j;
+        keep = j;
+      }
+      // temperature, then draw
+      float zt = 0.f;
+      for (int i = 0; i < keep; ++i) zt += __expf((cval[i] - top) / temp);
+      const unsigned long long r = splitmix64(P.seed[b] ^ (0xD1B54A32D192ED03ull * (unsigned long long)(P.step[b] + 1)));
+      const float u = (float)(r >> 40) * (1.0f / 16777216.0f) * zt;
+      float c = 0.f;
+      int pick = keep - 1;
+      for (int i = 0; i < keep; ++i) {
+        c += __expf((cval[i] - top) / temp);
+        if (u < c) { pick = i; break; }
+      }
+      chosen = cidx[pick];
+      chosen_lp = (cval[pick] - top) / temp - __logf(zt);
+      redi[0] = chosen;
+      redv[0] = chosen_lp;
+    }
+    __syncthreads();
+    chosen = redi[0];
+    chosen_lp = redv[0];
+  }
+  if (threadIdx.x == 0) {
+    P.out[b] = chosen;
+    if (P.out_logprob) P.out_logprob[b] = chosen_lp;
+    P.history[(long long)b * P.hist_cap + (seen % P.hist_cap)] = chosen;
+    P.hist_count[b] = seen + 1;
+    P.step[b] += 1;
+  }
+}
+
+void sample(const SampleParams& P, hipStream_t s) {
+  if (P.B <= 0) return;
+  hipLaunchKernelGGL(sample_kernel, dim3(P.B), dim3(SAMPLE_NT), 0, s, P);
+}
+
+__global__ __launch_bounds__(SAMPLE_NT) void argmax_kernel(const float* logits, int V, int ld, int* out) {
+  __shared__ float sv[SAMPLE_NT / 64];
+  __shared__ int si[SAMPLE_NT / 64];
+  float best;
+  int bi;
+  block_argmax(logits + (long long)blockIdx.x * ld, V, sv, si, best, bi);
+  if (threadIdx.x == 0) out[blockIdx.x] = bi;
+}
+
+void argmax(const float* logits, int B, int V, int ld, int* out, hipStream_t s) {
+  if (B <= 0) return;
+  hipLaunchKernelGGL(argmax_kernel, dim3(B), dim3(SAMPLE_NT), 0, s, logits, V, ld, out);
+}
+
+}  // namespace omx

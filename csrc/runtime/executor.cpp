@@ -1,0 +1,198 @@
+#include "executor.h"
+
+#include <cmath>
+#include <stdexcept>
+
+namespace omx {
+
+static GemvParams base_params(const QMat& w, int B, const float* x, int ldx) {
+  GemvParams P{};
+  P.w = w;
+  P.B = B;
+  P.x = x;
+  P.ldx = ldx;
+  P.eps = 1e-5f;
+  P.n_sel = 1;
+  return P;
+}
+
+void Executor::embed(const StepInputs& in, hipStream_t s) {
+  embed_rows(tok_embd, in.tokens, in.B, ws.resid, cfg.E, s);
+}
+
+void Executor::attn_block(int i, const StepInputs& in, hipStream_t s) {
+  const LayerW& L = layers[i];
+  const int B = in.B, E = cfg.E, Eq = cfg.H * cfg.D, Ekv = cfg.Hkv * cfg.D;
+  const bool phi = cfg.arch == 1;
+  // --- QKV projection: fused norm prologue, RoPE + paged K/V scatter epilogue
+  GemvParams P = base_params(L.wqk, B, ws.resid, E);
+  P.norm = phi ? NORM_LAYER : NORM_RMS;
+  P.norm_w = L.attn_norm;
+  P.norm_b = L.attn_norm_b;
+  P.eps = cfg.eps;
+  P.epi = EPI_QKV;
+  P.y = ws.qbuf;
+  P.ldy = Eq;
+  P.bias = L.qkv_bias;
+  P.pos = in.pos;
+  P.slot = in.slot;
+  P.kc = L.kc;
+  P.vc = L.vc;
+  P.inv_freq = inv_freq;
+  P.Eq = Eq;
+  P.Ekv = Ekv;
+  P.D = cfg.D;
+  P.n_rot = cfg.n_rot;
+  P.n_kv = cfg.Hkv;
+  P.bs = in.bs;
+  gemv(P, s);
+  if (!L.qkv_fused) {
+    GemvParams V = P;
+    V.w = L.wv;
+    V.row_offset = Eq + Ekv;
+    gemv(V, s);
+  }
+  if (phi) {  // parallel block: FFN up reads the same normed input, before O touches resid
+    GemvParams U = base_params(L.wgu, B, ws.resid, E);
+    U.norm = NORM_LAYER;
+    U.norm_w = L.attn_norm;
+    U.norm_b = L.attn_norm_b;
+    U.eps = cfg.eps;
+    U.epi = EPI_GELU;
+    U.bias = L.bup;
+    U.y = ws.hbuf;
+    U.ldy = cfg.F;
+    gemv(U, s);
+  }
+  // --- attention over the paged cache
+  AttnParams A{};
+  A.q = ws.qbuf;
+  A.ldq = Eq;
+  A.kc = L.kc;
+  A.vc = L.vc;
+  A.block_table = in.block_table;
+  A.max_blocks = in.max_blocks;
+  A.q_seq = in.q_seq;
+  A.q_len = in.q_len;
+  A.NQ = B;
+  A.H = cfg.H;
+  A.n_kv = cfg.Hkv;
+  A.D = cfg.D;
+  A.bs = in.bs;
+  A.scale = 1.0f / std::sqrt((float)cfg.D);
+  A.window = cfg.window;
+  A.out = ws.abuf;
+  A.ldo = Eq;
+  A.ws = ws.attn_ws;
+  A.n_splits = ws.n_splits;
+  attention_decode(A, s);
+  // --- output projection (+ residual, or partial sum under TP)
+  GemvParams O = base_params(L.wo, B, ws.abuf, Eq);
+  O.bias = L.bo;
+  if (cfg.tp > 1) {
+    O.epi = EPI_STORE;
+    O.y = ws.ypart;
+  } else {
+    O.epi = EPI_ADD;
+    O.y = ws.resid;
+  }
+  O.ldy = E;
+  gemv(O, s);
+}
+
+void Executor::ffn_block(int i, const StepInputs& in, hipStream_t s) {
+  const LayerW& L = layers[i];
+  const int B = in.B, E = cfg.E, F = cfg.F;
+  float* dst = cfg.tp > 1 ? ws.ypart : ws.resid;
+  const int dst_epi = cfg.tp > 1 ? EPI_STORE : EPI_ADD;
+  if (cfg.arch == 1) {  // phi2: up+GELU already done in attn_block
+    GemvParams Dn = base_params(L.wdown, B, ws.hbuf, F);
+    Dn.epi = dst_epi;
+    Dn.bias = L.bdown;
+    Dn.y = dst;
+    Dn.ldy = E;
+    gemv(Dn, s);
+    return;
+  }
+  if (cfg.n_expert > 0) {
+    const int X = cfg.n_expert, k = cfg.n_expert_used;
+    GemvParams R = base_params(L.router, B, ws.resid, E);
+    R.norm = NORM_RMS;
+    R.norm_w = L.ffn_norm;
+    R.eps = cfg.eps;
+    R.epi = EPI_STORE;
+    R.y = ws.rlogits;
+    R.ldy = X;
+    gemv(R, s);
+    moe_route(ws.rlogits, B, X, k, ws.eids, ws.ew, s);
+    GemvParams G = base_params(L.gu_exps, B, ws.resid, E);
+    G.norm = NORM_RMS;
+    G.norm_w = L.ffn_norm;
+    G.eps = cfg.eps;
+    G.epi = EPI_GLU;
+    G.y = ws.hbuf;
+    G.ldy = k * F;
+    G.expert_ids = ws.eids;
+    G.n_sel = k;
+    G.y_sel_stride = F;
+    gemv(G, s);
+    if (cfg.tp > 1) hipMemsetAsync(ws.ypart, 0, sizeof(float) * (size_t)B * E, s);
+    GemvParams Dn = base_params(L.down_exps, B, ws.hbuf, k * F);
+    Dn.epi = EPI_ADD;  // expert-weighted, atomically accumulated
+    Dn.y = dst;
+    Dn.ldy = E;
+    Dn.expert_ids = ws.eids;
+    Dn.expert_w = ws.ew;
+    Dn.n_sel = k;
+    Dn.x_per_sel = 1;
+    Dn.x_sel_stride = F;
+    gemv(Dn, s);
+    return;
+  }
+  GemvParams G = base_params(L.wgu, B, ws.resid, E);
+  G.norm = NORM_RMS;
+  G.norm_w = L.ffn_norm;
+  G.eps = cfg.eps;
+  G.epi = EPI_GLU;
+  G.y = ws.hbuf;
+  G.ldy = F;
+  gemv(G, s);
+  GemvParams Dn = base_params(L.wdown, B, ws.hbuf, F);
+  Dn.epi = dst_epi;
+  Dn.y = dst;
+  Dn.ldy = E;
+  gemv(Dn, s);
+}
+
+void Executor::head(const StepInputs& in, hipStream_t s) {
+  const int E = cfg.E;
+  const float* x = ws.resid;
+  if (in.n_logits <= 0) return;
+  if (in.logit_idx) {
+    gather_rows(ws.resid, E, in.logit_idx, in.n_logits, E, ws.lbuf, s);
+    x = ws.lbuf;
+  }
+  GemvParams P = base_params(lm_head, in.n_logits, x, E);
+  P.norm = cfg.arch == 1 ? NORM_LAYER : NORM_RMS;
+  P.norm_w = out_norm;
+  P.norm_b = out_norm_b;
+  P.eps = cfg.eps;
+  P.epi = EPI_STORE;
+  P.bias = lm_bias;
+  P.y = in.logits;
+  P.ldy = lm_head.N;
+  gemv(P, s);
+}
+
+void Executor::forward(const StepInputs& in, hipStream_t s) {
+  if (cfg.tp != 1) throw std::runtime_error("Executor::forward is the TP=1 path; TP steps are driven per block");
+  if (in.B > ws.max_B) throw std::runtime_error("batch exceeds workspace");
+  embed(in, s);
+  for (int i = 0; i < cfg.n_layer; ++i) {
+    attn_block(i, in, s);
+    ffn_block(i, in, s);
+  }
+  head(in, s);
+}
+
+}  // namespace omx

@@ -1,0 +1,94 @@
+// Native step executor: the per-token launch sequence of a transformer on gfx950 kernels.
+// Python owns the device memory (torch tensors) and hands raw pointers in; the executor only
+// enqueues kernels on a stream, so a whole step is capturable into one hipGraph.
+// Reference parity: replaces the llama.cpp runner inside `ollama/ollama` (reference
+// pkg/model/pod.go:10-12; SURVEY.md §3.4 hot loop).
+#pragma once
+#include <hip/hip_runtime_api.h>
+
+#include <vector>
+
+#include "../kernels/ops.h"
+
+namespace omx {
+
+struct ExecConfig {
+  int arch = 0;          // 0 llama-family (llama/mistral/mixtral), 1 phi2
+  int E = 0, H = 0, Hkv = 0, D = 0, n_rot = 0, F = 0, n_layer = 0, V = 0;  // per-rank (TP) sizes
+  float eps = 1e-5f;
+  int n_expert = 0, n_expert_used = 0;
+  int window = 0;
+  int tp = 1;            // >1: O/down projections write partial sums to ypart (caller all-reduces)
+};
+
+struct LayerW {
+  const float* attn_norm = nullptr;
+  const float* attn_norm_b = nullptr;
+  const float* ffn_norm = nullptr;
+  QMat wqk{};            // q,k rows (and v rows too when qkv_fused)
+  QMat wv{};             // v rows when not fused (different quant type)
+  int qkv_fused = 1;
+  const float* qkv_bias = nullptr;
+  QMat wo{};
+  const float* bo = nullptr;
+  QMat wgu{};            // llama: gate/up rows interleaved; phi2: up
+  const float* bup = nullptr;
+  QMat wdown{};
+  const float* bdown = nullptr;
+  QMat router{};         // MoE router [X][E]
+  QMat gu_exps{};        // [X][2F][E] interleaved gate/up per expert
+  QMat down_exps{};      // [X][E][F]
+  void* kc = nullptr;    // fp16 [nblk][Hkv][bs][D]
+  void* vc = nullptr;
+};
+
+struct Workspace {
+  float* resid = nullptr;    // [maxB][E]
+  float* qbuf = nullptr;     // [maxB][H*D]
+  float* abuf = nullptr;     // [maxB][H*D]
+  float* hbuf = nullptr;     // [maxB][n_sel][F]
+  float* ypart = nullptr;    // [maxB][E] (TP partial sums)
+  float* lbuf = nullptr;     // [maxB][E] gathered rows for the LM head
+  float* rlogits = nullptr;  // [maxB][X]
+  int* eids = nullptr;       // [maxB][n_sel]
+  float* ew = nullptr;       // [maxB][n_sel]
+  float* attn_ws = nullptr;  // split-K workspace
+  int max_B = 0;
+  int n_splits = 1;
+};
+
+struct StepInputs {
+  int B = 0;
+  const int* tokens = nullptr;    // [B]
+  const int* pos = nullptr;       // [B]
+  const int* slot = nullptr;      // [B]
+  const int* q_len = nullptr;     // [B] = pos + 1
+  const int* q_seq = nullptr;     // [B] row of block_table
+  const int* block_table = nullptr;
+  int max_blocks = 0;
+  int bs = 16;
+  int n_logits = 0;               // rows that need logits
+  const int* logit_idx = nullptr; // [n_logits] (null = first n_logits rows)
+  float* logits = nullptr;        // [n_logits][V]
+};
+
+class Executor {
+ public:
+  ExecConfig cfg;
+  std::vector<LayerW> layers;
+  QMat tok_embd{};
+  const float* out_norm = nullptr;
+  const float* out_norm_b = nullptr;
+  QMat lm_head{};
+  const float* lm_bias = nullptr;
+  const float* inv_freq = nullptr;
+  Workspace ws;
+
+  void embed(const StepInputs& in, hipStream_t s);
+  void attn_block(int i, const StepInputs& in, hipStream_t s);
+  void ffn_block(int i, const StepInputs& in, hipStream_t s);
+  void head(const StepInputs& in, hipStream_t s);
+  void forward(const StepInputs& in, hipStream_t s);  // tp == 1 only
+};
+
+}  // namespace omx

@@ -1,0 +1,364 @@
+"""Model runner: weights + paged KV cache + step buffers + executor + sampler + hipGraph decode.
+
+One `Runner` serves one model on one device (one TP rank). The executor is the native gfx950 one
+(`_C.Executor`, csrc/runtime/executor.cpp) on a GPU and the torch twin (`ops.reference`) on CPU;
+both read the same buffers, so prefill/decode/batching logic is shared and tested on CPU.
+
+Decode is captured once per batch size into a hipGraph (torch.cuda.CUDAGraph): forward over all
+layers + on-device sampling + feeding the sampled token back as the next input. The host only
+uploads (pos, slot, q_len) for the next step from a pinned ring and reads the sampled token one
+step behind, so the GPU never waits on Python.
+"""
+from __future__ import annotations
+
+import math
+import os
+import time
+from dataclasses import dataclass
+from typing import Callable, Iterator
+
+import numpy as np
+import torch
+
+from ..ops import has_native, native, stream_handle
+from ..ops.reference import TorchExecutor
+from .kv_cache import PagedKV
+from .sampling import SamplingOptions, sample_host
+from .weights import DeviceWeights
+
+HIST_CAP = 256
+
+
+class NativeExec:
+    """Adapter: runner buffers -> `_C.Executor`."""
+
+    def __init__(self, runner: "Runner"):
+        C = native()
+        r = runner
+        w, loc, cfg = r.w, r.w.local, r.w.cfg
+        self.r = r
+        self.exe = e = C.Executor()
+        e.configure(dict(arch=1 if cfg.arch == "phi2" else 0, E=loc["E"], H=loc["H"], Hkv=loc["Hkv"], D=loc["D"],
+                         n_rot=cfg.n_rot, F=loc["F"], n_layer=cfg.n_layer, V=loc["V"], eps=float(cfg.norm_eps),
+                         n_expert=cfg.n_expert, n_expert_used=cfg.n_expert_used, window=cfg.sliding_window,
+                         tp=r.tp_size))
+        p = lambda t: t.data_ptr() if t is not None else 0  # noqa: E731
+        e.set_globals(w.tok_embd.tup, p(w.out_norm), p(w.out_norm_b), w.lm_head.tup, p(w.lm_bias), p(w.inv_freq))
+        for i, L in enumerate(w.layers):
+            d = {}
+            for k, v in L.items():
+                if v is None:
+                    continue
+                d[k] = v.tup if hasattr(v, "tup") else v.data_ptr()
+            d["kc"] = r.kc[i].data_ptr()
+            d["vc"] = r.vc[i].data_ptr()
+            e.set_layer(i, d)
+        e.set_workspace(dict(resid=p(r.resid), qbuf=p(r.qbuf), abuf=p(r.abuf), hbuf=p(r.hbuf), ypart=p(r.ypart),
+                             lbuf=p(r.lbuf), rlogits=p(r.rlogits), eids=p(r.eids), ew=p(r.ew),
+                             attn_ws=p(r.attn_ws), max_B=r.max_batch, n_splits=1))
+        self.inputs = dict(tokens=p(r.d_tokens), pos=p(r.d_pos), slot=p(r.d_slot), q_len=p(r.d_qlen),
+                           q_seq=p(r.d_qseq), block_table=p(r.d_block_table), max_blocks=r.max_blocks,
+                           bs=r.block_size, logits=p(r.logits))
+        self.logit_idx_ptr = p(r.d_logit_idx)
+
+    def run(self, stage: str, layer: int, B: int, n_logits: int = 0, use_idx: bool = False):
+        d = dict(self.inputs)
+        d["B"] = B
+        d["n_logits"] = n_logits
+        d["logit_idx"] = self.logit_idx_ptr if use_idx else 0
+        self.exe.set_splits(self.r.n_splits(B))
+        self.exe.run(stage, layer, d, stream_handle())
+
+
+@dataclass
+class StepTimes:
+    prompt_tokens: int = 0
+    prompt_s: float = 0.0
+    gen_tokens: int = 0
+    gen_s: float = 0.0
+    load_s: float = 0.0
+
+
+class Runner:
+    def __init__(self, model_path: str, device: str | None = None, max_batch: int = 64, max_seqs: int = 4,
+                 ctx: int | None = None, block_size: int = 16, tp_rank: int = 0, tp_size: int = 1,
+                 tp_group=None, use_graphs: bool | None = None, weights: DeviceWeights | None = None):
+        t0 = time.perf_counter()
+        if device is None:
+            device = f"cuda:{torch.cuda.current_device()}" if torch.cuda.is_available() else "cpu"
+        self.device = torch.device(device)
+        self.is_gpu = self.device.type == "cuda"
+        if self.is_gpu:
+            native()  # fail loudly: no silent torch fallback on a GPU box
+        self.tp_rank, self.tp_size, self.tp_group = tp_rank, tp_size, tp_group
+        self.w = weights or DeviceWeights(model_path, self.device, tp_rank, tp_size)
+        cfg = self.cfg = self.w.cfg
+        loc = self.w.local
+        self.max_batch = max_batch
+        self.block_size = block_size
+        self.ctx = min(ctx or cfg.ctx_len, cfg.ctx_len)
+        self.max_blocks = (self.ctx + block_size - 1) // block_size
+        n_blocks = max_seqs * self.max_blocks
+        dev = self.device
+        f32 = dict(device=dev, dtype=torch.float32)
+        i32 = dict(device=dev, dtype=torch.int32)
+        E, Eq, Fl, Vl = loc["E"], loc["H"] * loc["D"], loc["F"], loc["V"]
+        ksel = max(1, cfg.n_expert_used)
+        self.kc = [torch.zeros(n_blocks, loc["Hkv"], block_size, loc["D"], device=dev, dtype=torch.float16)
+                   for _ in range(cfg.n_layer)]
+        self.vc = [torch.zeros_like(k) for k in self.kc]
+        self.resid = torch.zeros(max_batch, E, **f32)
+        self.qbuf = torch.zeros(max_batch, Eq, **f32)
+        self.abuf = torch.zeros(max_batch, Eq, **f32)
+        self.hbuf = torch.zeros(max_batch, ksel * Fl, **f32)
+        self.ypart = torch.zeros(max_batch, E, **f32)
+        self.lbuf = torch.zeros(max_batch, E, **f32)
+        self.rlogits = torch.zeros(max_batch, max(1, cfg.n_expert), **f32)
+        self.eids = torch.zeros(max_batch, ksel, **i32)
+        self.ew = torch.zeros(max_batch, ksel, **f32)
+        ws = max(self._ws_floats(B) for B in range(1, max_batch + 1))
+        self.attn_ws = torch.zeros(max(ws, 1), **f32)
+        self.logits = torch.zeros(max_batch, Vl, **f32)
+        self.full_logits = torch.zeros(max_batch, cfg.n_vocab, **f32) if tp_size > 1 else self.logits
+        # step inputs, packed so one H2D copy refreshes (pos, slot, q_len, q_seq, logit_idx)
+        self.d_step = torch.zeros(6, max_batch, **i32)
+        self.d_pos, self.d_slot, self.d_qlen, self.d_qseq, self.d_logit_idx, self.d_tokens = self.d_step.unbind(0)
+        self.d_block_table = torch.zeros(max_seqs, self.max_blocks, **i32)
+        # sampler state (indexed by batch row)
+        self.s_temp = torch.zeros(max_batch, **f32)
+        self.s_topk = torch.zeros(max_batch, **i32)
+        self.s_topp = torch.ones(max_batch, **f32)
+        self.s_minp = torch.zeros(max_batch, **f32)
+        self.s_rpen = torch.ones(max_batch, **f32)
+        self.s_ppen = torch.zeros(max_batch, **f32)
+        self.s_fpen = torch.zeros(max_batch, **f32)
+        self.s_lastn = torch.zeros(max_batch, **i32)
+        self.s_seed = torch.zeros(max_batch, device=dev, dtype=torch.int64)
+        self.s_step = torch.zeros(max_batch, **i32)
+        self.s_hist = torch.zeros(max_batch, HIST_CAP, **i32)
+        self.s_hcount = torch.zeros(max_batch, **i32)
+        self.s_out = torch.zeros(max_batch, **i32)
+        self.kv = PagedKV(n_blocks, block_size, max_seqs, self.max_blocks)
+        self.exe = NativeExec(self) if self.is_gpu else TorchExecutor(self)
+        if use_graphs is None:
+            use_graphs = self.is_gpu and os.environ.get("OMX_NO_GRAPH", "0") != "1"
+        self.use_graphs = use_graphs
+        self.graphs: dict[int, torch.cuda.CUDAGraph] = {}
+        self._host_sampler: dict[int, tuple] = {}
+        self._pinned = None
+        if self.is_gpu:
+            self._pinned = [torch.zeros(5, max_batch, dtype=torch.int32).pin_memory() for _ in range(4)]
+            self._pin_i = 0
+            self._tok_host = torch.zeros(max_batch, dtype=torch.int32).pin_memory()
+        self.load_s = time.perf_counter() - t0
+
+    # ------------------------------------------------------------------ sizing helpers
+    def n_splits(self, B: int) -> int:
+        hkv = self.w.local["Hkv"]
+        return max(1, min(32, 512 // max(1, B * hkv)))
+
+    def _ws_floats(self, B: int) -> int:
+        loc = self.w.local
+        S = self.n_splits(B)
+        return B * loc["H"] * S * (loc["D"] + 2) if S > 1 else 0
+
+    # ------------------------------------------------------------------ forward
+    def _all_reduce_add(self, B: int):
+        import torch.distributed as dist
+        dist.all_reduce(self.ypart[:B], group=self.tp_group)
+        self.resid[:B] += self.ypart[:B]
+
+    def forward(self, B: int, n_logits: int, use_idx: bool = False):
+        if self.tp_size == 1:
+            self.exe.run("forward", 0, B, n_logits, use_idx)
+            return
+        import torch.distributed as dist
+        self.exe.run("embed", 0, B)
+        for i in range(self.cfg.n_layer):
+            self.exe.run("attn", i, B)
+            self._all_reduce_add(B)
+            self.exe.run("ffn", i, B)
+            self._all_reduce_add(B)
+        self.exe.run("head", 0, B, n_logits, use_idx)
+        if n_logits:
+            parts = [torch.empty_like(self.logits[:n_logits]) for _ in range(self.tp_size)]
+            dist.all_gather(parts, self.logits[:n_logits].contiguous(), group=self.tp_group)
+            self.full_logits[:n_logits] = torch.cat(parts, dim=1)
+
+    # ------------------------------------------------------------------ inputs
+    def _upload(self, arr: np.ndarray, tokens: np.ndarray | None):
+        """arr: int32 [5, B] = (pos, slot, qlen, qseq, logit_idx)."""
+        B = arr.shape[1]
+        if self.is_gpu:
+            buf = self._pinned[self._pin_i]
+            self._pin_i = (self._pin_i + 1) % len(self._pinned)
+            buf[:, :B] = torch.from_numpy(arr)
+            self.d_step[:5, :B].copy_(buf[:, :B], non_blocking=True)
+            if tokens is not None:
+                self.d_tokens[:len(tokens)].copy_(torch.from_numpy(tokens.astype(np.int32)), non_blocking=False)
+        else:
+            self.d_step[:5, :B] = torch.from_numpy(arr)
+            if tokens is not None:
+                self.d_tokens[:len(tokens)] = torch.from_numpy(tokens.astype(np.int32))
+
+    def _sync_block_table(self, sid: int):
+        s = self.kv.seqs[sid]
+        row = torch.tensor(s.blocks, dtype=torch.int32)
+        self.d_block_table[s.row, :len(s.blocks)].copy_(row.to(self.device))
+
+    # ------------------------------------------------------------------ sequences
+    def new_sequence(self) -> int:
+        return self.kv.new_seq()
+
+    def free_sequence(self, sid: int) -> None:
+        self.kv.free_seq(sid)
+
+    def prefill(self, sid: int, tokens: list[int], want_logits: bool = True) -> None:
+        """Append `tokens` to sequence `sid` (KV computed), leaving logits of the last one in row 0."""
+        s = self.kv.seqs[sid]
+        start = s.length
+        n = len(tokens)
+        if start + n > self.ctx:
+            raise ValueError(f"context overflow: {start + n} > {self.ctx}")
+        self.kv.reserve(sid, start + n)
+        self._sync_block_table(sid)
+        C = self.max_batch
+        for c0 in range(0, n, C):
+            chunk = tokens[c0:c0 + C]
+            B = len(chunk)
+            pos = np.arange(start + c0, start + c0 + B, dtype=np.int32)
+            slots = np.array([self.kv.slot(sid, int(p)) for p in pos], np.int32)
+            last = c0 + B >= n
+            arr = np.stack([pos, slots, pos + 1, np.full(B, s.row, np.int32),
+                            np.full(B, B - 1, np.int32)]).astype(np.int32)
+            self._upload(arr, np.asarray(chunk, np.int32))
+            self.forward(B, 1 if (last and want_logits) else 0, use_idx=True)
+        s.tokens.extend(tokens)
+
+    # ------------------------------------------------------------------ sampling
+    def _set_sampler(self, row: int, o: SamplingOptions, history: list[int], seed: int):
+        self.s_temp[row] = o.temperature
+        self.s_topk[row] = o.top_k
+        self.s_topp[row] = o.top_p
+        self.s_minp[row] = o.min_p
+        self.s_rpen[row] = o.repeat_penalty
+        self.s_ppen[row] = o.presence_penalty
+        self.s_fpen[row] = o.frequency_penalty
+        self.s_lastn[row] = o.repeat_last_n
+        self.s_seed[row] = seed - (1 << 64) if seed >= (1 << 63) else seed
+        self.s_step[row] = 0
+        h = history[-HIST_CAP:]
+        self.s_hist[row].zero_()
+        if h:
+            self.s_hist[row, :len(h)] = torch.tensor(h, dtype=torch.int32)
+        self.s_hcount[row] = len(h)
+        self._host_sampler[row] = (o, list(history), seed, 0)
+
+    def _sample(self, B: int):
+        lg = self.full_logits
+        if self.is_gpu:
+            p = lambda t: t.data_ptr()  # noqa: E731
+            native().sample(dict(logits=p(lg), B=B, V=self.cfg.n_vocab, ld=lg.shape[1], temperature=p(self.s_temp),
+                                 top_k=p(self.s_topk), top_p=p(self.s_topp), min_p=p(self.s_minp),
+                                 repeat_penalty=p(self.s_rpen), presence_penalty=p(self.s_ppen),
+                                 frequency_penalty=p(self.s_fpen), history=p(self.s_hist),
+                                 hist_count=p(self.s_hcount), hist_cap=HIST_CAP, repeat_last_n=p(self.s_lastn),
+                                 seed=p(self.s_seed), step=p(self.s_step), out=p(self.s_out)), stream_handle())
+        else:
+            for b in range(B):
+                o, hist, seed, step = self._host_sampler[b]
+                t = sample_host(lg[b, :self.cfg.n_vocab].numpy(), hist, o, seed, step)
+                hist.append(t)
+                self._host_sampler[b] = (o, hist, seed, step + 1)
+                self.s_out[b] = t
+
+    # ------------------------------------------------------------------ decode
+    def _decode_body(self, B: int):
+        self.forward(B, B, use_idx=False)
+        self._sample(B)
+        self.d_tokens[:B].copy_(self.s_out[:B])
+
+    def _graph(self, B: int):
+        g = self.graphs.get(B)
+        if g is None:
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                # warm-up on the capture stream (first launches load code objects)
+                self.forward(B, B, use_idx=False)
+            torch.cuda.current_stream().wait_stream(s)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._decode_body(B)
+            self.graphs[B] = g
+        return g
+
+    def decode_step(self, sid: int) -> None:
+        """One token for sequence `sid` whose input token (not yet in `tokens`) is already in
+        d_tokens[0] on device; it sits at position len(tokens)."""
+        s = self.kv.seqs[sid]
+        pos = s.length
+        if pos + 1 > len(s.blocks) * self.block_size:
+            self.kv.reserve(sid, min(self.ctx, pos + 4 * self.block_size))
+            self._sync_block_table(sid)
+        arr = np.array([[pos], [self.kv.slot(sid, pos)], [pos + 1], [s.row], [0]], np.int32)
+        self._upload(arr, None)
+        if self.use_graphs:
+            self._graph(1).replay()
+        else:
+            self._decode_body(1)
+
+    def generate(self, sid: int, prompt: list[int], options: SamplingOptions | None = None,
+                 max_tokens: int = 128, stop: Callable[[int], bool] | None = None,
+                 times: StepTimes | None = None) -> Iterator[int]:
+        """Stream sampled tokens. Reuses the KV prefix shared with what `sid` already holds."""
+        o = options or SamplingOptions()
+        seed = o.resolved_seed()
+        st = self.kv.seqs[sid]
+        keep = self.kv.common_prefix(st.tokens, prompt)
+        keep = min(keep, len(prompt) - 1)
+        self.kv.truncate(sid, keep)
+        t0 = time.perf_counter()
+        self.prefill(sid, prompt[keep:])
+        self._set_sampler(0, o, prompt, seed)
+        self._sample(1)
+        if self.is_gpu:
+            self.d_tokens[:1].copy_(self.s_out[:1])
+            self._tok_host[:1].copy_(self.s_out[:1], non_blocking=True)
+            torch.cuda.synchronize()
+            first = int(self._tok_host[0])
+        else:
+            first = int(self.s_out[0])
+            self.d_tokens[0] = first
+        if times is not None:
+            times.prompt_tokens = len(prompt) - keep
+            times.prompt_s = time.perf_counter() - t0
+        t1 = time.perf_counter()
+        n = 0
+        tok = first
+        max_tokens = min(max_tokens, self.ctx - st.length)
+        try:
+            while True:
+                n += 1
+                done = n >= max_tokens or (stop is not None and stop(tok))
+                if not done:
+                    # enqueue the next step before handing this token out: the GPU runs one step
+                    # ahead of the host (detokenize / stream / stop checks overlap the forward)
+                    self.decode_step(sid)
+                    if self.is_gpu:
+                        self._tok_host[:1].copy_(self.s_out[:1], non_blocking=True)
+                        ev = torch.cuda.Event()
+                        ev.record()
+                    st.tokens.append(tok)  # its KV is being written by the step just issued
+                yield tok
+                if done:
+                    break
+                if self.is_gpu:
+                    ev.synchronize()
+                    tok = int(self._tok_host[0])
+                else:
+                    tok = int(self.s_out[0])
+        finally:
+            if times is not None:
+                times.gen_tokens = n
+                times.gen_s = time.perf_counter() - t1

@@ -1,0 +1,260 @@
+"""Device weight loader: GGUF -> repacked quant streams in HBM.
+
+Every projection is uploaded as a `DevQMat` (csrc/kernels/qmat.h) laid out for the fused GEMV:
+  * q/k/v rows concatenated into one matrix when they share a quant type (one QKV launch);
+  * phi2 q/k rows re-ordered inside each head so NEOX rotary pairs (i, i + n_rot/2) become
+    adjacent rows (the GEMV epilogue only rotates adjacent pairs) -- q.k dot products unchanged;
+  * gate/up rows interleaved (row 2j = gate j, 2j+1 = up j) so SiLU-GLU fuses into the epilogue;
+  * tensor-parallel shards cut on head / row / 256-weight-block boundaries;
+  * MoE experts stacked [X][N][K] so the kernel offsets to the routed expert on device.
+Types without a native kernel (Q4_1/Q5_x/F16/BF16/F32 projections) are requantised to Q8_0 at
+load -- documented precision upgrade for those files, never a silent fallback.
+Host staging goes through the native repack (`_C.GGUFMap.repack`, multi-threaded over the mmap).
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from ..gguf import GGMLType, read_gguf
+from ..gguf.constants import BLOCK_GEOMETRY
+from ..models.config import ROPE_NEOX, ModelConfig
+from ..quant import dequantize, quantize
+from ..ops import has_native, native
+
+NATIVE_QTYPES = (GGMLType.Q4_0, GGMLType.Q8_0, GGMLType.Q4_K, GGMLType.Q6_K)
+
+
+def stream_bytes(qtype: int, K: int) -> list[int]:
+    q = GGMLType(qtype)
+    if q == GGMLType.Q4_K:
+        return [K // 2, K // 16]
+    if q == GGMLType.Q6_K:
+        return [K // 2, K // 4, K // 16, K // 128]
+    if q == GGMLType.Q4_0:
+        return [K // 2, K // 16]
+    if q == GGMLType.Q8_0:
+        return [K, K // 16]
+    raise ValueError(f"no device layout for {q.name}")
+
+
+@dataclass
+class DevQMat:
+    qtype: int
+    N: int
+    K: int
+    streams: list[torch.Tensor] = field(default_factory=list)
+
+    @property
+    def tup(self) -> tuple:
+        p = [s.data_ptr() for s in self.streams] + [0] * (4 - len(self.streams))
+        return (p[0], p[1], p[2], p[3], self.N, self.K, int(self.qtype))
+
+    @property
+    def nbytes(self) -> int:
+        return sum(s.numel() for s in self.streams)
+
+
+def _np_repack_rows(src: np.ndarray, qtype: int, K_src: int, rows: np.ndarray, dst_rows: np.ndarray,
+                    kb0: int, kb1: int, dst: list[np.ndarray]) -> None:
+    """numpy twin of csrc/gguf/gguf.cpp repack_rows (CPU-only environments / tests)."""
+    from ..quant import repack
+    blk, nb = BLOCK_GEOMETRY[GGMLType(qtype)]
+    b = src.reshape(-1, K_src // blk, nb)[rows][:, kb0:kb1]
+    K = (kb1 - kb0) * blk
+    st = repack(b.reshape(-1), qtype, len(rows), K)
+    names = {GGMLType.Q4_K: ["qs", "meta"], GGMLType.Q6_K: ["ql", "qh", "sc", "d"],
+             GGMLType.Q4_0: ["qs", "d"], GGMLType.Q8_0: ["qs", "d"]}[GGMLType(qtype)]
+    for i, n in enumerate(names):
+        dst[i].reshape(-1, st[n].shape[1])[dst_rows] = st[n]
+
+
+class WeightSource:
+    """Reads tensors from a GGUF file (native mmap + repack when built, numpy otherwise)."""
+
+    def __init__(self, path: str):
+        self.path = path
+        self.g = read_gguf(path)
+        self.cfg = ModelConfig.from_gguf_metadata(self.g.metadata)
+        self.nat = native().GGUFMap(path) if has_native() else None
+        self.threads = min(16, os.cpu_count() or 4)
+        self._requant: dict[str, np.ndarray] = {}
+
+    def info(self, name: str):
+        return self.g.tensors[name]
+
+    def has(self, name: str) -> bool:
+        return name in self.g.tensors
+
+    def f32(self, name: str) -> np.ndarray:
+        return np.ascontiguousarray(self.g.array(name), dtype=np.float32).reshape(-1)
+
+    def qtype_of(self, name: str) -> int:
+        t = self.info(name).ggml_type
+        return int(t) if t in NATIVE_QTYPES else int(GGMLType.Q8_0)
+
+    def _requantized(self, name: str) -> np.ndarray:
+        if name not in self._requant:
+            t = self.info(name)
+            x = dequantize(self.g.raw(name), t.ggml_type, t.n_elements)
+            self._requant[name] = quantize(x, GGMLType.Q8_0)
+        return self._requant[name]
+
+    def repack_into(self, name: str, K_src: int, rows: np.ndarray, dst_rows: np.ndarray, kb0: int, kb1: int,
+                    dst: list[np.ndarray]) -> None:
+        t = self.info(name)
+        rows = np.ascontiguousarray(rows, dtype=np.int64)
+        dst_rows = np.ascontiguousarray(dst_rows, dtype=np.int64)
+        if t.ggml_type in NATIVE_QTYPES:
+            if self.nat is not None:
+                self.nat.repack(name, rows, dst_rows, K_src, kb0, kb1, [d.ctypes.data for d in dst], self.threads)
+            else:
+                _np_repack_rows(self.g.raw(name), int(t.ggml_type), K_src, rows, dst_rows, kb0, kb1, dst)
+        else:
+            src = self._requantized(name)
+            if self.nat is not None:
+                native().repack_ptr(src.ctypes.data, int(GGMLType.Q8_0), K_src, rows, dst_rows, kb0, kb1,
+                                    [d.ctypes.data for d in dst], self.threads)
+            else:
+                _np_repack_rows(src, int(GGMLType.Q8_0), K_src, rows, dst_rows, kb0, kb1, dst)
+
+
+def build_qmat(src: WeightSource, parts: list[tuple[str, np.ndarray, np.ndarray]], N: int, K_src: int,
+               kb: tuple[int, int] | None, device, expert_rows: int = 0) -> DevQMat:
+    """parts: (tensor, source rows, destination rows). All parts must share one device qtype."""
+    qts = {src.qtype_of(p[0]) for p in parts}
+    if len(qts) != 1:
+        raise ValueError(f"mixed quant types in one matrix: {qts}")
+    qt = qts.pop()
+    blk = BLOCK_GEOMETRY[GGMLType(qt)][0]
+    kb0, kb1 = kb if kb is not None else (0, K_src // blk)
+    K = (kb1 - kb0) * blk
+    sb = stream_bytes(qt, K)
+    host = [np.zeros(N * b, np.uint8) for b in sb]
+    for name, rows, drows in parts:
+        src.repack_into(name, K_src, rows, drows, kb0, kb1, host)
+    streams = [torch.from_numpy(h).to(device) for h in host]
+    return DevQMat(qt, expert_rows or N, K, streams)
+
+
+def neox_pair_perm(D: int, n_rot: int) -> np.ndarray:
+    """Row order inside one head that makes NEOX pairs (i, i + n_rot/2) adjacent."""
+    half = n_rot // 2
+    p = []
+    for i in range(half):
+        p += [i, i + half]
+    return np.array(p + list(range(n_rot, D)), np.int64)
+
+
+def rope_inv_freq(n_rot: int, base: float) -> np.ndarray:
+    i = np.arange(n_rot // 2, dtype=np.float64)
+    return (base ** (-2.0 * i / n_rot)).astype(np.float32)
+
+
+class DeviceWeights:
+    """All weights of one model (one TP rank) resident on `device`."""
+
+    def __init__(self, path: str, device: str | torch.device = "cuda", tp_rank: int = 0, tp_size: int = 1):
+        self.src = src = WeightSource(path)
+        cfg = self.full_cfg = src.cfg
+        self.device = device
+        self.tp_rank, self.tp_size = tp_rank, tp_size
+        T, r = tp_size, tp_rank
+        E, H, Hkv, D, F, V = cfg.n_embd, cfg.n_head, cfg.n_head_kv, cfg.head_dim, cfg.n_ff, cfg.n_vocab
+        if H % T or Hkv % T or F % T or V % T:
+            raise ValueError(f"tp={T} must divide heads ({H}/{Hkv}), n_ff ({F}) and vocab ({V})")
+        Hl, Hkvl, Fl, Vl = H // T, Hkv // T, F // T, V // T
+        self.cfg = cfg
+        self.local = dict(E=E, H=Hl, Hkv=Hkvl, D=D, F=Fl, V=Vl)
+        dev = device
+        t = lambda a: torch.from_numpy(np.array(a, np.float32)).to(dev)  # noqa: E731
+        phi = cfg.arch == "phi2"
+        perm = neox_pair_perm(D, cfg.n_rot) if cfg.rope_mode == ROPE_NEOX else np.arange(D, dtype=np.int64)
+
+        def head_rows(h0: int, nh: int, permute: bool) -> np.ndarray:
+            base = (np.arange(h0, h0 + nh, dtype=np.int64)[:, None] * D)
+            return (base + (perm if permute else np.arange(D))[None, :]).reshape(-1)
+
+        def kblocks(K_full: int, name: str) -> tuple[int, int]:
+            blk = BLOCK_GEOMETRY[GGMLType(src.qtype_of(name))][0]
+            nb = K_full // blk
+            if nb % T:
+                raise ValueError(f"{name}: {nb} blocks of {blk} not divisible by tp={T}")
+            return (r * nb // T, (r + 1) * nb // T)
+
+        ar = lambda n, off=0: np.arange(off, off + n, dtype=np.int64)  # noqa: E731
+        self.tok_embd = build_qmat(src, [("token_embd.weight", ar(V), ar(V))], V, E, None, dev)
+        self.layers = []
+        Eq, Ekv = Hl * D, Hkvl * D
+        for i in range(cfg.n_layer):
+            b = f"blk.{i}."
+            L: dict = {}
+            if phi:
+                qkv = b + "attn_qkv.weight"
+                rq = head_rows(r * Hl, Hl, True)
+                rk = E + head_rows(r * Hkvl, Hkvl, True)
+                rv = E + Hkv * D + head_rows(r * Hkvl, Hkvl, False)
+                rows = np.concatenate([rq, rk, rv])
+                L["wqk"] = build_qmat(src, [(qkv, rows, ar(len(rows)))], Eq + 2 * Ekv, E, None, dev)
+                L["qkv_bias"] = t(src.f32(b + "attn_qkv.bias")[rows])
+                L["attn_norm"] = t(src.f32(b + "attn_norm.weight"))
+                L["attn_norm_b"] = t(src.f32(b + "attn_norm.bias"))
+                L["wo"] = build_qmat(src, [(b + "attn_output.weight", ar(E), ar(E))], E, E,
+                                     kblocks(E, b + "attn_output.weight"), dev)
+                L["bo"] = t(src.f32(b + "attn_output.bias")) if r == 0 else None
+                L["wgu"] = build_qmat(src, [(b + "ffn_up.weight", ar(Fl, r * Fl), ar(Fl))], Fl, E, None, dev)
+                L["bup"] = t(src.f32(b + "ffn_up.bias")[r * Fl:(r + 1) * Fl])
+                L["wdown"] = build_qmat(src, [(b + "ffn_down.weight", ar(E), ar(E))], E, F,
+                                        kblocks(F, b + "ffn_down.weight"), dev)
+                L["bdown"] = t(src.f32(b + "ffn_down.bias")) if r == 0 else None
+            else:
+                rq = head_rows(r * Hl, Hl, cfg.rope_mode == ROPE_NEOX)
+                rk = head_rows(r * Hkvl, Hkvl, cfg.rope_mode == ROPE_NEOX)
+                rv = head_rows(r * Hkvl, Hkvl, False)
+                nq, nk, nv = b + "attn_q.weight", b + "attn_k.weight", b + "attn_v.weight"
+                if src.qtype_of(nq) == src.qtype_of(nk) == src.qtype_of(nv):
+                    L["wqk"] = build_qmat(src, [(nq, rq, ar(Eq)), (nk, rk, ar(Ekv, Eq)), (nv, rv, ar(Ekv, Eq + Ekv))],
+                                          Eq + 2 * Ekv, E, None, dev)
+                else:
+                    L["wqk"] = build_qmat(src, [(nq, rq, ar(Eq)), (nk, rk, ar(Ekv, Eq))], Eq + Ekv, E, None, dev)
+                    L["wv"] = build_qmat(src, [(nv, rv, ar(Ekv))], Ekv, E, None, dev)
+                L["attn_norm"] = t(src.f32(b + "attn_norm.weight"))
+                L["ffn_norm"] = t(src.f32(b + "ffn_norm.weight"))
+                L["wo"] = build_qmat(src, [(b + "attn_output.weight", ar(E), ar(E))], E, E,
+                                     kblocks(E, b + "attn_output.weight"), dev)
+                if cfg.n_expert:
+                    X = cfg.n_expert
+                    L["router"] = build_qmat(src, [(b + "ffn_gate_inp.weight", ar(X), ar(X))], X, E, None, dev)
+                    gparts = []
+                    for e in range(X):
+                        loc = ar(Fl, e * F + r * Fl)
+                        gparts.append((b + "ffn_gate_exps.weight", loc, e * 2 * Fl + 2 * ar(Fl)))
+                        gparts.append((b + "ffn_up_exps.weight", loc, e * 2 * Fl + 2 * ar(Fl) + 1))
+                    L["gu_exps"] = build_qmat(src, gparts, X * 2 * Fl, E, None, dev, expert_rows=2 * Fl)
+                    L["down_exps"] = build_qmat(src, [(b + "ffn_down_exps.weight", ar(X * E), ar(X * E))], X * E, F,
+                                                kblocks(F, b + "ffn_down_exps.weight"), dev, expert_rows=E)
+                else:
+                    ng, nu = b + "ffn_gate.weight", b + "ffn_up.weight"
+                    loc = ar(Fl, r * Fl)
+                    L["wgu"] = build_qmat(src, [(ng, loc, 2 * ar(Fl)), (nu, loc, 2 * ar(Fl) + 1)], 2 * Fl, E, None, dev)
+                    L["wdown"] = build_qmat(src, [(b + "ffn_down.weight", ar(E), ar(E))], E, F,
+                                            kblocks(F, b + "ffn_down.weight"), dev)
+            self.layers.append(L)
+        self.out_norm = t(src.f32("output_norm.weight"))
+        self.out_norm_b = t(src.f32("output_norm.bias")) if src.has("output_norm.bias") else None
+        out_name = "output.weight" if src.has("output.weight") else "token_embd.weight"  # tied embeddings
+        self.lm_head = build_qmat(src, [(out_name, ar(Vl, r * Vl), ar(Vl))], Vl, E, None, dev)
+        self.lm_bias = t(src.f32("output.bias")[r * Vl:(r + 1) * Vl]) if src.has("output.bias") else None
+        self.inv_freq = t(rope_inv_freq(cfg.n_rot, cfg.rope_base))
+
+    @property
+    def nbytes(self) -> int:
+        n = self.tok_embd.nbytes + self.lm_head.nbytes
+        for L in self.layers:
+            for v in L.values():
+                if isinstance(v, DevQMat):
+                    n += v.nbytes
+        return n

@@ -230,7 +230,7 @@ def random_blocks(ggml_type: int, n_rows: int, k: int, rng: np.random.Generator,
         return quantize(rng.standard_normal(n, dtype=np.float32) * std, t)
     blk, nb = BLOCK_GEOMETRY[t]
     nblk = n // blk
-    out = rng.integers(0, 256, size=(nblk, nb), dtype=np.uint8)
+    out = np.frombuffer(rng.bytes(nblk * nb), dtype=np.uint8).reshape(nblk, nb).copy()
     if t in (GGMLType.Q4_0,):
         d = np.full(nblk, std / 4.6, np.float32) * rng.uniform(0.75, 1.25, nblk).astype(np.float32)
         out[:, 0:2] = _to_f16_bytes(d)
