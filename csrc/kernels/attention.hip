@@ -62,25 +62,39 @@ __global__ __launch_bounds__(256) void attn_partial_kernel(AttnParams P) {
   const int* bt = P.block_table + (long long)seq * P.max_blocks;
   const f16* kc = (const f16*)P.kc;
   const f16* vc = (const f16*)P.vc;
-  for (int t = t0 + wave * 4 + tg; t < t1; t += 16) {
-    const long long blk = bt[t / P.bs];
-    const long long base = ((blk * P.n_kv + kvh) * P.bs + (t % P.bs)) * D + li * DPL;
-    float k[DPL], v[DPL];
-    load_row<DPL>(kc + base, k);
-    load_row<DPL>(vc + base, v);
+  // 4 key slots per lane group per step (64 keys per block-step): all K/V loads of a step are
+  // issued before any is consumed, so one HBM round trip covers 64 keys
+  constexpr int U = 4;
+  for (int ts = t0; ts < t1; ts += 16 * U) {
+    float k[U][DPL], v[U][DPL];
+    bool ok[U];
 #pragma unroll
-    for (int g = 0; g < G; ++g) {
-      float s = 0.f;
+    for (int u = 0; u < U; ++u) {
+      const int t = ts + u * 16 + wave * 4 + tg;
+      ok[u] = t < t1;
+      const int tt = ok[u] ? t : t0;
+      const long long blk = bt[tt / P.bs];
+      const long long base = ((blk * P.n_kv + kvh) * P.bs + (tt % P.bs)) * D + li * DPL;
+      load_row<DPL>(kc + base, k[u]);
+      load_row<DPL>(vc + base, v[u]);
+    }
 #pragma unroll
-      for (int j = 0; j < DPL; ++j) s += q[g][j] * k[j];
-      s = group_sum<16>(s);
-      const float mn = fmaxf(m[g], s);
-      const float corr = __expf(m[g] - mn);
-      const float p = __expf(s - mn);
-      l[g] = l[g] * corr + p;
+    for (int u = 0; u < U; ++u) {
+      if (!ok[u]) continue;  // uniform within the 16-lane group
 #pragma unroll
-      for (int j = 0; j < DPL; ++j) acc[g][j] = acc[g][j] * corr + p * v[j];
-      m[g] = mn;
+      for (int g = 0; g < G; ++g) {
+        float sc = 0.f;
+#pragma unroll
+        for (int j = 0; j < DPL; ++j) sc += q[g][j] * k[u][j];
+        sc = group_sum<16>(sc);
+        const float mn = fmaxf(m[g], sc);
+        const float corr = __expf(m[g] - mn);
+        const float p = __expf(sc - mn);
+        l[g] = l[g] * corr + p;
+#pragma unroll
+        for (int j = 0; j < DPL; ++j) acc[g][j] = acc[g][j] * corr + p * v[u][j];
+        m[g] = mn;
+      }
     }
   }
   // merge the 4 token groups of the wave (lanes li, li+16, li+32, li+48)
@@ -140,23 +154,28 @@ __global__ __launch_bounds__(256) void attn_partial_kernel(AttnParams P) {
 }
 
 __global__ __launch_bounds__(128) void attn_combine_kernel(AttnParams P) {
+  // splits' (m, l) are read once by the first wave into LDS weights; every output dim then sums
+  // S independent partials (no serial dependent-load chain)
+  __shared__ float sw[64];
+  __shared__ float sL;
   const int qi = blockIdx.x, h = blockIdx.y, S = P.n_splits, D = P.D;
   const float* ws = P.ws + ((long long)qi * P.H + h) * S * (D + 2);
-  float M = -INFINITY;
-  for (int s = 0; s < S; ++s)
-    if (ws[s * (D + 2) + D + 1] > 0.f) M = fmaxf(M, ws[s * (D + 2) + D]);
+  if (threadIdx.x < 64) {
+    const int s = threadIdx.x;
+    const bool live = s < S && ws[s * (D + 2) + D + 1] > 0.f;
+    const float m = live ? ws[s * (D + 2) + D] : -INFINITY;
+    const float M = wave_max(m);
+    const float w = live ? __expf(m - M) : 0.f;
+    sw[s] = w;
+    const float L = wave_sum(live ? w * ws[s * (D + 2) + D + 1] : 0.f);
+    if (s == 0) sL = L;
+  }
+  __syncthreads();
+  const float L = sL;
   for (int d = threadIdx.x; d < D; d += blockDim.x) {
-    float L = 0.f, A = 0.f;
-    if (M != -INFINITY) {
-      for (int s = 0; s < S; ++s) {
-        const float* w = ws + s * (D + 2);
-        if (w[D + 1] > 0.f) {
-          const float c = __expf(w[D] - M);
-          L += w[D + 1] * c;
-          A += w[d] * c;
-        }
-      }
-    }
+    float A = 0.f;
+#pragma unroll 8
+    for (int s = 0; s < S; ++s) A += sw[s] * ws[s * (D + 2) + d];
     P.out[(long long)qi * P.ldo + h * D + d] = L > 0.f ? A / L : 0.f;
   }
 }

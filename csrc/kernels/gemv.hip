@@ -195,92 +195,62 @@ __device__ void stage_activation(const GemvParams& P, int b, int K, i32x4* lq, f
   }
 }
 
-template <int QT, int NPC, int R, int BT>
-__global__ __launch_bounds__(256) void gemv_kernel(GemvParams P) {
-  constexpr int NT = 256;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const QMat& w = P.w;
-  const int K = w.K, N = w.N;
-  const int G = K / 16;
-  i32x4* lq = (i32x4*)smem;                               // [BT][G]
-  float* ld = (float*)(smem + (size_t)BT * G * 16);       // [BT][G]
-  float* ls = ld + BT * G;                                // [BT][G]
-  float* red = ls + BT * G;                               // [NT/64]
-  const int b0 = blockIdx.y * BT;
+// --------------------------------------------------------------------------------------------
+// Kernel structure (per 256-thread block = 4 waves, each wave owns R = 2 rows of a row tile):
+//   1. issue the first tile's weight loads (they do not depend on x)
+//   2. activation prologue into LDS (overlaps the weight fetch)
+//   3. persistent loop over row tiles (tile += gridDim.x): prefetch the next tile's weights into
+//      a second register set while the current tile is computed (MODE 0), or reload (MODE 1/2).
+// MODE 0: one K round, double-buffered; MODE 1: one K round, single buffer; MODE 2: K split in
+// rounds of 64*NPC pieces (K > 16384).
+constexpr int GEMV_NW = 4;
+constexpr int GEMV_R = 2;
 
-  // expert routing (MoE): blockIdx.z selects the k-th chosen expert of batch row b0
-  long long row_base = 0;
-  const float* x_save = P.x;
-  GemvParams Q = P;
-  if (P.expert_ids) {
-    const int e = P.expert_ids[b0 * P.n_sel + blockIdx.z];
-    row_base = (long long)e * N;
-    if (P.x_per_sel) Q.x = P.x + (long long)blockIdx.z * P.x_sel_stride;
-  }
-  (void)x_save;
-
+template <int QT, int NPC>
+__device__ __forceinline__ void load_tile(const QMat& w, long long row_base, int row0, int N, int base, int Pc,
+                                          int lane, WFrag (&wf)[GEMV_R][NPC]) {
 #pragma unroll
-  for (int b = 0; b < BT; ++b) {
-    if (b0 + b < P.B) {
-      stage_activation<NT>(Q, b0 + b, K, lq + b * G, ld + b * G, ls + b * G, red);
-    } else {
-      for (int g = threadIdx.x; g < G; g += NT) {
-        lq[b * G + g] = (i32x4){0, 0, 0, 0};
-        ld[b * G + g] = 0.f;
-        ls[b * G + g] = 0.f;
+  for (int i = 0; i < NPC; ++i) {
+    const int p = min(base + 64 * i + lane, Pc - 1);
+#pragma unroll
+    for (int r = 0; r < GEMV_R; ++r) load_wfrag<QT>(w, row_base + min(row0 + r, N - 1), p, wf[r][i]);
+  }
+}
+
+template <int QT, int NPC, int BT>
+__device__ __forceinline__ void compute_tile(const WFrag (&wf)[GEMV_R][NPC], int base, int Pc, int lane, int G,
+                                             const i32x4* lq, const float* ld, const float* ls,
+                                             float (&acc)[GEMV_R][BT]) {
+#pragma unroll
+  for (int i = 0; i < NPC; ++i) {
+    const int p = base + 64 * i + lane;
+    if (p < Pc) {
+      int glo, ghi;
+      piece_groups(QT, p, glo, ghi);
+#pragma unroll
+      for (int b = 0; b < BT; ++b) {
+        XFrag xf;
+        xf.lo = lq[b * G + glo];
+        xf.hi = lq[b * G + ghi];
+        xf.dlo = ld[b * G + glo];
+        xf.dhi = ld[b * G + ghi];
+        xf.slo = ls[b * G + glo];
+        xf.shi = ls[b * G + ghi];
+#pragma unroll
+        for (int r = 0; r < GEMV_R; ++r) acc[r][b] += piece_dot<QT>(wf[r][i], xf, p);
       }
     }
   }
-  __syncthreads();
+}
 
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int row0 = (blockIdx.x * (NT / 64) + wave) * R;
-  if (row0 >= N) return;
-  const int Pc = K / 32;
-  float acc[R][BT];
-#pragma unroll
-  for (int r = 0; r < R; ++r)
-#pragma unroll
-    for (int b = 0; b < BT; ++b) acc[r][b] = 0.f;
-
-  for (int base = 0; base < Pc; base += 64 * NPC) {
-    WFrag wf[R][NPC];
-#pragma unroll
-    for (int i = 0; i < NPC; ++i) {
-      const int p = min(base + 64 * i + lane, Pc - 1);
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const long long row = row_base + min(row0 + r, N - 1);
-        load_wfrag<QT>(w, row, p, wf[r][i]);
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < NPC; ++i) {
-      const int p = base + 64 * i + lane;
-      if (p < Pc) {
-        int glo, ghi;
-        piece_groups(QT, p, glo, ghi);
-#pragma unroll
-        for (int b = 0; b < BT; ++b) {
-          XFrag xf;
-          xf.lo = lq[b * G + glo];
-          xf.hi = lq[b * G + ghi];
-          xf.dlo = ld[b * G + glo];
-          xf.dhi = ld[b * G + ghi];
-          xf.slo = ls[b * G + glo];
-          xf.shi = ls[b * G + ghi];
-#pragma unroll
-          for (int r = 0; r < R; ++r) acc[r][b] += piece_dot<QT>(wf[r][i], xf, p);
-        }
-      }
-    }
-  }
+template <int BT>
+__device__ __forceinline__ void epilogue(const GemvParams& P, float (&acc)[GEMV_R][BT], int row0, int N, int b0,
+                                         int lane) {
+  constexpr int R = GEMV_R;
 #pragma unroll
   for (int r = 0; r < R; ++r)
 #pragma unroll
     for (int b = 0; b < BT; ++b) acc[r][b] = wave_sum(acc[r][b]);
-
-  // ---- fused epilogues: lane (r*BT + b) owns output (row0 + r, b0 + b)
 #pragma unroll
   for (int r = 0; r < R; ++r) {
 #pragma unroll
@@ -310,7 +280,7 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvParams P) {
           break;
         case EPI_GLU:
           if ((r & 1) == 0) {  // even row = gate, odd row = up
-            const float u = acc[r + 1 < R ? r + 1 : r][b];
+            const float u = acc[r + 1][b];
             P.y[(long long)bb * P.ldy + (long long)blockIdx.z * P.y_sel_stride + vn / 2] = silu(v) * u;
           }
           break;
@@ -323,8 +293,7 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvParams P) {
           if (P.bias) v += P.bias[vn];
           float out = v;
           if (which < 2 && d < P.n_rot) {
-            const int pr = r ^ 1;
-            float pv = acc[pr][b];
+            float pv = acc[r ^ 1][b];
             if (P.bias) pv += P.bias[vn ^ 1];
             const float ang = (float)P.pos[bb] * P.inv_freq[d >> 1];
             float sn, cs;
@@ -336,8 +305,10 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvParams P) {
           } else {
             const int slot = P.slot[bb];
             const long long blk = slot / P.bs, off = slot % P.bs;
-            f16* dst = (f16*)(which == 1 ? P.kc : P.vc);
-            dst[((blk * P.n_kv + hh) * P.bs + off) * D + d] = (f16)out;
+            const long long idx = ((blk * P.n_kv + hh) * P.bs + off) * D + d;
+            // two explicit stores: a pointer select here is lowered to an indexed scratch array
+            if (which == 1) ((f16*)P.kc)[idx] = (f16)out;
+            else ((f16*)P.vc)[idx] = (f16)out;
           }
           break;
         }
@@ -346,24 +317,122 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvParams P) {
   }
 }
 
-template <int QT, int NPC, int R, int BT>
+template <int QT, int NPC, int BT, int MODE>
+__global__ __launch_bounds__(256) void gemv_kernel(GemvParams P) {
+  constexpr int NT = 256, R = GEMV_R, ROWS = GEMV_NW * GEMV_R;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const QMat& w = P.w;
+  const int K = w.K, N = w.N;
+  const int G = K / 16;
+  i32x4* lq = (i32x4*)smem;                               // [BT][G]
+  float* ld = (float*)(smem + (size_t)BT * G * 16);       // [BT][G]
+  float* ls = ld + BT * G;                                // [BT][G]
+  float* red = ls + BT * G;                               // [NT/64]
+  const int b0 = blockIdx.y * BT;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int Pc = K / 32;
+  const int n_tiles = (N + ROWS - 1) / ROWS;
+  int tile = blockIdx.x;
+
+  long long row_base = 0;
+  GemvParams Q = P;
+  if (P.expert_ids) {  // MoE: blockIdx.z = k-th selected expert of batch row b0
+    const int e = P.expert_ids[b0 * P.n_sel + blockIdx.z];
+    row_base = (long long)e * N;
+    if (P.x_per_sel) Q.x = P.x + (long long)blockIdx.z * P.x_sel_stride;
+  }
+
+  WFrag wa[R][NPC];
+  if (MODE != 2 && tile < n_tiles) load_tile<QT, NPC>(w, row_base, tile * ROWS + wave * R, N, 0, Pc, lane, wa);
+
+#pragma unroll
+  for (int b = 0; b < BT; ++b) {
+    if (b0 + b < P.B) {
+      stage_activation<NT>(Q, b0 + b, K, lq + b * G, ld + b * G, ls + b * G, red);
+    } else {
+      for (int g = threadIdx.x; g < G; g += NT) {
+        lq[b * G + g] = (i32x4){0, 0, 0, 0};
+        ld[b * G + g] = 0.f;
+        ls[b * G + g] = 0.f;
+      }
+    }
+  }
+  __syncthreads();
+
+  for (; tile < n_tiles; tile += gridDim.x) {
+    const int row0 = tile * ROWS + wave * R;
+    const int next = tile + gridDim.x;
+    float acc[R][BT];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+      for (int b = 0; b < BT; ++b) acc[r][b] = 0.f;
+    if constexpr (MODE == 0) {
+      WFrag wb[R][NPC];
+      if (next < n_tiles) load_tile<QT, NPC>(w, row_base, next * ROWS + wave * R, N, 0, Pc, lane, wb);
+      compute_tile<QT, NPC, BT>(wa, 0, Pc, lane, G, lq, ld, ls, acc);
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int i = 0; i < NPC; ++i) wa[r][i] = wb[r][i];
+    } else if constexpr (MODE == 1) {
+      compute_tile<QT, NPC, BT>(wa, 0, Pc, lane, G, lq, ld, ls, acc);
+      if (next < n_tiles) load_tile<QT, NPC>(w, row_base, next * ROWS + wave * R, N, 0, Pc, lane, wa);
+    } else {
+      for (int base = 0; base < Pc; base += 64 * NPC) {
+        load_tile<QT, NPC>(w, row_base, row0, N, base, Pc, lane, wa);
+        compute_tile<QT, NPC, BT>(wa, base, Pc, lane, G, lq, ld, ls, acc);
+      }
+    }
+    if (row0 < N) epilogue<BT>(P, acc, row0, N, b0, lane);
+  }
+}
+
+template <int QT, int NPC, int BT, int MODE>
 static void launch_t(const GemvParams& P, hipStream_t s) {
   const int N = P.w.N;
-  const int rows_per_block = 4 * R;
-  dim3 grid((N + rows_per_block - 1) / rows_per_block, (P.B + BT - 1) / BT, P.expert_ids ? P.n_sel : 1);
+  const int rows_per_block = GEMV_NW * GEMV_R;
+  const int tiles = (N + rows_per_block - 1) / rows_per_block;
+  const int by = (P.B + BT - 1) / BT;
+  const int bz = P.expert_ids ? P.n_sel : 1;
+  // persistent grid: ~2 blocks per CU over all (y, z) slices; each block walks its row tiles
+  int gx = tiles;
+  const int cap = 512 / (by * bz) > 0 ? 512 / (by * bz) : 1;
+  if (gx > cap) gx = cap;
+  dim3 grid(gx, by, bz);
   const size_t lds = (size_t)BT * (P.w.K / 16) * 24 + 64;
-  hipLaunchKernelGGL((gemv_kernel<QT, NPC, R, BT>), grid, dim3(256), lds, s, P);
+  hipLaunchKernelGGL((gemv_kernel<QT, NPC, BT, MODE>), grid, dim3(256), lds, s, P);
+}
+
+template <int QT, int BT>
+static void launch_b(const GemvParams& P, hipStream_t s) {
+  const int Pc = P.w.K / 32;
+  const int need = (Pc + 63) / 64;
+  switch (need) {
+    case 1: launch_t<QT, 1, BT, 0>(P, s); break;
+    case 2: launch_t<QT, 2, BT, 0>(P, s); break;
+    case 3: launch_t<QT, 3, BT, 1>(P, s); break;
+    case 4: launch_t<QT, 4, BT, 1>(P, s); break;
+    case 5: launch_t<QT, 5, BT, 1>(P, s); break;
+    case 6: launch_t<QT, 6, BT, 1>(P, s); break;
+    case 7: launch_t<QT, 7, BT, 1>(P, s); break;
+    case 8: launch_t<QT, 8, BT, 1>(P, s); break;
+    default: launch_t<QT, 8, BT, 2>(P, s); break;
+  }
 }
 
 template <int QT>
 static void launch_q(const GemvParams& P, hipStream_t s) {
-  const int Pc = P.w.K / 32;
-  const int need = (Pc + 63) / 64;
-  const bool b1 = P.B == 1 || P.expert_ids != nullptr;  // MoE: experts differ per batch row
-  if (need <= 1) { if (b1) launch_t<QT, 1, 4, 1>(P, s); else launch_t<QT, 1, 2, 4>(P, s); }
-  else if (need <= 2) { if (b1) launch_t<QT, 2, 4, 1>(P, s); else launch_t<QT, 2, 2, 4>(P, s); }
-  else if (need <= 4) { if (b1) launch_t<QT, 4, 2, 1>(P, s); else launch_t<QT, 4, 2, 4>(P, s); }
-  else { if (b1) launch_t<QT, 8, 2, 1>(P, s); else launch_t<QT, 8, 2, 4>(P, s); }
+  if (P.B == 1 || P.expert_ids != nullptr) {  // decode (and MoE: experts differ per batch row)
+    launch_b<QT, 1>(P, s);
+    return;
+  }
+  // small-batch tiles of 4 rows (chunked prefill / batched decode): 2 pieces per lane per K
+  // round keeps the 4 x-fragment sets + weights inside the register budget
+  const int need = (P.w.K / 32 + 63) / 64;
+  if (need == 1) launch_t<QT, 1, 4, 0>(P, s);
+  else if (need == 2) launch_t<QT, 2, 4, 0>(P, s);
+  else launch_t<QT, 2, 4, 2>(P, s);
 }
 
 void gemv(const GemvParams& P, hipStream_t s) {

@@ -2,8 +2,9 @@
 // decode step -- forward + sampling + history update -- stays inside one hipGraph replay.
 // Order follows Ollama's (llama.cpp) default chain: repeat/presence/frequency penalties over the
 // last `repeat_last_n` tokens -> top-k -> top-p -> min-p (on T = 1 probabilities) -> temperature
-// -> categorical draw. temperature <= 0 is greedy argmax. Top-k uses a 4-pass 8-bit radix select
-// over order-preserving float keys, then a bitonic sort of the survivors in LDS.
+// -> categorical draw. temperature <= 0 is greedy argmax. Top-k: a histogram of (max - logit) in
+// fine bins locates the k-th largest, the survivors are bitonic-sorted in LDS; an exact 4-pass
+// radix select over order-preserving float keys is the fallback when too many logits tie.
 #include "common.h"
 #include "ops.h"
 
@@ -11,6 +12,8 @@ namespace omx {
 
 constexpr int SAMPLE_NT = 1024;
 constexpr int SAMPLE_CAP = 1024;
+constexpr int SAMPLE_BINS = 2 * SAMPLE_NT;  // 2048 bins of 1/32 logit unit = 64 units below max
+constexpr float SAMPLE_BIN_SCALE = 32.f;
 
 __device__ __forceinline__ unsigned fkey(float f) {
   const unsigned u = __float_as_uint(f);
@@ -56,7 +59,9 @@ __global__ __launch_bounds__(SAMPLE_NT) void sample_kernel(SampleParams P) {
   __shared__ float redv[SAMPLE_NT / 64];
   __shared__ int redi[SAMPLE_NT / 64];
   __shared__ unsigned s_prefix, s_mask, s_remaining;
-  __shared__ int s_count;
+  __shared__ int s_count, s_bstar;
+  __shared__ unsigned bins[SAMPLE_BINS];
+  __shared__ unsigned wsum[SAMPLE_NT / 64];
   const int b = blockIdx.x;
   float* lg = (float*)P.logits + (long long)b * P.ld;
   const int V = P.V;
@@ -100,7 +105,54 @@ __global__ __launch_bounds__(SAMPLE_NT) void sample_kernel(SampleParams P) {
     int k = P.top_k[b];
     if (k <= 0 || k > SAMPLE_CAP) k = SAMPLE_CAP;
     if (k > V) k = V;
-    // ---- radix select: key of the k-th largest logit
+    // ---- fast path: histogram of (max - x) in 1/32-wide bins. Logits spread over the bins, so
+    // the LDS atomics rarely collide (a radix pass on raw float keys puts nearly every logit in
+    // 2-3 exponent bins and serialises). Everything in bins <= b* (the bin holding the k-th
+    // largest) is collected and sorted exactly; the radix select below remains the fallback.
+    float mx;
+    {
+      float lm = -INFINITY;
+      for (int i = threadIdx.x; i < V; i += SAMPLE_NT) lm = fmaxf(lm, lg[i]);
+      mx = block_max<SAMPLE_NT>(lm, redv);
+    }
+    for (int i = threadIdx.x; i < SAMPLE_BINS; i += SAMPLE_NT) bins[i] = 0;
+    __syncthreads();
+    for (int i = threadIdx.x; i < V; i += SAMPLE_NT) {
+      const float d = (mx - lg[i]) * SAMPLE_BIN_SCALE;
+      if (d < (float)(SAMPLE_BINS - 1)) atomicAdd(&bins[(int)d], 1u);
+    }
+    if (threadIdx.x == 0) { s_bstar = SAMPLE_BINS - 1; s_count = 0; }
+    __syncthreads();
+    {  // block-wide exclusive scan over bins (2 per thread) -> first bin where cum >= k
+      const unsigned a0 = bins[2 * threadIdx.x], a1 = bins[2 * threadIdx.x + 1];
+      unsigned v = a0 + a1, incl = v;
+      const int ln = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const unsigned t = __shfl_up(incl, o, 64);
+        if (ln >= o) incl += t;
+      }
+      if (ln == 63) wsum[wv] = incl;
+      __syncthreads();
+      unsigned pre = 0;
+      for (int w = 0; w < wv; ++w) pre += wsum[w];
+      const unsigned ex = pre + incl - v;
+      if (ex < (unsigned)k && ex + a0 >= (unsigned)k) s_bstar = 2 * threadIdx.x;
+      else if (ex + a0 < (unsigned)k && ex + v >= (unsigned)k) s_bstar = 2 * threadIdx.x + 1;
+    }
+    __syncthreads();
+    const int bstar = s_bstar;
+    for (int i = threadIdx.x; i < V; i += SAMPLE_NT) {
+      const float v = lg[i];
+      const float d = (mx - v) * SAMPLE_BIN_SCALE;
+      if (d < (float)(bstar + 1)) {
+        const int slot = atomicAdd(&s_count, 1);
+        if (slot < SAMPLE_CAP) { cval[slot] = v; cidx[slot] = i; }
+      }
+    }
+    __syncthreads();
+    if (s_count > SAMPLE_CAP) {
+    // ---- radix select fallback: key of the k-th largest logit
     if (threadIdx.x == 0) { s_prefix = 0; s_mask = 0; s_remaining = k; }
     __syncthreads();
     for (int pass = 0; pass < 4; ++pass) {
@@ -137,6 +189,7 @@ __global__ __launch_bounds__(SAMPLE_NT) void sample_kernel(SampleParams P) {
       }
     }
     __syncthreads();
+    }
     const int cnt = min(s_count, SAMPLE_CAP);
     int n2 = 1;
     while (n2 < cnt) n2 <<= 1;
