@@ -139,7 +139,10 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("attention", [](uintptr_t q, int ldq, uintptr_t kc, uintptr_t vc, uintptr_t block_table, int max_blocks,
                         uintptr_t q_seq, uintptr_t q_len, int NQ, int H, int n_kv, int D, int bs, float scale,
-                        int window, uintptr_t out, int ldo, uintptr_t ws, int n_splits, uintptr_t stream) {
+                        int window, uintptr_t out, int ldo, uintptr_t ws, int n_splits, uintptr_t counters,
+                        uintptr_t stream) {
+    if (n_splits < 1 || n_splits > 64) throw std::runtime_error("n_splits must be in [1, 64]");
+    if (n_splits > 1 && (!ws || !counters)) throw std::runtime_error("split attention needs ws and counters");
     check_attn(H, n_kv, D);
     AttnParams A{};
     A.q = Pp<const float>(q);
@@ -161,9 +164,12 @@ PYBIND11_MODULE(_C, m) {
     A.ldo = ldo;
     A.ws = Pp<float>(ws);
     A.n_splits = n_splits;
+    A.counters = Pp<int>(counters);
     attention_decode(A, S(stream));
   });
   m.def("attention_ws_floats", &attention_ws_floats);
+  m.def("set_gemv_tuning", &set_gemv_tuning, py::arg("blocks_per_cu") = 0, py::arg("rows_per_wave") = 0,
+        py::arg("r1") = -1);
   m.def("embed_rows", [](py::object w, uintptr_t rows, int n, uintptr_t out, int ldo, uintptr_t stream) {
     embed_rows(qmat(w), Pp<const int>(rows), n, Pp<float>(out), ldo, S(stream));
   });
@@ -271,6 +277,7 @@ PYBIND11_MODULE(_C, m) {
         w.eids = Pp<int>(ptr("eids"));
         w.ew = Pp<float>(ptr("ew"));
         w.attn_ws = Pp<float>(ptr("attn_ws"));
+        w.attn_cnt = Pp<int>(ptr("attn_cnt"));
         w.max_B = d["max_B"].cast<int>();
         w.n_splits = d["n_splits"].cast<int>();
       })

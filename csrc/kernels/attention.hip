@@ -6,8 +6,8 @@
 // and the 4 waves 16 keys per step; scores reduce inside the 16-lane group with xor-shuffles.
 // Online softmax per lane group, merged across groups/waves at the end. The key range of a query
 // is cut into `n_splits` equal chunks computed ON DEVICE from its length (flash-decode), so the
-// grid is fixed and the launch is hipGraph-capturable for any context length; a tiny combine
-// kernel merges split partials (skipped when n_splits == 1).
+// grid is fixed and the launch is hipGraph-capturable for any context length; the last split
+// block to arrive (agent-scope release/acquire ticket) merges the partials in the same launch.
 // Causal prefill uses the same kernel: each prompt token is a query with length pos + 1.
 #include "common.h"
 #include "ops.h"
@@ -142,41 +142,60 @@ __global__ __launch_bounds__(256) void attn_partial_kernel(AttnParams P) {
     const int h = kvh * G + g;
     if (S == 1) {
       P.out[(long long)qi * P.ldo + h * D + d] = L > 0.f ? A / L : 0.f;
-    } else {
+    } else {  // write-through (sc1) stores: the hand-off below then needs no release fence
       float* ws = P.ws + (((long long)qi * P.H + h) * S + split) * (D + 2);
-      ws[d] = A;
+      __hip_atomic_store(ws + d, A, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (d == 0) {
-        ws[D] = M;
-        ws[D + 1] = L;
+        __hip_atomic_store(ws + D, M, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(ws + D + 1, L, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
   }
-}
-
-__global__ __launch_bounds__(128) void attn_combine_kernel(AttnParams P) {
-  // splits' (m, l) are read once by the first wave into LDS weights; every output dim then sums
-  // S independent partials (no serial dependent-load chain)
-  __shared__ float sw[64];
-  __shared__ float sL;
-  const int qi = blockIdx.x, h = blockIdx.y, S = P.n_splits, D = P.D;
-  const float* ws = P.ws + ((long long)qi * P.H + h) * S * (D + 2);
-  if (threadIdx.x < 64) {
-    const int s = threadIdx.x;
-    const bool live = s < S && ws[s * (D + 2) + D + 1] > 0.f;
-    const float m = live ? ws[s * (D + 2) + D] : -INFINITY;
-    const float M = wave_max(m);
-    const float w = live ? __expf(m - M) : 0.f;
-    sw[s] = w;
-    const float L = wave_sum(live ? w * ws[s * (D + 2) + D + 1] : 0.f);
-    if (s == 0) sL = L;
+  if (S == 1) return;
+  // ---- in-launch split combine (cdna_hip_programming.md §6 Guideline 16 / MI355X_MICROARCH.md
+  // "Valid forms" row 1): partials were stored sc1; every wave drains them (vmcnt(0)), the block
+  // barriers, one lane takes an agent-scope ticket. The block drawing the last ticket reads every
+  // partial with sc1 loads (no acquire needed) and merges its G heads. Saves the separate
+  // combine launch (~4.5 us per layer at batch 1).
+  __shared__ int s_last;
+  __shared__ float sw[G][64];
+  __shared__ float sL[G];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int* cnt = P.counters + (long long)qi * P.n_kv + kvh;
+    const int old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = old == S - 1;
+    if (last) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+    s_last = last;
   }
   __syncthreads();
-  const float L = sL;
-  for (int d = threadIdx.x; d < D; d += blockDim.x) {
+  if (!s_last) return;
+  auto ld1 = [](const float* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+  if (threadIdx.x < 64) {
+    const int s = threadIdx.x;
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const float* ws = P.ws + (((long long)qi * P.H + kvh * G + g) * S + (s < S ? s : 0)) * (D + 2);
+      const float lv = ld1(ws + D + 1);
+      const bool live = s < S && lv > 0.f;
+      const float mm = live ? ld1(ws + D) : -INFINITY;
+      const float MM = wave_max(mm);
+      const float w = live ? __expf(mm - MM) : 0.f;
+      sw[g][s] = w;
+      const float LL = wave_sum(live ? w * lv : 0.f);
+      if (s == 0) sL[g] = LL;
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < G * D; i += 256) {
+    const int g = i / D, d = i % D;
+    const float* ws = P.ws + ((long long)qi * P.H + kvh * G + g) * S * (D + 2);
     float A = 0.f;
 #pragma unroll 8
-    for (int s = 0; s < S; ++s) A += sw[s] * ws[s * (D + 2) + d];
-    P.out[(long long)qi * P.ldo + h * D + d] = L > 0.f ? A / L : 0.f;
+    for (int s = 0; s < S; ++s) A += sw[g][s] * ld1(ws + s * (D + 2) + d);
+    const float L = sL[g];
+    P.out[(long long)qi * P.ldo + (kvh * G + g) * D + d] = L > 0.f ? A / L : 0.f;
   }
 }
 
@@ -202,8 +221,7 @@ void attention_decode(const AttnParams& P, hipStream_t s) {
     case 128: launch_d<128>(P, s); break;
     default: break;
   }
-  if (P.n_splits > 1)
-    hipLaunchKernelGGL(attn_combine_kernel, dim3(P.NQ, P.H), dim3(128), 0, s, P);
+  // split partials are merged in-launch by the last-arriving block (see attn_partial_kernel)
 }
 
 size_t attention_ws_floats(int NQ, int H, int D, int n_splits) {

@@ -206,21 +206,28 @@ __device__ void stage_activation(const GemvParams& P, int b, int K, i32x4* lq, f
 constexpr int GEMV_NW = 4;
 constexpr int GEMV_R = 2;
 
-template <int QT, int NPC>
+GemvTuning g_tune;
+void set_gemv_tuning(int blocks_per_cu, int rows_per_wave, int r1) {
+  if (blocks_per_cu > 0) g_tune.blocks_per_cu = blocks_per_cu;
+  if (rows_per_wave == 2 || rows_per_wave == 4) g_tune.rows_per_wave = rows_per_wave;
+  if (r1 >= 0) g_tune.r1 = r1;
+}
+
+template <int QT, int NPC, int R>
 __device__ __forceinline__ void load_tile(const QMat& w, long long row_base, int row0, int N, int base, int Pc,
-                                          int lane, WFrag (&wf)[GEMV_R][NPC]) {
+                                          int lane, WFrag (&wf)[R][NPC]) {
 #pragma unroll
   for (int i = 0; i < NPC; ++i) {
     const int p = min(base + 64 * i + lane, Pc - 1);
 #pragma unroll
-    for (int r = 0; r < GEMV_R; ++r) load_wfrag<QT>(w, row_base + min(row0 + r, N - 1), p, wf[r][i]);
+    for (int r = 0; r < R; ++r) load_wfrag<QT>(w, row_base + min(row0 + r, N - 1), p, wf[r][i]);
   }
 }
 
-template <int QT, int NPC, int BT>
-__device__ __forceinline__ void compute_tile(const WFrag (&wf)[GEMV_R][NPC], int base, int Pc, int lane, int G,
+template <int QT, int NPC, int BT, int R>
+__device__ __forceinline__ void compute_tile(const WFrag (&wf)[R][NPC], int base, int Pc, int lane, int G,
                                              const i32x4* lq, const float* ld, const float* ls,
-                                             float (&acc)[GEMV_R][BT]) {
+                                             float (&acc)[R][BT]) {
 #pragma unroll
   for (int i = 0; i < NPC; ++i) {
     const int p = base + 64 * i + lane;
@@ -237,16 +244,15 @@ __device__ __forceinline__ void compute_tile(const WFrag (&wf)[GEMV_R][NPC], int
         xf.slo = ls[b * G + glo];
         xf.shi = ls[b * G + ghi];
 #pragma unroll
-        for (int r = 0; r < GEMV_R; ++r) acc[r][b] += piece_dot<QT>(wf[r][i], xf, p);
+        for (int r = 0; r < R; ++r) acc[r][b] += piece_dot<QT>(wf[r][i], xf, p);
       }
     }
   }
 }
 
-template <int BT>
-__device__ __forceinline__ void epilogue(const GemvParams& P, float (&acc)[GEMV_R][BT], int row0, int N, int b0,
+template <int BT, int R>
+__device__ __forceinline__ void epilogue(const GemvParams& P, float (&acc)[R][BT], int row0, int N, int b0,
                                          int lane) {
-  constexpr int R = GEMV_R;
 #pragma unroll
   for (int r = 0; r < R; ++r)
 #pragma unroll
@@ -280,7 +286,7 @@ __device__ __forceinline__ void epilogue(const GemvParams& P, float (&acc)[GEMV_
           break;
         case EPI_GLU:
           if ((r & 1) == 0) {  // even row = gate, odd row = up
-            const float u = acc[r + 1][b];
+            const float u = acc[(r + 1) % R][b];  // R == 1 never takes this path (dispatch)
             P.y[(long long)bb * P.ldy + (long long)blockIdx.z * P.y_sel_stride + vn / 2] = silu(v) * u;
           }
           break;
@@ -293,7 +299,7 @@ __device__ __forceinline__ void epilogue(const GemvParams& P, float (&acc)[GEMV_
           if (P.bias) v += P.bias[vn];
           float out = v;
           if (which < 2 && d < P.n_rot) {
-            float pv = acc[r ^ 1][b];
+            float pv = acc[(r ^ 1) % R][b];
             if (P.bias) pv += P.bias[vn ^ 1];
             const float ang = (float)P.pos[bb] * P.inv_freq[d >> 1];
             float sn, cs;
@@ -317,9 +323,9 @@ __device__ __forceinline__ void epilogue(const GemvParams& P, float (&acc)[GEMV_
   }
 }
 
-template <int QT, int NPC, int BT, int MODE>
+template <int QT, int NPC, int BT, int MODE, int R>
 __global__ __launch_bounds__(256) void gemv_kernel(GemvParams P) {
-  constexpr int NT = 256, R = GEMV_R, ROWS = GEMV_NW * GEMV_R;
+  constexpr int NT = 256, ROWS = GEMV_NW * R;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const QMat& w = P.w;
   const int K = w.K, N = w.N;
@@ -343,7 +349,7 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvParams P) {
   }
 
   WFrag wa[R][NPC];
-  if (MODE != 2 && tile < n_tiles) load_tile<QT, NPC>(w, row_base, tile * ROWS + wave * R, N, 0, Pc, lane, wa);
+  if (MODE != 2 && tile < n_tiles) load_tile<QT, NPC, R>(w, row_base, tile * ROWS + wave * R, N, 0, Pc, lane, wa);
 
 #pragma unroll
   for (int b = 0; b < BT; ++b) {
@@ -359,6 +365,31 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvParams P) {
   }
   __syncthreads();
 
+  if constexpr (MODE == 0) {
+    // explicit ping-pong (no register copy: a wa = wb copy would force a vmcnt(0) drain every
+    // tile): while one register set is consumed, the other tile's loads are in flight
+    WFrag wb[R][NPC];
+    auto step = [&](WFrag (&cur)[R][NPC], WFrag (&nxt)[R][NPC], int t) {
+      const int row0 = t * ROWS + wave * R;
+      const int next = t + gridDim.x;
+      if (next < n_tiles) load_tile<QT, NPC, R>(w, row_base, next * ROWS + wave * R, N, 0, Pc, lane, nxt);
+      float acc[R][BT];
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int b = 0; b < BT; ++b) acc[r][b] = 0.f;
+      compute_tile<QT, NPC, BT, R>(cur, 0, Pc, lane, G, lq, ld, ls, acc);
+      if (row0 < N) epilogue<BT, R>(P, acc, row0, N, b0, lane);
+    };
+    while (tile < n_tiles) {
+      step(wa, wb, tile);
+      tile += gridDim.x;
+      if (tile >= n_tiles) break;
+      step(wb, wa, tile);
+      tile += gridDim.x;
+    }
+    return;
+  }
   for (; tile < n_tiles; tile += gridDim.x) {
     const int row0 = tile * ROWS + wave * R;
     const int next = tile + gridDim.x;
@@ -367,50 +398,64 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvParams P) {
     for (int r = 0; r < R; ++r)
 #pragma unroll
       for (int b = 0; b < BT; ++b) acc[r][b] = 0.f;
-    if constexpr (MODE == 0) {
-      WFrag wb[R][NPC];
-      if (next < n_tiles) load_tile<QT, NPC>(w, row_base, next * ROWS + wave * R, N, 0, Pc, lane, wb);
-      compute_tile<QT, NPC, BT>(wa, 0, Pc, lane, G, lq, ld, ls, acc);
-#pragma unroll
-      for (int r = 0; r < R; ++r)
-#pragma unroll
-        for (int i = 0; i < NPC; ++i) wa[r][i] = wb[r][i];
-    } else if constexpr (MODE == 1) {
-      compute_tile<QT, NPC, BT>(wa, 0, Pc, lane, G, lq, ld, ls, acc);
-      if (next < n_tiles) load_tile<QT, NPC>(w, row_base, next * ROWS + wave * R, N, 0, Pc, lane, wa);
+    if constexpr (MODE == 1) {
+      compute_tile<QT, NPC, BT, R>(wa, 0, Pc, lane, G, lq, ld, ls, acc);
+      if (next < n_tiles) load_tile<QT, NPC, R>(w, row_base, next * ROWS + wave * R, N, 0, Pc, lane, wa);
     } else {
       for (int base = 0; base < Pc; base += 64 * NPC) {
-        load_tile<QT, NPC>(w, row_base, row0, N, base, Pc, lane, wa);
-        compute_tile<QT, NPC, BT>(wa, base, Pc, lane, G, lq, ld, ls, acc);
+        load_tile<QT, NPC, R>(w, row_base, row0, N, base, Pc, lane, wa);
+        compute_tile<QT, NPC, BT, R>(wa, base, Pc, lane, G, lq, ld, ls, acc);
       }
     }
-    if (row0 < N) epilogue<BT>(P, acc, row0, N, b0, lane);
+    if (row0 < N) epilogue<BT, R>(P, acc, row0, N, b0, lane);
   }
 }
 
-template <int QT, int NPC, int BT, int MODE>
+template <int QT, int NPC, int BT, int MODE, int R = GEMV_R>
 static void launch_t(const GemvParams& P, hipStream_t s) {
   const int N = P.w.N;
-  const int rows_per_block = GEMV_NW * GEMV_R;
+  const int rows_per_block = GEMV_NW * R;
   const int tiles = (N + rows_per_block - 1) / rows_per_block;
   const int by = (P.B + BT - 1) / BT;
   const int bz = P.expert_ids ? P.n_sel : 1;
   // persistent grid: ~2 blocks per CU over all (y, z) slices; each block walks its row tiles
   int gx = tiles;
-  const int cap = 512 / (by * bz) > 0 ? 512 / (by * bz) : 1;
+  const int slots = 256 * g_tune.blocks_per_cu;
+  const int cap = slots / (by * bz) > 0 ? slots / (by * bz) : 1;
   if (gx > cap) gx = cap;
   dim3 grid(gx, by, bz);
   const size_t lds = (size_t)BT * (P.w.K / 16) * 24 + 64;
-  hipLaunchKernelGGL((gemv_kernel<QT, NPC, BT, MODE>), grid, dim3(256), lds, s, P);
+  hipLaunchKernelGGL((gemv_kernel<QT, NPC, BT, MODE, R>), grid, dim3(256), lds, s, P);
 }
 
 template <int QT, int BT>
 static void launch_b(const GemvParams& P, hipStream_t s) {
   const int Pc = P.w.K / 32;
   const int need = (Pc + 63) / 64;
+  // one row per wave doubles the waves in flight and halves each wave's serial dot work; only
+  // the epilogues that pair adjacent rows (GLU gate/up, QKV RoPE) need two rows per wave
+  const bool r1 = BT == 1 && g_tune.r1 && P.epi != EPI_GLU && P.epi != EPI_QKV && need <= 8;
+  if (r1) {
+    switch (need) {
+      case 1: launch_t<QT, 1, BT, 0, 1>(P, s); return;
+      case 2: launch_t<QT, 2, BT, 0, 1>(P, s); return;
+      case 3: launch_t<QT, 3, BT, 0, 1>(P, s); return;
+      case 4: launch_t<QT, 4, BT, 0, 1>(P, s); return;
+      case 5: launch_t<QT, 5, BT, 1, 1>(P, s); return;
+      case 6: launch_t<QT, 6, BT, 1, 1>(P, s); return;
+      case 7: launch_t<QT, 7, BT, 1, 1>(P, s); return;
+      default: launch_t<QT, 8, BT, 1, 1>(P, s); return;
+    }
+  }
   switch (need) {
-    case 1: launch_t<QT, 1, BT, 0>(P, s); break;
-    case 2: launch_t<QT, 2, BT, 0>(P, s); break;
+    case 1:
+      if (BT == 1 && g_tune.rows_per_wave == 4) launch_t<QT, 1, BT, 0, 4>(P, s);
+      else launch_t<QT, 1, BT, 0>(P, s);
+      break;
+    case 2:
+      if (BT == 1 && g_tune.rows_per_wave == 4) launch_t<QT, 2, BT, 0, 4>(P, s);
+      else launch_t<QT, 2, BT, 0>(P, s);
+      break;
     case 3: launch_t<QT, 3, BT, 1>(P, s); break;
     case 4: launch_t<QT, 4, BT, 1>(P, s); break;
     case 5: launch_t<QT, 5, BT, 1>(P, s); break;

@@ -44,6 +44,15 @@ struct GemvParams {
 
 void gemv(const GemvParams& P, hipStream_t s);
 
+// launch-shape knobs for the decode GEMV (tuned on MI355X; see scripts/bench_gemv.py)
+struct GemvTuning {
+  int blocks_per_cu = 3;  // persistent grid = 256 CUs x this (scripts/bench_gemv.py sweep)
+  int rows_per_wave = 2;  // 2 or 4 (K <= 4096 decode kernels)
+  int r1 = 1;             // one row per wave for epilogues without row pairs
+};
+extern GemvTuning g_tune;
+void set_gemv_tuning(int blocks_per_cu, int rows_per_wave, int r1);
+
 // Dequantize rows of a repacked matrix (embedding gather / fp16 copies)
 void embed_rows(const QMat& w, const int* rows, int n, float* out, int ldo, hipStream_t s);
 void dequant_f16(const QMat& w, void* out_f16, hipStream_t s);
@@ -63,7 +72,8 @@ struct AttnParams {
   float* out;                  // [NQ][ldo] fp32
   int ldo;
   float* ws;                   // split workspace: [NQ][H][S][D + 2] fp32
-  int n_splits;
+  int n_splits;                // <= 64
+  int* counters;               // [NQ][n_kv] arrival tickets, zero before first use (self re-arming)
 };
 void attention_decode(const AttnParams& P, hipStream_t s);
 size_t attention_ws_floats(int NQ, int H, int D, int n_splits);

@@ -53,6 +53,7 @@ struct Workspace {
   int* eids = nullptr;       // [maxB][n_sel]
   float* ew = nullptr;       // [maxB][n_sel]
   float* attn_ws = nullptr;  // split-K workspace
+  int* attn_cnt = nullptr;   // [maxB][Hkv] split arrival tickets (zero-initialised)
   int max_B = 0;
   int n_splits = 1;
 };

@@ -55,7 +55,7 @@ class NativeExec:
             e.set_layer(i, d)
         e.set_workspace(dict(resid=p(r.resid), qbuf=p(r.qbuf), abuf=p(r.abuf), hbuf=p(r.hbuf), ypart=p(r.ypart),
                              lbuf=p(r.lbuf), rlogits=p(r.rlogits), eids=p(r.eids), ew=p(r.ew),
-                             attn_ws=p(r.attn_ws), max_B=r.max_batch, n_splits=1))
+                             attn_ws=p(r.attn_ws), attn_cnt=p(r.attn_cnt), max_B=r.max_batch, n_splits=1))
         self.inputs = dict(tokens=p(r.d_tokens), pos=p(r.d_pos), slot=p(r.d_slot), q_len=p(r.d_qlen),
                            q_seq=p(r.d_qseq), block_table=p(r.d_block_table), max_blocks=r.max_blocks,
                            bs=r.block_size, logits=p(r.logits))
@@ -118,6 +118,7 @@ class Runner:
         self.ew = torch.zeros(max_batch, ksel, **f32)
         ws = max(self._ws_floats(B) for B in range(1, max_batch + 1))
         self.attn_ws = torch.zeros(max(ws, 1), **f32)
+        self.attn_cnt = torch.zeros(max_batch * loc["Hkv"], **i32)  # self re-arming tickets
         self.logits = torch.zeros(max_batch, Vl, **f32)
         self.full_logits = torch.zeros(max_batch, cfg.n_vocab, **f32) if tp_size > 1 else self.logits
         # step inputs, packed so one H2D copy refreshes (pos, slot, q_len, q_seq, logit_idx)

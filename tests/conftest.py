@@ -1,5 +1,6 @@
 import os
 import sys
+import zlib
 
 import pytest
 
@@ -40,6 +41,6 @@ def tiny_models(tmp_path_factory):
                      ("tiny-llama-q40", FileType.MOSTLY_Q4_0)]:
         base = name.replace("-q8", "").replace("-q40", "")
         p = str(d / f"{name}.gguf")
-        write_random_gguf(p, preset(base), ft, seed=hash(name) % 1000, quantize_from_float=True)
+        write_random_gguf(p, preset(base), ft, seed=zlib.crc32(name.encode()) % 1000, quantize_from_float=True)
         out[name] = p
     return out

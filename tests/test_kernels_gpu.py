@@ -154,9 +154,14 @@ def test_attention_paged(D, G, splits):
     qlen = torch.tensor(lens, device="cuda", dtype=torch.int32)
     out = torch.zeros(NQ, H * D, device="cuda")
     ws = torch.zeros(max(1, C().attention_ws_floats(NQ, H, D, splits)), device="cuda")
+    cnt = torch.zeros(NQ * Hkv, device="cuda", dtype=torch.int32)
     scale = 1 / math.sqrt(D)
-    C().attention(q.data_ptr(), H * D, kc.data_ptr(), vc.data_ptr(), bt.data_ptr(), max_blocks, 0, qlen.data_ptr(),
-                  NQ, H, Hkv, D, bs, scale, 0, out.data_ptr(), H * D, ws.data_ptr(), splits, S())
+    for rep in range(3):  # tickets must re-arm themselves between launches
+        out.zero_()
+        C().attention(q.data_ptr(), H * D, kc.data_ptr(), vc.data_ptr(), bt.data_ptr(), max_blocks, 0,
+                      qlen.data_ptr(), NQ, H, Hkv, D, bs, scale, 0, out.data_ptr(), H * D, ws.data_ptr(), splits,
+                      cnt.data_ptr(), S())
+    assert int(cnt.abs().sum()) == 0
     for i, n in enumerate(lens):
         t = torch.arange(n, device="cuda")
         kk = kc[bt[i][t // bs].long(), :, t % bs].float().repeat_interleave(G, 1)
