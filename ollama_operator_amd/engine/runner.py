@@ -236,6 +236,27 @@ class Runner:
             self.forward(B, 1 if (last and want_logits) else 0, use_idx=True)
         s.tokens.extend(tokens)
 
+    def embed(self, tokens: list[int]) -> np.ndarray:
+        """Mean-pooled final hidden state (after the output norm) -- /api/embed, /v1/embeddings."""
+        sid = self.new_sequence()
+        try:
+            acc, n = None, 0
+            for c0 in range(0, len(tokens), self.max_batch):
+                chunk = tokens[c0:c0 + self.max_batch]
+                self.prefill(sid, chunk, want_logits=False)
+                h = self.resid[:len(chunk)].float()
+                if self.cfg.arch == "phi2":
+                    h = torch.nn.functional.layer_norm(h, (h.shape[-1],), self.w.out_norm, self.w.out_norm_b,
+                                                       self.cfg.norm_eps)
+                else:
+                    h = h * torch.rsqrt(h.pow(2).mean(-1, keepdim=True) + self.cfg.norm_eps) * self.w.out_norm
+                s = h.sum(0)
+                acc = s if acc is None else acc + s
+                n += len(chunk)
+            return (acc / max(n, 1)).cpu().numpy()
+        finally:
+            self.free_sequence(sid)
+
     # ------------------------------------------------------------------ sampling
     def _set_sampler(self, row: int, o: SamplingOptions, history: list[int], seed: int):
         self.s_temp[row] = o.temperature

@@ -1,0 +1,270 @@
+"""Loaded-model manager: lazy load on first request (reference SURVEY.md §2.4 "Lazy load
+semantics": readiness only checks /api/tags), keep-alive eviction, per-model request
+serialisation, stop sequences, and the Ollama timing fields (`*_duration` in ns) that clients --
+and our benchmark -- read tokens/s from (eval_count / eval_duration).
+"""
+from __future__ import annotations
+
+import os
+import threading
+import time
+from dataclasses import dataclass, field
+from typing import Any, Iterator
+
+import numpy as np
+
+from ..engine.sampling import SamplingOptions
+from ..tokenizer import StreamDecoder, Tokenizer, from_gguf_metadata
+from .store import MT_SYSTEM, MT_TEMPLATE, ModelName, ModelStore, StoreError
+
+DEFAULT_KEEP_ALIVE = float(os.environ.get("OLLAMA_KEEP_ALIVE_SECONDS", "300"))
+DEFAULT_NUM_CTX = int(os.environ.get("OLLAMA_CONTEXT_LENGTH", "2048"))
+
+
+def parse_keep_alive(v: Any) -> float:
+    """Ollama keep_alive: number of seconds, duration string ("5m", "1h", "30s"), <0 = forever."""
+    if v is None:
+        return DEFAULT_KEEP_ALIVE
+    if isinstance(v, (int, float)):
+        return float("inf") if v < 0 else float(v)
+    s = str(v).strip()
+    try:
+        f = float(s)
+        return float("inf") if f < 0 else f
+    except ValueError:
+        pass
+    total = 0.0
+    import re
+    for num, unit in re.findall(r"(-?\d+(?:\.\d+)?)(ms|s|m|h)", s):
+        total += float(num) * {"ms": 1e-3, "s": 1, "m": 60, "h": 3600}[unit]
+    return float("inf") if total < 0 else total
+
+
+@dataclass
+class LoadedModel:
+    name: ModelName
+    digest: str
+    path: str
+    runner: Any
+    tokenizer: Tokenizer
+    template: str | None
+    system: str | None
+    params: dict
+    num_ctx: int
+    size: int
+    load_duration_ns: int
+    expires_at: float = 0.0
+    lock: threading.Lock = field(default_factory=threading.Lock)
+    sid: int | None = None
+
+
+@dataclass
+class GenResult:
+    text: str = ""
+    done_reason: str = "stop"
+    prompt_eval_count: int = 0
+    prompt_eval_duration: int = 0
+    eval_count: int = 0
+    eval_duration: int = 0
+    load_duration: int = 0
+    total_duration: int = 0
+    context: list = field(default_factory=list)
+
+
+class ModelManager:
+    def __init__(self, store: ModelStore, device: str | None = None, max_loaded: int | None = None):
+        self.store = store
+        self.device = device
+        self.max_loaded = max_loaded or int(os.environ.get("OLLAMA_MAX_LOADED_MODELS", "3"))
+        self.loaded: dict[str, LoadedModel] = {}
+        self.mu = threading.Lock()
+        self.stats = {"requests": 0, "tokens_generated": 0, "prompt_tokens": 0}
+
+    # ------------------------------------------------------------------ loading
+    def _evict_expired(self):
+        now = time.time()
+        for k, lm in list(self.loaded.items()):
+            if lm.expires_at <= now and not lm.lock.locked():
+                self._unload(k)
+
+    def _unload(self, key: str):
+        lm = self.loaded.pop(key, None)
+        if lm is not None:
+            del lm.runner
+            try:
+                import torch
+                if torch.cuda.is_available():
+                    torch.cuda.empty_cache()
+            except Exception:
+                pass
+
+    def unload(self, model: str) -> bool:
+        with self.mu:
+            key = str(ModelName.parse(model))
+            if key in self.loaded:
+                self._unload(key)
+                return True
+            return False
+
+    def get(self, model: str, keep_alive: Any = None, num_ctx: int | None = None) -> LoadedModel:
+        name = ModelName.parse(model)
+        key = str(name)
+        ka = parse_keep_alive(keep_alive)
+        with self.mu:
+            self._evict_expired()
+            m = self.store.read_manifest(name)
+            lm = self.loaded.get(key)
+            want_ctx = num_ctx or int(self.store.params(m).get("num_ctx", DEFAULT_NUM_CTX))
+            if lm is not None and (lm.digest != m.digest or want_ctx > lm.num_ctx):
+                self._unload(key)
+                lm = None
+            if lm is None:
+                while len(self.loaded) >= self.max_loaded:
+                    oldest = min(self.loaded.values(), key=lambda x: x.expires_at)
+                    self._unload(str(oldest.name))
+                lm = self._load(name, m, want_ctx)
+                self.loaded[key] = lm
+            lm.expires_at = time.time() + ka
+            return lm
+
+    def _load(self, name: ModelName, m, num_ctx: int) -> LoadedModel:
+        from ..engine.runner import Runner
+        from ..gguf import read_gguf
+        t0 = time.perf_counter()
+        path = self.store.model_blob(name)
+        g = read_gguf(path)
+        tok = from_gguf_metadata(g.metadata)
+        g.close()
+        ctx_cap = int(os.environ.get("OMX_MAX_CTX", "0")) or None
+        runner = Runner(path, device=self.device, max_batch=int(os.environ.get("OMX_PREFILL_CHUNK", "64")),
+                        max_seqs=2, ctx=min(num_ctx, ctx_cap) if ctx_cap else num_ctx)
+        return LoadedModel(name=name, digest=m.digest, path=path, runner=runner, tokenizer=tok,
+                           template=self.store.text_layer(m, MT_TEMPLATE), system=self.store.text_layer(m, MT_SYSTEM),
+                           params=self.store.params(m), num_ctx=runner.ctx, size=os.path.getsize(path),
+                           load_duration_ns=int((time.perf_counter() - t0) * 1e9))
+
+    def ps(self) -> list[LoadedModel]:
+        with self.mu:
+            self._evict_expired()
+            return list(self.loaded.values())
+
+    # ------------------------------------------------------------------ generation
+    def options(self, lm: LoadedModel, req_opts: dict | None) -> tuple[SamplingOptions, dict]:
+        merged = dict(lm.params)
+        merged.update(req_opts or {})
+        return SamplingOptions.from_options(merged), merged
+
+    def generate(self, lm: LoadedModel, prompt_ids: list[int], req_opts: dict | None, load_ns: int,
+                 t_start: float) -> Iterator[tuple[str, GenResult | None]]:
+        """Yields (text_piece, None) while generating and ("", GenResult) at the end."""
+        from ..engine.runner import StepTimes
+        so, merged = self.options(lm, req_opts)
+        stops = merged.get("stop") or []
+        if isinstance(stops, str):
+            stops = [stops]
+        num_predict = int(merged.get("num_predict", -1))
+        runner = lm.runner
+        room = runner.ctx - 1
+        if len(prompt_ids) > room:  # Ollama truncates the prompt from the front (keeps num_keep)
+            keep = int(merged.get("num_keep", 4))
+            prompt_ids = prompt_ids[:keep] + prompt_ids[len(prompt_ids) - (room - keep) // 2:]
+        max_new = runner.ctx - len(prompt_ids)
+        if num_predict >= 0:
+            max_new = min(max_new, num_predict)
+        res = GenResult(load_duration=load_ns, context=list(prompt_ids))
+        if max_new <= 0:
+            res.done_reason = "length"
+            res.total_duration = int((time.perf_counter() - t_start) * 1e9)
+            yield "", res
+            return
+        with lm.lock:
+            if lm.sid is None:
+                lm.sid = runner.new_sequence()
+            times = StepTimes()
+            dec = StreamDecoder(lm.tokenizer, first=not prompt_ids or prompt_ids[-1] == lm.tokenizer.bos_id)
+            pending = ""
+            out_text = []
+            gen = runner.generate(lm.sid, prompt_ids, so, max_tokens=max_new, times=times)
+            n = 0
+            reason = "length"
+            try:
+                for tid in gen:
+                    n += 1
+                    res.context.append(tid)
+                    if lm.tokenizer.is_eog(tid):
+                        reason = "stop"
+                        break
+                    pending += dec.push(tid)
+                    hit = _find_stop(pending, stops)
+                    if hit is not None:
+                        piece = pending[:hit]
+                        if piece:
+                            out_text.append(piece)
+                            yield piece, None
+                        pending = ""
+                        reason = "stop"
+                        break
+                    safe = _safe_len(pending, stops)
+                    if safe:
+                        piece = pending[:safe]
+                        pending = pending[safe:]
+                        out_text.append(piece)
+                        yield piece, None
+                else:
+                    reason = "length"
+                if reason == "length":
+                    pending += dec.flush()
+                    if pending:
+                        out_text.append(pending)
+                        yield pending, None
+            finally:
+                gen.close()
+        self.stats["requests"] += 1
+        self.stats["tokens_generated"] += n
+        self.stats["prompt_tokens"] += times.prompt_tokens
+        res.text = "".join(out_text)
+        res.done_reason = reason
+        res.prompt_eval_count = times.prompt_tokens or len(prompt_ids)
+        res.prompt_eval_duration = int(times.prompt_s * 1e9)
+        res.eval_count = n
+        res.eval_duration = int(times.gen_s * 1e9)
+        res.total_duration = int((time.perf_counter() - t_start) * 1e9)
+        yield "", res
+
+    def embed(self, lm: LoadedModel, texts: list[str], truncate: bool = True) -> tuple[list[list[float]], int]:
+        total = 0
+        out = []
+        with lm.lock:
+            for t in texts:
+                ids = lm.tokenizer.encode(t)
+                if len(ids) > lm.runner.ctx:
+                    if not truncate:
+                        raise StoreError("input length exceeds context length")
+                    ids = ids[:lm.runner.ctx]
+                total += len(ids)
+                v = lm.runner.embed(ids)
+                n = float(np.linalg.norm(v)) or 1.0
+                out.append([float(x) / n for x in v])
+        return out, total
+
+
+def _find_stop(text: str, stops: list[str]) -> int | None:
+    best = None
+    for s in stops:
+        if not s:
+            continue
+        i = text.find(s)
+        if i >= 0 and (best is None or i < best):
+            best = i
+    return best
+
+
+def _safe_len(text: str, stops: list[str]) -> int:
+    """Length of the prefix that cannot be the start of any stop sequence."""
+    hold = 0
+    for s in stops:
+        for k in range(min(len(s) - 1, len(text)), 0, -1):
+            if text.endswith(s[:k]):
+                hold = max(hold, k)
+                break
+    return len(text) - hold
