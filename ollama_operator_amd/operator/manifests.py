@@ -1,0 +1,213 @@
+"""Render the deployable manifests (reference config/** and dist/install.yaml):
+CRD, RBAC, manager Deployment, samples, kustomize overlays and the single-file installer.
+`python -m ollama_operator_amd.operator.manifests [outdir]` regenerates deploy/; a test checks
+the committed files are current.
+
+Differences from the reference, on purpose: Events RBAC is cluster-wide (reference only grants it
+in the operator namespace); metrics are served directly (no
+kube-rbac-proxy sidecar image); model pods request `amd.com/gpu`.
+"""
+from __future__ import annotations
+
+import os
+import sys
+
+import yaml
+
+from . import api
+
+NAMESPACE = "ollama-operator-system"
+PREFIX = "ollama-operator-"
+OPERATOR_IMAGE = "ollama-operator-amd/operator:latest"
+SERVER_IMAGE = api.DEFAULT_SERVER_IMAGE
+
+
+def _dump(objs: list[dict]) -> str:
+    return "---\n" + "---\n".join(yaml.safe_dump(o, sort_keys=False) for o in objs)
+
+
+def rbac() -> dict[str, list[dict]]:
+    rules = [
+        {"apiGroups": ["apps"], "resources": ["deployments", "statefulsets"],
+         "verbs": ["create", "delete", "get", "list", "patch", "update", "watch"]},
+        {"apiGroups": [""], "resources": ["services", "persistentvolumeclaims"],
+         "verbs": ["create", "delete", "get", "list", "patch", "update", "watch"]},
+        {"apiGroups": [""], "resources": ["persistentvolumes", "namespaces", "pods"], "verbs": ["get", "list", "watch"]},
+        {"apiGroups": ["storage.k8s.io"], "resources": ["storageclasses"], "verbs": ["get", "list", "watch"]},
+        {"apiGroups": [""], "resources": ["events"], "verbs": ["create", "patch"]},
+        {"apiGroups": [api.GROUP], "resources": ["models"],
+         "verbs": ["create", "delete", "get", "list", "patch", "update", "watch"]},
+        {"apiGroups": [api.GROUP], "resources": ["models/finalizers"], "verbs": ["update"]},
+        {"apiGroups": [api.GROUP], "resources": ["models/status"], "verbs": ["get", "patch", "update"]},
+    ]
+    le = [{"apiGroups": [""], "resources": ["configmaps"],
+           "verbs": ["get", "list", "watch", "create", "update", "patch", "delete"]},
+          {"apiGroups": ["coordination.k8s.io"], "resources": ["leases"],
+           "verbs": ["get", "list", "watch", "create", "update", "patch", "delete"]},
+          {"apiGroups": [""], "resources": ["events"], "verbs": ["create", "patch"]}]
+    sa = {"apiVersion": "v1", "kind": "ServiceAccount", "metadata": {"name": "controller-manager", "namespace": "system"}}
+    return {
+        "service_account.yaml": [sa],
+        "role.yaml": [{"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "ClusterRole",
+                       "metadata": {"name": "manager-role"}, "rules": rules}],
+        "role_binding.yaml": [{"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "ClusterRoleBinding",
+                               "metadata": {"name": "manager-rolebinding"},
+                               "roleRef": {"apiGroup": "rbac.authorization.k8s.io", "kind": "ClusterRole",
+                                           "name": "manager-role"},
+                               "subjects": [{"kind": "ServiceAccount", "name": "controller-manager",
+                                             "namespace": "system"}]}],
+        "leader_election_role.yaml": [{"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "Role",
+                                       "metadata": {"name": "leader-election-role", "namespace": "system"},
+                                       "rules": le}],
+        "leader_election_role_binding.yaml": [{
+            "apiVersion": "rbac.authorization.k8s.io/v1", "kind": "RoleBinding",
+            "metadata": {"name": "leader-election-rolebinding", "namespace": "system"},
+            "roleRef": {"apiGroup": "rbac.authorization.k8s.io", "kind": "Role", "name": "leader-election-role"},
+            "subjects": [{"kind": "ServiceAccount", "name": "controller-manager", "namespace": "system"}]}],
+        "model_editor_role.yaml": [{"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "ClusterRole",
+                                    "metadata": {"name": "model-editor-role"},
+                                    "rules": [{"apiGroups": [api.GROUP], "resources": ["models"],
+                                               "verbs": ["create", "delete", "get", "list", "patch", "update",
+                                                         "watch"]},
+                                              {"apiGroups": [api.GROUP], "resources": ["models/status"],
+                                               "verbs": ["get"]}]}],
+        "model_viewer_role.yaml": [{"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "ClusterRole",
+                                    "metadata": {"name": "model-viewer-role"},
+                                    "rules": [{"apiGroups": [api.GROUP], "resources": ["models"],
+                                               "verbs": ["get", "list", "watch"]},
+                                              {"apiGroups": [api.GROUP], "resources": ["models/status"],
+                                               "verbs": ["get"]}]}],
+        "metrics_service.yaml": [{"apiVersion": "v1", "kind": "Service",
+                                  "metadata": {"name": "controller-manager-metrics-service", "namespace": "system",
+                                               "labels": {"control-plane": "controller-manager"}},
+                                  "spec": {"selector": {"control-plane": "controller-manager"},
+                                           "ports": [{"name": "http", "port": 8080, "targetPort": 8080,
+                                                      "protocol": "TCP"}]}}],
+    }
+
+
+def manager() -> list[dict]:
+    ns = {"apiVersion": "v1", "kind": "Namespace",
+          "metadata": {"name": "system", "labels": {"control-plane": "controller-manager"}}}
+    dep = {
+        "apiVersion": "apps/v1", "kind": "Deployment",
+        "metadata": {"name": "controller-manager", "namespace": "system",
+                     "labels": {"control-plane": "controller-manager"}},
+        "spec": {
+            "replicas": 1,
+            "selector": {"matchLabels": {"control-plane": "controller-manager"}},
+            "template": {
+                "metadata": {"labels": {"control-plane": "controller-manager"},
+                             "annotations": {"kubectl.kubernetes.io/default-container": "manager"}},
+                "spec": {
+                    "securityContext": {"runAsNonRoot": True},
+                    "serviceAccountName": "controller-manager",
+                    "terminationGracePeriodSeconds": 10,
+                    "containers": [{
+                        "name": "manager", "image": OPERATOR_IMAGE,
+                        "command": ["python3", "-m", "ollama_operator_amd.operator"],
+                        "args": ["--leader-elect", "--health-probe-bind-address=:8081",
+                                 "--metrics-bind-address=:8080"],
+                        "env": [{"name": "OMX_SERVER_IMAGE", "value": SERVER_IMAGE},
+                                {"name": "POD_NAMESPACE", "valueFrom": {"fieldRef": {"fieldPath": "metadata.namespace"}}}],
+                        "ports": [{"containerPort": 8080, "name": "metrics"}],
+                        "securityContext": {"allowPrivilegeEscalation": False, "capabilities": {"drop": ["ALL"]}},
+                        "livenessProbe": {"httpGet": {"path": "/healthz", "port": 8081},
+                                          "initialDelaySeconds": 15, "periodSeconds": 20},
+                        "readinessProbe": {"httpGet": {"path": "/readyz", "port": 8081},
+                                           "initialDelaySeconds": 5, "periodSeconds": 10},
+                        "resources": {"limits": {"cpu": "500m", "memory": "256Mi"},
+                                      "requests": {"cpu": "10m", "memory": "64Mi"}},
+                    }],
+                },
+            },
+        },
+    }
+    return [ns, dep]
+
+
+def samples() -> dict[str, list[dict]]:
+    def m(name, image, **spec):
+        return {"apiVersion": api.API_VERSION, "kind": "Model",
+                "metadata": {"name": name, "labels": {"app.kubernetes.io/name": "model"}},
+                "spec": {"image": image, **spec}}
+    return {
+        "ollama_v1_model.yaml": [m("model-sample", "phi")],
+        "llama2_7b_mi355x.yaml": [m("llama2-7b", "llama2:7b-chat-q4_K_M", numCtx=4096)],
+        "mistral_7b_dp8.yaml": [m("mistral", "mistral", replicas=8)],
+        "llama2_70b_tp8.yaml": [m("llama2-70b", "llama2:70b", tensorParallelSize=8)],
+        "mixtral_8x7b.yaml": [m("mixtral", "mixtral:8x7b", tensorParallelSize=2)],
+        "synthetic_demo.yaml": [m("synthetic-llama", "synthetic/tiny-llama:q4_k_m",
+                                  resources={"limits": {"cpu": "2", "memory": "4Gi"}})],
+    }
+
+
+def kustomizations() -> dict[str, dict]:
+    return {
+        "config/default/kustomization.yaml": {
+            "namespace": NAMESPACE, "namePrefix": PREFIX,
+            "resources": ["../crd", "../rbac", "../manager"]},
+        "config/crd/kustomization.yaml": {"resources": ["bases/ollama.ayaka.io_models.yaml"]},
+        "config/rbac/kustomization.yaml": {"resources": sorted(rbac())},
+        "config/manager/kustomization.yaml": {
+            "resources": ["manager.yaml"],
+            "images": [{"name": OPERATOR_IMAGE.split(":")[0], "newName": OPERATOR_IMAGE.split(":")[0],
+                        "newTag": "latest"}]},
+        "config/samples/kustomization.yaml": {"resources": sorted(samples())},
+    }
+
+
+def _prefixed(objs: list[dict]) -> list[dict]:
+    """Apply the default overlay (namespace + namePrefix) for the single-file installer."""
+    out = []
+    for o in objs:
+        o = yaml.safe_load(yaml.safe_dump(o))
+        kind = o["kind"]
+        md = o["metadata"]
+        if kind == "Namespace":
+            md["name"] = NAMESPACE
+        elif kind != "CustomResourceDefinition":
+            md["name"] = PREFIX + md["name"]
+            if kind not in ("ClusterRole", "ClusterRoleBinding"):
+                md["namespace"] = NAMESPACE
+        if "roleRef" in o:
+            o["roleRef"]["name"] = PREFIX + o["roleRef"]["name"]
+        for s in o.get("subjects", []):
+            s["name"] = PREFIX + s["name"]
+            s["namespace"] = NAMESPACE
+        if kind == "Deployment":
+            o["spec"]["template"]["spec"]["serviceAccountName"] = PREFIX + "controller-manager"
+        out.append(o)
+    return out
+
+
+def render_all() -> dict[str, str]:
+    files: dict[str, str] = {"config/crd/bases/ollama.ayaka.io_models.yaml": _dump([api.crd()])}
+    for n, objs in rbac().items():
+        files[f"config/rbac/{n}"] = _dump(objs)
+    files["config/manager/manager.yaml"] = _dump(manager())
+    for n, objs in samples().items():
+        files[f"config/samples/{n}"] = _dump(objs)
+    for n, k in kustomizations().items():
+        files[n] = yaml.safe_dump({"apiVersion": "kustomize.config.k8s.io/v1beta1", "kind": "Kustomization", **k},
+                                  sort_keys=False)
+    allobjs = [manager()[0], api.crd()] + [o for objs in rbac().values() for o in objs] + [manager()[1]]
+    files["dist/install.yaml"] = _dump(_prefixed(allobjs))
+    return files
+
+
+def write(outdir: str) -> list[str]:
+    written = []
+    for rel, text in render_all().items():
+        p = os.path.join(outdir, rel)
+        os.makedirs(os.path.dirname(p), exist_ok=True)
+        with open(p, "w") as f:
+            f.write(text)
+        written.append(p)
+    return written
+
+
+if __name__ == "__main__":
+    out = sys.argv[1] if len(sys.argv) > 1 else os.path.join(os.path.dirname(__file__), "..", "..", "deploy")
+    for p in write(out):
+        print(p)

@@ -66,6 +66,17 @@ def create_app(store: ModelStore | None = None, manager: ModelManager | None = N
     app.state.manager = manager
     metrics = _Metrics()
 
+    preload = os.environ.get("OMX_PRELOAD")
+    if preload:  # operator-managed model pods load weights at start-up (the probe stays /api/tags)
+        import threading
+
+        def _preload():
+            try:
+                manager.get(preload, os.environ.get("OLLAMA_KEEP_ALIVE", "-1"))
+            except Exception as e:  # noqa: BLE001 - a failed preload retries lazily on first request
+                print(f"preload of {preload} failed: {e}", flush=True)
+        threading.Thread(target=_preload, daemon=True).start()
+
     @app.get("/")
     @app.head("/")
     def root():
