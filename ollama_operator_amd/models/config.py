@@ -133,6 +133,15 @@ PRESETS: dict[str, ModelConfig] = {
     "tiny-phi2": ModelConfig(name="tiny-phi2", arch="phi2", n_vocab=512, n_embd=256, n_layer=2,
                              n_head=4, n_head_kv=4, n_ff=1024, n_rot=32, rope_mode=ROPE_NEOX,
                              ctx_len=256, bos_id=0, eos_id=0),
+    # tensor-parallel test shapes: every row-parallel K spans >= 2 super-blocks per rank at TP=2
+    "tiny-llama-tp": ModelConfig(name="tiny-llama-tp", n_vocab=512, n_embd=1024, n_layer=2, n_head=16,
+                                 n_head_kv=4, n_ff=1024, n_rot=64, ctx_len=256),
+    "tiny-phi2-tp": ModelConfig(name="tiny-phi2-tp", arch="phi2", n_vocab=512, n_embd=1024, n_layer=2,
+                                n_head=16, n_head_kv=16, n_ff=2048, n_rot=32, rope_mode=ROPE_NEOX,
+                                ctx_len=256, bos_id=0, eos_id=0),
+    "tiny-mixtral-tp": ModelConfig(name="tiny-mixtral-tp", n_vocab=512, n_embd=1024, n_layer=2, n_head=16,
+                                   n_head_kv=4, n_ff=1024, n_rot=64, ctx_len=256, n_expert=4,
+                                   n_expert_used=2),
 }
 
 
