@@ -149,16 +149,38 @@ const TensorEntry& GGUFMap::get(const std::string& name) const {
   return tensors_[it->second];
 }
 
-// stream geometry per row for K weights: bytes per row of each stream
+// Stream geometry (layout v2, see ollama_operator_amd/quant.py "device repack"): K padded to SB
+// super-blocks of 256; codes piece-major across super-blocks, scales per super-block.
 static void stream_bytes(int qt, int64_t K, int64_t out[4]) {
+  const int64_t SB = (K + 255) / 256;
   out[0] = out[1] = out[2] = out[3] = 0;
   switch (qt) {
-    case 12: out[0] = K / 2; out[1] = K / 16; break;
-    case 14: out[0] = K / 2; out[1] = K / 4; out[2] = K / 16; out[3] = K / 128; break;
-    case 2: out[0] = K / 2; out[1] = K / 16; break;
-    case 8: out[0] = K; out[1] = K / 16; break;
+    case 12: out[0] = 128 * SB; out[1] = 16 * SB; break;
+    case 14: out[0] = 128 * SB; out[1] = 64 * SB; out[2] = 16 * SB; out[3] = 2 * SB; break;
+    case 2: out[0] = 128 * SB; out[1] = 16 * SB; break;
+    case 8: out[0] = 256 * SB; out[1] = 16 * SB; break;
     default: throw std::runtime_error("repack: unsupported type");
   }
+}
+
+static inline void copy_xor80(uint8_t* d, const uint8_t* s) {  // high nibble -> signed (n - 8)
+  for (int i = 0; i < 16; ++i) d[i] = s[i] ^ 0x80;
+}
+
+// Q6_K high bits of one super-block (64 B, ggml order) -> 8 pieces x (H0 | H1), 8 B each.
+static void q6k_split_qh(const uint8_t* qh, uint8_t* dst, int64_t piece_stride) {
+  for (int n = 0; n < 2; ++n)
+    for (int sub = 0; sub < 4; ++sub) {
+      uint8_t o[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      for (int half = 0; half < 2; ++half) {
+        const int f = (sub >> 1) + 2 * half;
+        for (int i = 0; i < 16; ++i) {
+          const int bits = (qh[n * 32 + (sub & 1) * 16 + i] >> (2 * f)) & 3;
+          o[half * 4 + (i & 3)] |= (uint8_t)(bits << (2 * (i >> 2)));
+        }
+      }
+      std::memcpy(dst + (4 * n + sub) * piece_stride, o, 8);
+    }
 }
 
 void repack_rows(const uint8_t* src, int qtype, int64_t K_src, const int64_t* rows, const int64_t* dst_rows,
@@ -168,6 +190,7 @@ void repack_rows(const uint8_t* src, int qtype, int64_t K_src, const int64_t* ro
   const int64_t nblk_src = K_src / blk;
   if (kb0 < 0 || kb1 > nblk_src || kb0 >= kb1) throw std::runtime_error("repack: bad K block range");
   const int64_t K = (kb1 - kb0) * blk;
+  const int64_t SB = (K + 255) / 256;
   int64_t sb[4];
   stream_bytes(qtype, K, sb);
   const int64_t row_bytes = nblk_src * nb;
@@ -181,24 +204,28 @@ void repack_rows(const uint8_t* src, int qtype, int64_t K_src, const int64_t* ro
       uint8_t* d3 = dst[3] ? dst[3] + o * sb[3] : nullptr;
       for (int64_t b = 0; b < kb1 - kb0; ++b, s += nb) {
         switch (qtype) {
-          case 12:  // d,dmin,scales | qs
+          case 12:  // d,dmin,scales | qs (8 pieces)
             std::memcpy(d1 + 16 * b, s, 16);
-            std::memcpy(d0 + 128 * b, s + 16, 128);
+            for (int t = 0; t < 8; ++t) copy_xor80(d0 + (t * SB + b) * 16, s + 16 + 16 * t);
             break;
           case 14:  // ql | qh | sc | d
-            std::memcpy(d0 + 128 * b, s, 128);
-            std::memcpy(d1 + 64 * b, s + 128, 64);
+            for (int t = 0; t < 8; ++t) std::memcpy(d0 + (t * SB + b) * 16, s + 16 * t, 16);
+            q6k_split_qh(s + 128, d1 + b * 8, SB * 8);
             std::memcpy(d2 + 16 * b, s + 192, 16);
             std::memcpy(d3 + 2 * b, s + 208, 2);
             break;
-          case 2:  // d | qs
-            std::memcpy(d1 + 2 * b, s, 2);
-            std::memcpy(d0 + 16 * b, s + 2, 16);
+          case 2: {  // d | qs ; 32-weight block b = piece (b & 7) of super-block b >> 3
+            const int64_t g = b >> 3, t = b & 7;
+            std::memcpy(d1 + 16 * g + 2 * t, s, 2);
+            copy_xor80(d0 + (t * SB + g) * 16, s + 2);
             break;
-          case 8:  // d | qs
-            std::memcpy(d1 + 2 * b, s, 2);
-            std::memcpy(d0 + 32 * b, s + 2, 32);
+          }
+          case 8: {
+            const int64_t g = b >> 3, t = b & 7;
+            std::memcpy(d1 + 16 * g + 2 * t, s, 2);
+            std::memcpy(d0 + (t * SB + g) * 32, s + 2, 32);
             break;
+          }
         }
       }
     }

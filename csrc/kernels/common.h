@@ -84,20 +84,24 @@ __device__ __forceinline__ float block_max(float v, float* red) {
 }
 
 
-// Row stream strides in bytes for a given K.
-__device__ __forceinline__ long long qs_row_bytes(int qt, int K) { return qt == QT_Q8_0 ? K : K / 2; }
+// Layout v2 geometry (ollama_operator_amd/quant.py "device repack"): SB super-blocks of 256 per
+// row (K padded), codes piece-major: piece t of super-block sb at byte (t * SB + sb) * piece_bytes.
+__device__ __forceinline__ int n_sb(int K) { return (K + 255) >> 8; }
 
-// Dequantize one 32-weight "piece" p of row `row` into two groups of 16 floats (lo, hi) and their
-// offsets (in weights) within the row. Used by the embedding gather and the fp16 dequant kernels.
+// Dequantize piece p (= 8 * sb + t, natural order) of row `row` into two groups of 16 floats
+// (lo, hi) and their offsets (in weights) within the row. Used by the embedding gather and the fp16
+// dequant kernels (the GEMV decodes pieces itself, see gemv.hip).
 __device__ inline void dequant_piece(const QMat& w, long long row, int p, float* lo, float* hi,
                                      int& off_lo, int& off_hi) {
-  const int K = w.K;
+  const int SB = n_sb(w.K);
+  const int sb = p >> 3, t = p & 7;
+  const long long pi = (long long)t * SB + sb;
   if (w.qtype == QT_Q4_K) {
-    const int sb = p >> 3, t = p & 7, c = t >> 1, h = t & 1;
+    const int c = t >> 1, h = t & 1;
     off_lo = 256 * sb + 64 * c + 16 * h;
     off_hi = off_lo + 32;
-    const u32x4 q = *(const u32x4*)(w.s0 + row * (K / 2) + 16LL * p);
-    const u32x4 m = *(const u32x4*)(w.s1 + row * (K / 16) + 16LL * sb);
+    const u32x4 q = *(const u32x4*)(w.s0 + row * SB * 128 + 16 * pi) ^ 0x80808080u;
+    const u32x4 m = *(const u32x4*)(w.s1 + row * SB * 16 + 16LL * sb);
     const float d = h2f(m.x & 0xFFFF), dmin = h2f(m.x >> 16);
     float sc[2], mn[2];
 #pragma unroll
@@ -117,27 +121,27 @@ __device__ inline void dequant_piece(const QMat& w, long long row, int p, float*
       hi[i] = sc[1] * (float)(byte >> 4) - mn[1];
     }
   } else if (w.qtype == QT_Q6_K) {
-    const int sb = p >> 3, t = p & 7, n = t >> 2, sub = t & 3;
+    const int n = t >> 2, sub = t & 3;
     off_lo = 256 * sb + 128 * n + 16 * sub;
     off_hi = off_lo + 64;
-    const u32x4 ql = *(const u32x4*)(w.s0 + row * (K / 2) + 16LL * p);
-    const u32x4 qh = *(const u32x4*)(w.s1 + row * (K / 4) + 64LL * sb + 32 * n + 16 * (sub & 1));
-    const int8_t* sc = (const int8_t*)(w.s2 + row * (K / 16) + 16LL * sb + 8 * n);
-    const float d = h2f(*(const uint16_t*)(w.s3 + row * (K / 128) + 2LL * sb));
-    const float slo = d * (float)sc[sub], shi = d * (float)sc[4 + sub];
-    const int shl = sub < 2 ? 0 : 2, shh = sub < 2 ? 4 : 6;
-    const unsigned L[4] = {ql.x, ql.y, ql.z, ql.w}, H[4] = {qh.x, qh.y, qh.z, qh.w};
+    const u32x4 ql = *(const u32x4*)(w.s0 + row * SB * 128 + 16 * pi);
+    const u32x2 qh = *(const u32x2*)(w.s1 + row * SB * 64 + 8 * pi);
+    const int8_t* sc = (const int8_t*)(w.s2 + row * SB * 16 + 16LL * sb);
+    const float d = h2f(*(const uint16_t*)(w.s3 + row * SB * 2 + 2LL * sb));
+    const float slo = d * (float)sc[8 * n + sub], shi = d * (float)sc[8 * n + sub + 4];
+    const unsigned L[4] = {ql.x, ql.y, ql.z, ql.w};
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      const unsigned lb = (L[i >> 2] >> (8 * (i & 3))) & 0xFF, hb = (H[i >> 2] >> (8 * (i & 3))) & 0xFF;
-      lo[i] = slo * (float)((int)((lb & 0xF) | (((hb >> shl) & 3) << 4)) - 32);
-      hi[i] = shi * (float)((int)((lb >> 4) | (((hb >> shh) & 3) << 4)) - 32);
+      const unsigned lb = (L[i >> 2] >> (8 * (i & 3))) & 0xFF;
+      const int sh = 8 * (i & 3) + 2 * (i >> 2);  // field (i >> 2) of byte (i & 3)
+      lo[i] = slo * (float)((int)((lb & 0xF) | (((qh.x >> sh) & 3) << 4)) - 32);
+      hi[i] = shi * (float)((int)((lb >> 4) | (((qh.y >> sh) & 3) << 4)) - 32);
     }
   } else if (w.qtype == QT_Q4_0) {
-    off_lo = 32 * p;
+    off_lo = 256 * sb + 32 * t;
     off_hi = off_lo + 16;
-    const u32x4 q = *(const u32x4*)(w.s0 + row * (K / 2) + 16LL * p);
-    const float d = h2f(*(const uint16_t*)(w.s1 + row * (K / 16) + 2LL * p));
+    const u32x4 q = *(const u32x4*)(w.s0 + row * SB * 128 + 16 * pi) ^ 0x80808080u;
+    const float d = h2f(*(const uint16_t*)(w.s1 + row * SB * 16 + 16LL * sb + 2 * t));
     const unsigned qq[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
@@ -146,10 +150,10 @@ __device__ inline void dequant_piece(const QMat& w, long long row, int p, float*
       hi[i] = d * ((float)(byte >> 4) - 8.f);
     }
   } else {  // Q8_0
-    off_lo = 32 * p;
+    off_lo = 256 * sb + 32 * t;
     off_hi = off_lo + 16;
-    const int8_t* q = (const int8_t*)(w.s0 + row * (long long)K + 32LL * p);
-    const float d = h2f(*(const uint16_t*)(w.s1 + row * (K / 16) + 2LL * p));
+    const int8_t* q = (const int8_t*)(w.s0 + row * SB * 256 + 32 * pi);
+    const float d = h2f(*(const uint16_t*)(w.s1 + row * SB * 16 + 16LL * sb + 2 * t));
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       lo[i] = d * (float)q[i];

@@ -1,20 +1,30 @@
-// Fused quantized GEMV for decode (M = batch <= a few rows) on gfx950.
+// Fused quantized GEMV for decode and small batches (M = B <= a few rows) on gfx950.
 //
 // y[b, n] = epilogue( sum_k W[n, k] * norm(x[b, :])[k] )
 //
 // Design (MI355X-first, see SURVEY.md §7.4 hard part 1 and docs/kernels.md):
-//  * Weights are repacked at load into 16-byte-aligned streams (quant.py `repack`), so one lane's
-//    16-B load is always one "piece" = 32 weights (two groups of 16) and a wave's loads coalesce
-//    into whole 1 KiB lines. Register-streamed, never through LDS (cdna_hip_programming.md §5 GEMV
-//    row): every lane issues all its R x NPC loads up front.
-//  * The activation prologue runs once per 256-thread block: x (fp32) is optionally RMS/Layer-
-//    normalised (the norm is FUSED here -- no separate launch), quantised to int8 per 16-element
-//    group with an fp32 scale and group sum, and staged in LDS. Every wave then reads its x
-//    fragments from LDS: x crosses L2 once per block, not once per wave.
-//  * Inner product: v_dot4c_i32_i8 on 4-bit/6-bit/8-bit codes against int8 x; K-quant mins and the
-//    Q4_0/Q6_K zero points are applied with the precomputed group sums.
-//  * Epilogues are fused: residual add, bias, SiLU-GLU (gate/up rows interleaved at load), GELU,
-//    and QKV (RoPE on adjacent row pairs + K/V scatter into the paged fp16 cache).
+//  * Weights use repack layout v2 (ollama_operator_amd/quant.py "device repack"): K padded to SB
+//    super-blocks of 256, codes stored piece-major across super-blocks -- qs[row][t][sb][16 B].
+//  * Lane mapping: a wave = 4 row groups of 16 lanes; lane s of a group owns super-blocks
+//    s, s+16, ... (NSB of them per K chunk) of R rows and walks all 8 pieces t of each. One load
+//    instruction for piece t therefore reads a contiguous 256 B run per row group, and t is a
+//    compile-time constant: the K-quant scales / mins are decoded once per 256 weights, with
+//    constant byte selects (v_cvt_f32_ubyteN), instead of once per 32-weight piece. The previous
+//    lane-per-piece kernel spent ~95 VALU ops per piece-row (rocprofv3 PMC, profiles/r1_pmc):
+//    VALU-bound next to an 8 us HBM floor. This one spends ~30.
+//  * 4-bit codes keep the high nibble signed (byte ^ 0x80 at repack), so `q & 0xF0F0F0F0` feeds
+//    v_dot4_i32_i8 directly (16 * (n - 8)): 2 VALU per dword to unpack both nibbles.
+//  * Activation prologue once per block: x (fp32) optionally RMS/Layer-normalised (fused), int8-
+//    quantised per 16-element group (fp32 scale + group sum for the K-quant mins / zero points),
+//    staged in LDS with one pad slot per super-block (17 slots) so the 16 lanes of a group -- one
+//    super-block apart -- hit distinct banks.
+//  * Weight loads for the first tile are issued before the prologue; persistent blocks prefetch the
+//    next (tile, K chunk) unit into a second register tile when the tile fits (DB), else rely on
+//    other waves for latency hiding.
+//  * Row sums: 16-lane DPP reduction (quad_perm / row_half_mirror / row_mirror), no LDS.
+//  * Epilogues fused: residual add (+ MoE routing weight, atomics for top-k > 1), bias, SiLU-GLU
+//    (gate/up rows interleaved at load), GELU, and QKV (RoPE on adjacent row pairs + fp16 paged KV
+//    scatter). Pair partners come from the same lane (R = 2) or the neighbouring row group (R = 1).
 // Reference parity: the reference delegates all of this to llama.cpp inside `ollama/ollama`
 // (reference pkg/model/pod.go:10-12); numerics are checked against quant.py + an fp32 torch GEMV.
 #include "common.h"
@@ -22,59 +32,30 @@
 
 namespace omx {
 
-// per-type piece geometry --------------------------------------------------------------------
-__device__ __forceinline__ int pieces_per_row(int qt, int K) { return K / 32; }
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
-// 16-group indices (in x) of the lo/hi halves of piece p
-__device__ __forceinline__ void piece_groups(int qt, int p, int& glo, int& ghi) {
-  if (qt == QT_Q4_K) {
-    const int sb = p >> 3, t = p & 7, c = t >> 1, h = t & 1;
-    glo = 16 * sb + 4 * c + h;
-    ghi = glo + 2;
-  } else if (qt == QT_Q6_K) {
-    const int sb = p >> 3, t = p & 7, n = t >> 2, sub = t & 3;
-    glo = 16 * sb + 8 * n + sub;
-    ghi = glo + 4;
-  } else {
-    glo = 2 * p;
-    ghi = 2 * p + 1;
-  }
+constexpr int GEMV_NT = 256;  // 4 waves
+constexpr int XPAD = 17;      // LDS x slots per super-block: 16 groups + 1 pad
+
+GemvTuning g_tune;
+void set_gemv_tuning(int blocks_per_cu, int rows, int) {
+  if (blocks_per_cu > 0) g_tune.blocks_per_cu = blocks_per_cu;
+  if (rows == 1 || rows == 2) g_tune.rows = rows;
 }
 
-struct WFrag {
-  u32x4 a;  // qs / ql / q0
-  u32x4 b;  // meta / qh / q1
-  u32x2 c;  // Q6_K: 8 scale bytes of this half
-  unsigned d;  // fp16 scale bits (Q6_K / Q4_0 / Q8_0)
-};
-
-template <int QT>
-__device__ __forceinline__ void load_wfrag(const QMat& w, long long row, int p, WFrag& f) {
-  const int K = w.K;
-  if constexpr (QT == QT_Q4_K) {
-    f.a = __builtin_nontemporal_load((const u32x4*)(w.s0 + row * (K / 2) + 16LL * p));
-    f.b = *(const u32x4*)(w.s1 + row * (K / 16) + 16LL * (p >> 3));
-  } else if constexpr (QT == QT_Q6_K) {
-    const int sb = p >> 3, t = p & 7, n = t >> 2, sub = t & 3;
-    f.a = __builtin_nontemporal_load((const u32x4*)(w.s0 + row * (K / 2) + 16LL * p));
-    f.b = *(const u32x4*)(w.s1 + row * (K / 4) + 64LL * sb + 32 * n + 16 * (sub & 1));
-    f.c = *(const u32x2*)(w.s2 + row * (K / 16) + 16LL * sb + 8 * n);
-    f.d = *(const uint16_t*)(w.s3 + row * (K / 128) + 2LL * sb);
-  } else if constexpr (QT == QT_Q4_0) {
-    f.a = __builtin_nontemporal_load((const u32x4*)(w.s0 + row * (K / 2) + 16LL * p));
-    f.d = *(const uint16_t*)(w.s1 + row * (K / 16) + 2LL * p);
-  } else {  // Q8_0
-    const u32x4* q = (const u32x4*)(w.s0 + row * (long long)K + 32LL * p);
-    f.a = __builtin_nontemporal_load(q);
-    f.b = __builtin_nontemporal_load(q + 1);
-    f.d = *(const uint16_t*)(w.s1 + row * (K / 16) + 2LL * p);
-  }
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
 }
 
-struct XFrag {
-  i32x4 lo, hi;
-  float dlo, dhi, slo, shi;
-};
+// sum over the 16 lanes of a DPP row; every lane of the row gets the total
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dpp<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp<0x141>(v);  // row_half_mirror
+  v += dpp<0x140>(v);  // row_mirror
+  return v;
+}
 
 __device__ __forceinline__ int dot16(u32x4 q, i32x4 x) {
   int s = sdot4((int)q.x, x.x, 0);
@@ -83,54 +64,194 @@ __device__ __forceinline__ int dot16(u32x4 q, i32x4 x) {
   return sdot4((int)q.w, x.w, s);
 }
 
-template <int QT>
-__device__ __forceinline__ float piece_dot(const WFrag& f, const XFrag& x, int p) {
-  if constexpr (QT == QT_Q4_K) {
-    const u32x4 lo = f.a & 0x0F0F0F0Fu;
-    const u32x4 hi = (f.a >> 4) & 0x0F0F0F0Fu;
-    const float dl = (float)dot16(lo, x.lo), dh = (float)dot16(hi, x.hi);
-    const float d = h2f(f.b.x & 0xFFFF), dmin = h2f(f.b.x >> 16);
-    const int c = (p & 7) >> 1;
-    const int sh = 8 * ((2 * c) & 3);  // j = 2c (lo) and 2c+1 (hi): shifts sh and sh+8
-    const unsigned a0 = (f.b.y >> sh) & 0xFF, b0 = (f.b.z >> sh) & 0xFF, e0 = (f.b.w >> sh) & 0xFF;
-    const unsigned a1 = (f.b.y >> (sh + 8)) & 0xFF, b1 = (f.b.z >> (sh + 8)) & 0xFF,
-                   e1 = (f.b.w >> (sh + 8)) & 0xFF;
-    const bool low = c < 2;
-    const float s0 = (float)(low ? (a0 & 63) : ((e0 & 0xF) | ((a0 >> 6) << 4)));
-    const float m0 = (float)(low ? (b0 & 63) : ((e0 >> 4) | ((b0 >> 6) << 4)));
-    const float s1 = (float)(low ? (a1 & 63) : ((e1 & 0xF) | ((a1 >> 6) << 4)));
-    const float m1 = (float)(low ? (b1 & 63) : ((e1 >> 4) | ((b1 >> 6) << 4)));
-    return d * (s0 * x.dlo * dl + s1 * x.dhi * dh) - dmin * (m0 * x.slo + m1 * x.shi);
-  } else if constexpr (QT == QT_Q6_K) {
-    const int sub = p & 3;
-    const int shl = sub < 2 ? 0 : 2;
-    const u32x4 lo = (f.a & 0x0F0F0F0Fu) | (((f.b >> shl) & 0x03030303u) << 4);
-    const u32x4 hi = ((f.a >> 4) & 0x0F0F0F0Fu) | (((f.b >> (shl + 4)) & 0x03030303u) << 4);
-    const float dl = (float)dot16(lo, x.lo), dh = (float)dot16(hi, x.hi);
-    const unsigned wlo = f.c.x, whi = f.c.y;  // bytes 0..3 and 4..7 of this half's scales
-    const float sl = (float)(int8_t)((wlo >> (8 * sub)) & 0xFF);
-    const float shh = (float)(int8_t)((whi >> (8 * sub)) & 0xFF);
-    const float d = h2f(f.d);
-    return d * (sl * (x.dlo * dl - 32.f * x.slo) + shh * (x.dhi * dh - 32.f * x.shi));
-  } else if constexpr (QT == QT_Q4_0) {
-    const u32x4 lo = f.a & 0x0F0F0F0Fu;
-    const u32x4 hi = (f.a >> 4) & 0x0F0F0F0Fu;
-    const float dl = (float)dot16(lo, x.lo), dh = (float)dot16(hi, x.hi);
-    return h2f(f.d) * (x.dlo * dl + x.dhi * dh - 8.f * (x.slo + x.shi));
-  } else {
-    const float dl = (float)dot16(f.a, x.lo), dh = (float)dot16(f.b, x.hi);
-    return h2f(f.d) * (x.dlo * dl + x.dhi * dh);
+__device__ __forceinline__ float ubyte(unsigned v, int k) { return (float)((v >> (8 * k)) & 0xFF); }
+__device__ __forceinline__ float sbyte(unsigned v, int k) { return (float)(int8_t)((v >> (8 * k)) & 0xFF); }
+__device__ __forceinline__ float f16lo(unsigned v) { return h2f(v & 0xFFFF); }
+__device__ __forceinline__ float f16hi(unsigned v) { return h2f(v >> 16); }
+
+// ---------------------------------------------------------------------------------------------
+// register tile: R rows x NSB super-blocks x 8 pieces of one lane
+template <int QT, int NSB, int R>
+struct WTile {
+  static constexpr bool Q8 = QT == QT_Q8_0, Q6 = QT == QT_Q6_K;
+  u32x4 a[R][NSB][8];                                  // qs / ql / Q8_0 first 16 B
+  u32x4 b[Q8 ? R : 1][Q8 ? NSB : 1][8];                // Q8_0 second 16 B
+  u32x2 h[Q6 ? R : 1][Q6 ? NSB : 1][8];                // Q6_K high bits (H0 | H1)
+  u32x4 m[R][NSB];                                     // super-block scales
+  unsigned d[Q6 ? R : 1][Q6 ? NSB : 1];                // Q6_K super-block scale (fp16)
+};
+
+template <int QT, int NSB, int R>
+__device__ __forceinline__ void load_wtile(const QMat& w, long long row_base, int row0, int N, int SB, int sb0,
+                                           int s, WTile<QT, NSB, R>& T) {
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const long long row = row_base + min(row0 + r, N - 1);
+#pragma unroll
+    for (int i = 0; i < NSB; ++i) {
+      const long long sb = min(sb0 + s + 16 * i, SB - 1);  // clamped: padding lanes re-read, never use
+      if constexpr (QT == QT_Q8_0) {
+        const uint8_t* q = w.s0 + row * SB * 256 + 32 * sb;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          T.a[r][i][t] = __builtin_nontemporal_load((const u32x4*)(q + 32LL * t * SB));
+          T.b[r][i][t] = __builtin_nontemporal_load((const u32x4*)(q + 32LL * t * SB + 16));
+        }
+        T.m[r][i] = *(const u32x4*)(w.s1 + row * SB * 16 + 16 * sb);
+      } else {
+        const uint8_t* q = w.s0 + row * SB * 128 + 16 * sb;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) T.a[r][i][t] = __builtin_nontemporal_load((const u32x4*)(q + 16LL * t * SB));
+        if constexpr (QT == QT_Q6_K) {
+          const uint8_t* hq = w.s1 + row * SB * 64 + 8 * sb;
+#pragma unroll
+          for (int t = 0; t < 8; ++t) T.h[r][i][t] = __builtin_nontemporal_load((const u32x2*)(hq + 8LL * t * SB));
+          T.m[r][i] = *(const u32x4*)(w.s2 + row * SB * 16 + 16 * sb);
+          T.d[r][i] = *(const uint16_t*)(w.s3 + row * SB * 2 + 2 * sb);
+        } else {
+          T.m[r][i] = *(const u32x4*)(w.s1 + row * SB * 16 + 16 * sb);
+        }
+      }
+    }
   }
 }
 
-// --------------------------------------------------------------------------------------------
-// activation prologue: x[b] (fp32) -> (norm) -> int8 groups of 16 in LDS
-// LDS layout per batch slot: i32x4 q[G] | float d[G] | float s[G]   (G = K/16)
+// x fragments of one piece for BT batch rows: int8 codes (lo/hi 16 groups) + {scale, sum}
+template <int BT>
+struct XFr {
+  i32x4 lo[BT], hi[BT];
+  f32x2 fl[BT], fh[BT];
+};
+
+template <int BT>
+__device__ __forceinline__ void load_x(const i32x4* xq, const f32x2* xf, int XS, int slot_lo, int slot_hi,
+                                       XFr<BT>& x) {
+#pragma unroll
+  for (int b = 0; b < BT; ++b) {
+    x.lo[b] = xq[b * XS + slot_lo];
+    x.hi[b] = xq[b * XS + slot_hi];
+    x.fl[b] = xf[b * XS + slot_lo];
+    x.fh[b] = xf[b * XS + slot_hi];
+  }
+}
+
+template <int QT, int NSB, int R, int BT>
+__device__ __forceinline__ void compute_wtile(const WTile<QT, NSB, R>& T, int SB, int sb0, int s, const i32x4* xq,
+                                              const f32x2* xf, int XS, float (&acc)[R][BT]) {
+#pragma unroll
+  for (int i = 0; i < NSB; ++i) {
+    const int sb = sb0 + s + 16 * i;
+    if (sb >= SB) continue;
+    const int xs0 = sb * XPAD;
+    if constexpr (QT == QT_Q4_K) {
+      // w = d*sc*n - dmin*m per 32-weight sub-block; lo nibbles: sub-block 2c, hi: 2c+1 (signed n-8)
+      float d[R], dm[R];
+      unsigned sl[R], ml[R], sh[R], mh[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const u32x4 m = T.m[r][i];
+        d[r] = f16lo(m.x);
+        dm[r] = f16hi(m.x);
+        sl[r] = m.y & 0x3F3F3F3Fu;                                  // scales 0..3
+        ml[r] = m.z & 0x3F3F3F3Fu;                                  // mins 0..3
+        sh[r] = (m.w & 0x0F0F0F0Fu) | ((m.y >> 2) & 0x30303030u);  // scales 4..7
+        mh[r] = ((m.w >> 4) & 0x0F0F0F0Fu) | ((m.z >> 2) & 0x30303030u);
+      }
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        float fsl[R], fml[R], fsh[R], gh[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const unsigned S = c < 2 ? sl[r] : sh[r], M = c < 2 ? ml[r] : mh[r];
+          const int k0 = (2 * c) & 3, k1 = (2 * c + 1) & 3;
+          const float s1 = ubyte(S, k1);
+          fsl[r] = d[r] * ubyte(S, k0);
+          fml[r] = dm[r] * ubyte(M, k0);
+          fsh[r] = (0.0625f * d[r]) * s1;
+          gh[r] = 8.f * d[r] * s1 - dm[r] * ubyte(M, k1);
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int t = 2 * c + h, gl = 4 * c + h;
+          XFr<BT> x;
+          load_x<BT>(xq, xf, XS, xs0 + gl, xs0 + gl + 2, x);
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+            const u32x4 a = T.a[r][i][t];
+            const u32x4 lo = a & 0x0F0F0F0Fu, hi = a & 0xF0F0F0F0u;
+#pragma unroll
+            for (int b = 0; b < BT; ++b) {
+              const float il = (float)dot16(lo, x.lo[b]), ih = (float)dot16(hi, x.hi[b]);
+              acc[r][b] += fsl[r] * (x.fl[b].x * il) + fsh[r] * (x.fh[b].x * ih) - fml[r] * x.fl[b].y +
+                           gh[r] * x.fh[b].y;
+            }
+          }
+        }
+      }
+    } else if constexpr (QT == QT_Q6_K) {
+      // w = d*sc*(q - 32); q = ql nibble | (2 high bits << 4)
+      float dq[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) dq[r] = h2f((uint16_t)T.d[r][i]);
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const int n = t >> 2, sub = t & 3, il_ = 8 * n + sub, ih_ = il_ + 4;
+        XFr<BT> x;
+        load_x<BT>(xq, xf, XS, xs0 + il_, xs0 + ih_, x);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const u32x4 m = T.m[r][i];
+          const float fl = dq[r] * sbyte(m[il_ >> 2], il_ & 3), fh = dq[r] * sbyte(m[ih_ >> 2], ih_ & 3);
+          const u32x4 a = T.a[r][i][t];
+          const u32x2 H = T.h[r][i][t];
+          u32x4 lo, hi;
+          lo.x = (a.x & 0x0F0F0F0Fu) | ((H.x << 4) & 0x30303030u);
+          lo.y = (a.y & 0x0F0F0F0Fu) | ((H.x << 2) & 0x30303030u);
+          lo.z = (a.z & 0x0F0F0F0Fu) | (H.x & 0x30303030u);
+          lo.w = (a.w & 0x0F0F0F0Fu) | ((H.x >> 2) & 0x30303030u);
+          hi.x = ((a.x >> 4) & 0x0F0F0F0Fu) | ((H.y << 4) & 0x30303030u);
+          hi.y = ((a.y >> 4) & 0x0F0F0F0Fu) | ((H.y << 2) & 0x30303030u);
+          hi.z = ((a.z >> 4) & 0x0F0F0F0Fu) | (H.y & 0x30303030u);
+          hi.w = ((a.w >> 4) & 0x0F0F0F0Fu) | ((H.y >> 2) & 0x30303030u);
+#pragma unroll
+          for (int b = 0; b < BT; ++b) {
+            const float il = (float)dot16(lo, x.lo[b]), ih = (float)dot16(hi, x.hi[b]);
+            acc[r][b] += fl * (x.fl[b].x * il - 32.f * x.fl[b].y) + fh * (x.fh[b].x * ih - 32.f * x.fh[b].y);
+          }
+        }
+      }
+    } else {
+      // Q4_0: w = d*(n - 8), lo nibble unsigned, hi nibble signed; Q8_0: w = d*q
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        XFr<BT> x;
+        load_x<BT>(xq, xf, XS, xs0 + 2 * t, xs0 + 2 * t + 1, x);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const unsigned dw = T.m[r][i][t >> 1];
+          const float d = (t & 1) ? f16hi(dw) : f16lo(dw);
+          const u32x4 a = T.a[r][i][t];
+#pragma unroll
+          for (int b = 0; b < BT; ++b) {
+            if constexpr (QT == QT_Q4_0) {
+              const float il = (float)dot16(a & 0x0F0F0F0Fu, x.lo[b]);
+              const float ih = (float)dot16(a & 0xF0F0F0F0u, x.hi[b]);
+              acc[r][b] += d * (x.fl[b].x * il - 8.f * x.fl[b].y + 0.0625f * x.fh[b].x * ih);
+            } else {
+              const float il = (float)dot16(a, x.lo[b]), ih = (float)dot16(T.b[r][i][t], x.hi[b]);
+              acc[r][b] += d * (x.fl[b].x * il + x.fh[b].x * ih);
+            }
+          }
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// activation prologue: x[b] (fp32) -> (norm) -> int8 groups of 16 in LDS (padded slots)
 template <int NT>
-__device__ void stage_activation(const GemvParams& P, int b, int K, i32x4* lq, float* ld, float* ls,
-                                 float* red) {
-  const int G = K / 16;
-  const float* x = P.x + (long long)b * P.ldx;
+__device__ void stage_x(const GemvParams& P, const float* x, int K, int SB, i32x4* lq, f32x2* lf, float* red) {
   float mean = 0.f, rstd = 1.f;
   if (P.norm != NORM_NONE) {
     float s = 0.f, ss = 0.f;
@@ -148,7 +269,13 @@ __device__ void stage_activation(const GemvParams& P, int b, int K, i32x4* lq, f
       rstd = rsqrtf(ss / K + P.eps);
     }
   }
-  for (int g = threadIdx.x; g < G; g += NT) {
+  for (int g = threadIdx.x; g < SB * 16; g += NT) {
+    const int slot = (g >> 4) * XPAD + (g & 15);
+    if (16 * g >= K) {  // K padding
+      lq[slot] = (i32x4){0, 0, 0, 0};
+      lf[slot] = (f32x2){0.f, 0.f};
+      continue;
+    }
     float v[16];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -189,83 +316,35 @@ __device__ void stage_activation(const GemvParams& P, int b, int K, i32x4* lq, f
     for (int j = 0; j < 4; ++j)
       pk[j] = (q[4 * j] & 0xFF) | ((q[4 * j + 1] & 0xFF) << 8) | ((q[4 * j + 2] & 0xFF) << 16) |
               ((q[4 * j + 3] & 0xFF) << 24);
-    lq[g] = pk;
-    ld[g] = d;
-    ls[g] = d * (float)qsum;
+    lq[slot] = pk;
+    lf[slot] = (f32x2){d, d * (float)qsum};
   }
 }
 
-// --------------------------------------------------------------------------------------------
-// Kernel structure (per 256-thread block = 4 waves, each wave owns R = 2 rows of a row tile):
-//   1. issue the first tile's weight loads (they do not depend on x)
-//   2. activation prologue into LDS (overlaps the weight fetch)
-//   3. persistent loop over row tiles (tile += gridDim.x): prefetch the next tile's weights into
-//      a second register set while the current tile is computed (MODE 0), or reload (MODE 1/2).
-// MODE 0: one K round, double-buffered; MODE 1: one K round, single buffer; MODE 2: K split in
-// rounds of 64*NPC pieces (K > 16384).
-constexpr int GEMV_NW = 4;
-constexpr int GEMV_R = 2;
-
-GemvTuning g_tune;
-void set_gemv_tuning(int blocks_per_cu, int rows_per_wave, int r1) {
-  if (blocks_per_cu > 0) g_tune.blocks_per_cu = blocks_per_cu;
-  if (rows_per_wave == 2 || rows_per_wave == 4) g_tune.rows_per_wave = rows_per_wave;
-  if (r1 >= 0) g_tune.r1 = r1;
-}
-
-template <int QT, int NPC, int R>
-__device__ __forceinline__ void load_tile(const QMat& w, long long row_base, int row0, int N, int base, int Pc,
-                                          int lane, WFrag (&wf)[R][NPC]) {
-#pragma unroll
-  for (int i = 0; i < NPC; ++i) {
-    const int p = min(base + 64 * i + lane, Pc - 1);
-#pragma unroll
-    for (int r = 0; r < R; ++r) load_wfrag<QT>(w, row_base + min(row0 + r, N - 1), p, wf[r][i]);
-  }
-}
-
-template <int QT, int NPC, int BT, int R>
-__device__ __forceinline__ void compute_tile(const WFrag (&wf)[R][NPC], int base, int Pc, int lane, int G,
-                                             const i32x4* lq, const float* ld, const float* ls,
-                                             float (&acc)[R][BT]) {
-#pragma unroll
-  for (int i = 0; i < NPC; ++i) {
-    const int p = base + 64 * i + lane;
-    if (p < Pc) {
-      int glo, ghi;
-      piece_groups(QT, p, glo, ghi);
-#pragma unroll
-      for (int b = 0; b < BT; ++b) {
-        XFrag xf;
-        xf.lo = lq[b * G + glo];
-        xf.hi = lq[b * G + ghi];
-        xf.dlo = ld[b * G + glo];
-        xf.dhi = ld[b * G + ghi];
-        xf.slo = ls[b * G + glo];
-        xf.shi = ls[b * G + ghi];
-#pragma unroll
-        for (int r = 0; r < R; ++r) acc[r][b] += piece_dot<QT>(wf[r][i], xf, p);
-      }
-    }
-  }
-}
-
-template <int BT, int R>
-__device__ __forceinline__ void epilogue(const GemvParams& P, float (&acc)[R][BT], int row0, int N, int b0,
-                                         int lane) {
+// ---------------------------------------------------------------------------------------------
+// row-group epilogue: reduce the 16 lanes, then lane s == r * BT + b writes (row0 + r, batch b)
+template <int R, int BT>
+__device__ __forceinline__ void finish_rows(const GemvParams& P, float (&acc)[R][BT], int row0, int N, int b0,
+                                            int s) {
+  float part[R][BT];
 #pragma unroll
   for (int r = 0; r < R; ++r)
 #pragma unroll
-    for (int b = 0; b < BT; ++b) acc[r][b] = wave_sum(acc[r][b]);
+    for (int b = 0; b < BT; ++b) acc[r][b] = row16_sum(acc[r][b]);
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int b = 0; b < BT; ++b) part[r][b] = R > 1 ? acc[r ^ 1][b] : __shfl_xor(acc[r][b], 16, OMX_WAVE);
 #pragma unroll
   for (int r = 0; r < R; ++r) {
 #pragma unroll
     for (int b = 0; b < BT; ++b) {
-      if (lane != r * BT + b) continue;
+      if (s != r * BT + b) continue;
       const int n = row0 + r;
       const int bb = b0 + b;
       if (n >= N || bb >= P.B) continue;
       float v = acc[r][b];
+      const float pv0 = part[r][b];
       const int vn = n + P.row_offset;  // row index in the virtual (concatenated) matrix
       switch (P.epi) {
         case EPI_STORE:
@@ -285,10 +364,8 @@ __device__ __forceinline__ void epilogue(const GemvParams& P, float (&acc)[R][BT
           P.y[(long long)bb * P.ldy + vn] = gelu_tanh(v);
           break;
         case EPI_GLU:
-          if ((r & 1) == 0) {  // even row = gate, odd row = up
-            const float u = acc[(r + 1) % R][b];  // R == 1 never takes this path (dispatch)
-            P.y[(long long)bb * P.ldy + (long long)blockIdx.z * P.y_sel_stride + vn / 2] = silu(v) * u;
-          }
+          if ((vn & 1) == 0)  // even row = gate, odd row = up
+            P.y[(long long)bb * P.ldy + (long long)blockIdx.z * P.y_sel_stride + vn / 2] = silu(v) * pv0;
           break;
         case EPI_QKV: {
           const int Eq = P.Eq, Ekv = P.Ekv, D = P.D;
@@ -299,7 +376,7 @@ __device__ __forceinline__ void epilogue(const GemvParams& P, float (&acc)[R][BT
           if (P.bias) v += P.bias[vn];
           float out = v;
           if (which < 2 && d < P.n_rot) {
-            float pv = acc[(r ^ 1) % R][b];
+            float pv = pv0;
             if (P.bias) pv += P.bias[vn ^ 1];
             const float ang = (float)P.pos[bb] * P.inv_freq[d >> 1];
             float sn, cs;
@@ -323,161 +400,138 @@ __device__ __forceinline__ void epilogue(const GemvParams& P, float (&acc)[R][BT
   }
 }
 
-template <int QT, int NPC, int BT, int MODE, int R>
-__global__ __launch_bounds__(256) void gemv_kernel(GemvParams P) {
-  constexpr int NT = 256, ROWS = GEMV_NW * R;
+// ---------------------------------------------------------------------------------------------
+// Block = 4 waves x 4 row groups x R rows = 16R rows per tile. Work unit = (tile, K chunk of
+// 16*NSB super-blocks); blocks are persistent over units (tile += gridDim.x).
+template <int QT, int NSB, int R, int BT>
+__global__ __launch_bounds__(GEMV_NT) void qgemv_kernel(GemvParams P) {
+  constexpr int PB = QT == QT_Q8_0 ? 8 : QT == QT_Q6_K ? 6 : 4;  // VGPRs per piece
+  constexpr bool DB = R * NSB * (8 * PB + 5) <= 80;               // room for a prefetch tile
+  constexpr int ROWS_W = 4 * R, ROWS_B = 4 * ROWS_W;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const QMat& w = P.w;
-  const int K = w.K, N = w.N;
-  const int G = K / 16;
-  i32x4* lq = (i32x4*)smem;                               // [BT][G]
-  float* ld = (float*)(smem + (size_t)BT * G * 16);       // [BT][G]
-  float* ls = ld + BT * G;                                // [BT][G]
-  float* red = ls + BT * G;                               // [NT/64]
+  const int K = w.K, N = w.N, SB = n_sb(K);
+  const int XS = SB * XPAD;
+  i32x4* lq = (i32x4*)smem;                         // [BT][XS]
+  f32x2* lf = (f32x2*)(smem + (size_t)BT * XS * 16);  // [BT][XS]
+  float* red = (float*)(lf + BT * XS);              // [NT/64]
   const int b0 = blockIdx.y * BT;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int Pc = K / 32;
-  const int n_tiles = (N + ROWS - 1) / ROWS;
-  int tile = blockIdx.x;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, s = lane & 15;
+  const int nc = (SB + 16 * NSB - 1) / (16 * NSB);
+  const int n_tiles = (N + ROWS_B - 1) / ROWS_B;
+  const int rbase = wave * ROWS_W + g * R;
 
   long long row_base = 0;
-  GemvParams Q = P;
+  const float* x = P.x;
   if (P.expert_ids) {  // MoE: blockIdx.z = k-th selected expert of batch row b0
     const int e = P.expert_ids[b0 * P.n_sel + blockIdx.z];
     row_base = (long long)e * N;
-    if (P.x_per_sel) Q.x = P.x + (long long)blockIdx.z * P.x_sel_stride;
+    if (P.x_per_sel) x = P.x + (long long)blockIdx.z * P.x_sel_stride;
   }
 
-  WFrag wa[R][NPC];
-  if (MODE != 2 && tile < n_tiles) load_tile<QT, NPC, R>(w, row_base, tile * ROWS + wave * R, N, 0, Pc, lane, wa);
+  int tile = blockIdx.x, c = 0;
+  WTile<QT, NSB, R> A;
+  if (tile < n_tiles) load_wtile<QT, NSB, R>(w, row_base, tile * ROWS_B + rbase, N, SB, 0, s, A);
 
 #pragma unroll
   for (int b = 0; b < BT; ++b) {
     if (b0 + b < P.B) {
-      stage_activation<NT>(Q, b0 + b, K, lq + b * G, ld + b * G, ls + b * G, red);
+      stage_x<GEMV_NT>(P, x + (long long)(b0 + b) * P.ldx, K, SB, lq + b * XS, lf + b * XS, red);
     } else {
-      for (int g = threadIdx.x; g < G; g += NT) {
-        lq[b * G + g] = (i32x4){0, 0, 0, 0};
-        ld[b * G + g] = 0.f;
-        ls[b * G + g] = 0.f;
+      for (int i = threadIdx.x; i < XS; i += GEMV_NT) {
+        lq[b * XS + i] = (i32x4){0, 0, 0, 0};
+        lf[b * XS + i] = (f32x2){0.f, 0.f};
       }
     }
   }
   __syncthreads();
 
-  if constexpr (MODE == 0) {
-    // explicit ping-pong (no register copy: a wa = wb copy would force a vmcnt(0) drain every
-    // tile): while one register set is consumed, the other tile's loads are in flight
-    WFrag wb[R][NPC];
-    auto step = [&](WFrag (&cur)[R][NPC], WFrag (&nxt)[R][NPC], int t) {
-      const int row0 = t * ROWS + wave * R;
-      const int next = t + gridDim.x;
-      if (next < n_tiles) load_tile<QT, NPC, R>(w, row_base, next * ROWS + wave * R, N, 0, Pc, lane, nxt);
-      float acc[R][BT];
+  float acc[R][BT];
 #pragma unroll
-      for (int r = 0; r < R; ++r)
+  for (int r = 0; r < R; ++r)
 #pragma unroll
-        for (int b = 0; b < BT; ++b) acc[r][b] = 0.f;
-      compute_tile<QT, NPC, BT, R>(cur, 0, Pc, lane, G, lq, ld, ls, acc);
-      if (row0 < N) epilogue<BT, R>(P, acc, row0, N, b0, lane);
-    };
-    while (tile < n_tiles) {
-      step(wa, wb, tile);
-      tile += gridDim.x;
-      if (tile >= n_tiles) break;
-      step(wb, wa, tile);
-      tile += gridDim.x;
-    }
-    return;
-  }
-  for (; tile < n_tiles; tile += gridDim.x) {
-    const int row0 = tile * ROWS + wave * R;
-    const int next = tile + gridDim.x;
-    float acc[R][BT];
+    for (int b = 0; b < BT; ++b) acc[r][b] = 0.f;
+  auto finish = [&](int t) {
+    finish_rows<R, BT>(P, acc, t * ROWS_B + rbase, N, b0, s);
 #pragma unroll
     for (int r = 0; r < R; ++r)
 #pragma unroll
       for (int b = 0; b < BT; ++b) acc[r][b] = 0.f;
-    if constexpr (MODE == 1) {
-      compute_tile<QT, NPC, BT, R>(wa, 0, Pc, lane, G, lq, ld, ls, acc);
-      if (next < n_tiles) load_tile<QT, NPC, R>(w, row_base, next * ROWS + wave * R, N, 0, Pc, lane, wa);
-    } else {
-      for (int base = 0; base < Pc; base += 64 * NPC) {
-        load_tile<QT, NPC, R>(w, row_base, row0, N, base, Pc, lane, wa);
-        compute_tile<QT, NPC, BT, R>(wa, base, Pc, lane, G, lq, ld, ls, acc);
-      }
+  };
+
+  if constexpr (DB) {
+    // explicit ping-pong (a register copy would force a vmcnt(0) drain every unit)
+    WTile<QT, NSB, R> Bt;
+    auto step = [&](WTile<QT, NSB, R>& cur, WTile<QT, NSB, R>& nxt) {
+      int nt = tile, ncc = c + 1;
+      if (ncc == nc) { ncc = 0; nt += gridDim.x; }
+      if (nt < n_tiles) load_wtile<QT, NSB, R>(w, row_base, nt * ROWS_B + rbase, N, SB, ncc * 16 * NSB, s, nxt);
+      compute_wtile<QT, NSB, R, BT>(cur, SB, c * 16 * NSB, s, lq, lf, XS, acc);
+      if (c == nc - 1) finish(tile);
+      tile = nt;
+      c = ncc;
+    };
+    while (tile < n_tiles) {
+      step(A, Bt);
+      if (tile >= n_tiles) break;
+      step(Bt, A);
     }
-    if (row0 < N) epilogue<BT, R>(P, acc, row0, N, b0, lane);
+  } else {
+    while (tile < n_tiles) {
+      compute_wtile<QT, NSB, R, BT>(A, SB, c * 16 * NSB, s, lq, lf, XS, acc);
+      if (c == nc - 1) finish(tile);
+      if (++c == nc) { c = 0; tile += gridDim.x; }
+      if (tile < n_tiles) load_wtile<QT, NSB, R>(w, row_base, tile * ROWS_B + rbase, N, SB, c * 16 * NSB, s, A);
+    }
   }
 }
 
-template <int QT, int NPC, int BT, int MODE, int R = GEMV_R>
+static size_t lds_bytes(int K, int BT) { return (size_t)BT * ((K + 255) / 256) * XPAD * 24 + 64; }
+
+template <int QT, int NSB, int R, int BT>
 static void launch_t(const GemvParams& P, hipStream_t s) {
   const int N = P.w.N;
-  const int rows_per_block = GEMV_NW * R;
-  const int tiles = (N + rows_per_block - 1) / rows_per_block;
+  const int tiles = (N + 16 * R - 1) / (16 * R);
   const int by = (P.B + BT - 1) / BT;
   const int bz = P.expert_ids ? P.n_sel : 1;
-  // persistent grid: ~2 blocks per CU over all (y, z) slices; each block walks its row tiles
   int gx = tiles;
   const int slots = 256 * g_tune.blocks_per_cu;
   const int cap = slots / (by * bz) > 0 ? slots / (by * bz) : 1;
   if (gx > cap) gx = cap;
-  dim3 grid(gx, by, bz);
-  const size_t lds = (size_t)BT * (P.w.K / 16) * 24 + 64;
-  hipLaunchKernelGGL((gemv_kernel<QT, NPC, BT, MODE, R>), grid, dim3(256), lds, s, P);
+  hipLaunchKernelGGL((qgemv_kernel<QT, NSB, R, BT>), dim3(gx, by, bz), dim3(GEMV_NT), lds_bytes(P.w.K, BT), s, P);
 }
 
-template <int QT, int BT>
-static void launch_b(const GemvParams& P, hipStream_t s) {
-  const int Pc = P.w.K / 32;
-  const int need = (Pc + 63) / 64;
-  // one row per wave doubles the waves in flight and halves each wave's serial dot work; only
-  // the epilogues that pair adjacent rows (GLU gate/up, QKV RoPE) need two rows per wave
-  const bool r1 = BT == 1 && g_tune.r1 && P.epi != EPI_GLU && P.epi != EPI_QKV && need <= 8;
-  if (r1) {
+template <int QT, int R, int BT>
+static void launch_nsb(const GemvParams& P, hipStream_t s) {
+  const int SB = (P.w.K + 255) / 256;
+  const int need = (SB + 15) / 16;
+  if constexpr (R == 2) {  // two rows per group only while both register tiles stay resident
+    if (need == 1) launch_t<QT, 1, 2, BT>(P, s);
+    else if (need == 2) launch_t<QT, 2, 2, BT>(P, s);
+    else launch_nsb<QT, 1, BT>(P, s);
+    return;
+  } else {
     switch (need) {
-      case 1: launch_t<QT, 1, BT, 0, 1>(P, s); return;
-      case 2: launch_t<QT, 2, BT, 0, 1>(P, s); return;
-      case 3: launch_t<QT, 3, BT, 0, 1>(P, s); return;
-      case 4: launch_t<QT, 4, BT, 0, 1>(P, s); return;
-      case 5: launch_t<QT, 5, BT, 1, 1>(P, s); return;
-      case 6: launch_t<QT, 6, BT, 1, 1>(P, s); return;
-      case 7: launch_t<QT, 7, BT, 1, 1>(P, s); return;
-      default: launch_t<QT, 8, BT, 1, 1>(P, s); return;
+      case 1: launch_t<QT, 1, R, BT>(P, s); return;
+      case 2: launch_t<QT, 2, R, BT>(P, s); return;
+      case 3: launch_t<QT, 3, R, BT>(P, s); return;
+      default: launch_t<QT, 4, R, BT>(P, s); return;  // K > 12288: chunks of 64 super-blocks
     }
-  }
-  switch (need) {
-    case 1:
-      if (BT == 1 && g_tune.rows_per_wave == 4) launch_t<QT, 1, BT, 0, 4>(P, s);
-      else launch_t<QT, 1, BT, 0>(P, s);
-      break;
-    case 2:
-      if (BT == 1 && g_tune.rows_per_wave == 4) launch_t<QT, 2, BT, 0, 4>(P, s);
-      else launch_t<QT, 2, BT, 0>(P, s);
-      break;
-    case 3: launch_t<QT, 3, BT, 1>(P, s); break;
-    case 4: launch_t<QT, 4, BT, 1>(P, s); break;
-    case 5: launch_t<QT, 5, BT, 1>(P, s); break;
-    case 6: launch_t<QT, 6, BT, 1>(P, s); break;
-    case 7: launch_t<QT, 7, BT, 1>(P, s); break;
-    case 8: launch_t<QT, 8, BT, 1>(P, s); break;
-    default: launch_t<QT, 8, BT, 2>(P, s); break;
   }
 }
 
 template <int QT>
 static void launch_q(const GemvParams& P, hipStream_t s) {
   if (P.B == 1 || P.expert_ids != nullptr) {  // decode (and MoE: experts differ per batch row)
-    launch_b<QT, 1>(P, s);
+    if (g_tune.rows == 2) launch_nsb<QT, 2, 1>(P, s);
+    else launch_nsb<QT, 1, 1>(P, s);
     return;
   }
-  // small-batch tiles of 4 rows (chunked prefill / batched decode): 2 pieces per lane per K
-  // round keeps the 4 x-fragment sets + weights inside the register budget
-  const int need = (P.w.K / 32 + 63) / 64;
-  if (need == 1) launch_t<QT, 1, 4, 0>(P, s);
-  else if (need == 2) launch_t<QT, 2, 4, 0>(P, s);
-  else launch_t<QT, 2, 4, 2>(P, s);
+  // batch tiles: the weights are unpacked once per piece and dotted against BT activation rows;
+  // BT bounded by the LDS the staged activations take
+  if (lds_bytes(P.w.K, 4) <= 96 * 1024) launch_nsb<QT, 1, 4>(P, s);
+  else if (lds_bytes(P.w.K, 2) <= 120 * 1024) launch_nsb<QT, 1, 2>(P, s);
+  else launch_nsb<QT, 1, 1>(P, s);
 }
 
 void gemv(const GemvParams& P, hipStream_t s) {
@@ -489,7 +543,5 @@ void gemv(const GemvParams& P, hipStream_t s) {
     default: break;
   }
 }
-
-size_t gemv_lds_bytes(int K, int B) { return (size_t)(B == 1 ? 1 : 4) * (K / 16) * 24 + 64; }
 
 }  // namespace omx

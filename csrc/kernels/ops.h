@@ -46,12 +46,11 @@ void gemv(const GemvParams& P, hipStream_t s);
 
 // launch-shape knobs for the decode GEMV (tuned on MI355X; see scripts/bench_gemv.py)
 struct GemvTuning {
-  int blocks_per_cu = 3;  // persistent grid = 256 CUs x this (scripts/bench_gemv.py sweep)
-  int rows_per_wave = 2;  // 2 or 4 (K <= 4096 decode kernels)
-  int r1 = 1;             // one row per wave for epilogues without row pairs
+  int blocks_per_cu = 4;  // persistent-grid cap = 256 CUs x this (scripts/bench_gemv.py sweep)
+  int rows = 1;           // rows per 16-lane row group in B == 1 launches (1 or 2)
 };
 extern GemvTuning g_tune;
-void set_gemv_tuning(int blocks_per_cu, int rows_per_wave, int r1);
+void set_gemv_tuning(int blocks_per_cu, int rows, int reserved);
 
 // Dequantize rows of a repacked matrix (embedding gather / fp16 copies)
 void embed_rows(const QMat& w, const int* rows, int n, float* out, int ldo, hipStream_t s);

@@ -22,23 +22,15 @@ import torch
 from ..gguf import GGMLType, read_gguf
 from ..gguf.constants import BLOCK_GEOMETRY
 from ..models.config import ROPE_NEOX, ModelConfig
-from ..quant import dequantize, quantize
+from ..quant import REPACK_STREAMS, dequantize, quantize, repack_row_bytes
 from ..ops import has_native, native
 
 NATIVE_QTYPES = (GGMLType.Q4_0, GGMLType.Q8_0, GGMLType.Q4_K, GGMLType.Q6_K)
 
 
 def stream_bytes(qtype: int, K: int) -> list[int]:
-    q = GGMLType(qtype)
-    if q == GGMLType.Q4_K:
-        return [K // 2, K // 16]
-    if q == GGMLType.Q6_K:
-        return [K // 2, K // 4, K // 16, K // 128]
-    if q == GGMLType.Q4_0:
-        return [K // 2, K // 16]
-    if q == GGMLType.Q8_0:
-        return [K, K // 16]
-    raise ValueError(f"no device layout for {q.name}")
+    """Per-row bytes of each device stream (layout v2, quant.repack)."""
+    return repack_row_bytes(qtype, K)
 
 
 @dataclass
@@ -66,9 +58,7 @@ def _np_repack_rows(src: np.ndarray, qtype: int, K_src: int, rows: np.ndarray, d
     b = src.reshape(-1, K_src // blk, nb)[rows][:, kb0:kb1]
     K = (kb1 - kb0) * blk
     st = repack(b.reshape(-1), qtype, len(rows), K)
-    names = {GGMLType.Q4_K: ["qs", "meta"], GGMLType.Q6_K: ["ql", "qh", "sc", "d"],
-             GGMLType.Q4_0: ["qs", "d"], GGMLType.Q8_0: ["qs", "d"]}[GGMLType(qtype)]
-    for i, n in enumerate(names):
+    for i, n in enumerate(REPACK_STREAMS[GGMLType(qtype)]):
         dst[i].reshape(-1, st[n].shape[1])[dst_rows] = st[n]
 
 

@@ -15,14 +15,13 @@ import torch
 import torch.nn.functional as F
 
 from ..gguf import GGMLType
-from ..quant import dequantize, unrepack
+from ..quant import REPACK_STREAMS, dequantize, repack_row_bytes, unrepack
 
 
 def dequant_qmat(m) -> torch.Tensor:
     """DevQMat -> float32 [rows_total, K] on the matrix's device."""
-    names = {GGMLType.Q4_K: ["qs", "meta"], GGMLType.Q6_K: ["ql", "qh", "sc", "d"],
-             GGMLType.Q4_0: ["qs", "d"], GGMLType.Q8_0: ["qs", "d"]}[GGMLType(m.qtype)]
-    rows = m.streams[0].numel() // (m.K // 2 if m.qtype != GGMLType.Q8_0 else m.K)
+    names = REPACK_STREAMS[GGMLType(m.qtype)]
+    rows = m.streams[0].numel() // repack_row_bytes(m.qtype, m.K)[0]
     st = {n: s.detach().cpu().numpy() for n, s in zip(names, m.streams)}
     raw = unrepack(st, m.qtype, rows, m.K)
     w = dequantize(raw, m.qtype, rows * m.K).reshape(rows, m.K)

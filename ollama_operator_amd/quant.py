@@ -257,10 +257,71 @@ def random_blocks(ggml_type: int, n_rows: int, k: int, rng: np.random.Generator,
 
 
 # ----------------------------------------------------------------------------------------------
-# device repack (block form -> aligned streams). Inverse provided for tests.
+# device repack (block form -> GEMV streams, layout v2). Inverse provided for tests.
+#
+# K is padded to SB = ceil(K/256) super-blocks of 256 weights (zero blocks; only Q4_0/Q8_0 rows can
+# need it). A "piece" is the 32 weights one lane consumes with one 16-B load; super-block `sb` holds
+# pieces t = 0..7. Quant codes are stored piece-major *across* super-blocks,
+#     qs[row][t][sb][16 B]     (Q8_0: 32 B, Q6_K high bits: 8 B)
+# so the 16 lanes of a row group (lane s owns super-blocks s, s+16, ...) read one contiguous 256 B
+# run per load instruction, while each lane's piece index t is a compile-time constant -- the
+# per-super-block scales are decoded once per 256 weights instead of once per piece
+# (csrc/kernels/gemv.hip). Scales / mins stay per super-block: meta[row][sb][16 B].
+# 4-bit codes store the HIGH nibble of every byte as a signed two's-complement (n - 8) (byte ^ 0x80),
+# so `q & 0xF0F0F0F0` is directly 16*(n-8) as int8 for v_dot4_i32_i8 (one VALU op, no shift).
+# Q6_K high bits are regrouped per piece: byte j of dword H0 (lo half) / H1 (hi half) holds the
+# 2-bit fields of weights j, 4+j, 8+j, 12+j at bits 0-1, 2-3, 4-5, 6-7.
 # ----------------------------------------------------------------------------------------------
 
 REPACK_TYPES = (GGMLType.Q4_0, GGMLType.Q8_0, GGMLType.Q4_K, GGMLType.Q6_K)
+REPACK_STREAMS = {GGMLType.Q4_K: ["qs", "meta"], GGMLType.Q6_K: ["ql", "qh", "sc", "d"],
+                  GGMLType.Q4_0: ["qs", "d"], GGMLType.Q8_0: ["qs", "d"]}
+
+
+def n_superblocks(k: int) -> int:
+    return (k + 255) // 256
+
+
+def repack_row_bytes(ggml_type: int, k: int) -> list[int]:
+    """Bytes per row of each repacked stream (order of REPACK_STREAMS)."""
+    sb = n_superblocks(k)
+    t = GGMLType(ggml_type)
+    if t == GGMLType.Q4_K:
+        return [128 * sb, 16 * sb]
+    if t == GGMLType.Q6_K:
+        return [128 * sb, 64 * sb, 16 * sb, 2 * sb]
+    if t == GGMLType.Q4_0:
+        return [128 * sb, 16 * sb]
+    if t == GGMLType.Q8_0:
+        return [256 * sb, 16 * sb]
+    raise ValueError(f"no device layout for {t.name}")
+
+
+def _q6k_qh_split(qh: np.ndarray) -> np.ndarray:
+    """qh [..., 64] (ggml order) -> [..., 8 pieces, 8 B] (H0 | H1 per piece)."""
+    q = qh.reshape(qh.shape[:-1] + (2, 32)).astype(np.uint32)   # [.., n, l]
+    out = np.zeros(qh.shape[:-1] + (2, 4, 2, 4), np.uint32)     # [.., n, sub, half, byte j]
+    for sub in range(4):
+        lsel = q[..., (sub & 1) * 16:(sub & 1) * 16 + 16]      # [.., n, 16] weight i
+        for half in range(2):
+            f = (sub >> 1) + 2 * half                           # field of qh holding this weight
+            bits = (lsel >> (2 * f)) & 3                        # [.., n, i]
+            for k in range(4):
+                out[..., sub, half, :] |= bits[..., 4 * k:4 * k + 4] << (2 * k)
+    return out.astype(np.uint8).reshape(qh.shape[:-1] + (8, 8))
+
+
+def _q6k_qh_join(h: np.ndarray) -> np.ndarray:
+    """inverse of _q6k_qh_split: [..., 8, 8] -> [..., 64]."""
+    h = h.reshape(h.shape[:-2] + (2, 4, 2, 4)).astype(np.uint32)
+    q = np.zeros(h.shape[:-4] + (2, 32), np.uint32)
+    for sub in range(4):
+        for half in range(2):
+            f = (sub >> 1) + 2 * half
+            for k in range(4):
+                bits = (h[..., sub, half, :] >> (2 * k)) & 3      # [.., n, j]
+                q[..., (sub & 1) * 16 + 4 * k:(sub & 1) * 16 + 4 * k + 4] |= bits << (2 * f)
+    return q.astype(np.uint8).reshape(h.shape[:-4] + (64,))
 
 
 def repack(raw: np.ndarray, ggml_type: int, n_rows: int, k: int) -> dict[str, np.ndarray]:
@@ -268,42 +329,55 @@ def repack(raw: np.ndarray, ggml_type: int, n_rows: int, k: int) -> dict[str, np
     blk, nb = BLOCK_GEOMETRY[t]
     if k % blk:
         raise ValueError(f"K={k} not a multiple of {blk} for {t.name}")
+    sb = n_superblocks(k)
     b = np.ascontiguousarray(raw).view(np.uint8).reshape(n_rows, k // blk, nb)
+    if blk == 32 and k % 256:  # pad Q4_0 / Q8_0 rows to whole super-blocks with zero blocks
+        b = np.concatenate([b, np.zeros((n_rows, sb * 8 - k // 32, nb), np.uint8)], axis=1)
+
+    def pm(x, w):  # [rows, sb, 8, w] -> piece-major [rows, 8 * sb * w]
+        return np.ascontiguousarray(x.reshape(n_rows, sb, 8, w).transpose(0, 2, 1, 3)).reshape(n_rows, -1)
+
     if t == GGMLType.Q4_K:
-        return {"qs": np.ascontiguousarray(b[:, :, 16:144]).reshape(n_rows, k // 2),
-                "meta": np.ascontiguousarray(b[:, :, 0:16]).reshape(n_rows, k // 16)}
+        return {"qs": pm(b[:, :, 16:144] ^ 0x80, 16),
+                "meta": np.ascontiguousarray(b[:, :, 0:16]).reshape(n_rows, 16 * sb)}
     if t == GGMLType.Q6_K:
-        return {"ql": np.ascontiguousarray(b[:, :, 0:128]).reshape(n_rows, k // 2),
-                "qh": np.ascontiguousarray(b[:, :, 128:192]).reshape(n_rows, k // 4),
-                "sc": np.ascontiguousarray(b[:, :, 192:208]).reshape(n_rows, k // 16),
-                "d": np.ascontiguousarray(b[:, :, 208:210]).reshape(n_rows, k // 128)}
+        return {"ql": pm(b[:, :, 0:128], 16),
+                "qh": pm(_q6k_qh_split(b[:, :, 128:192]), 8),
+                "sc": np.ascontiguousarray(b[:, :, 192:208]).reshape(n_rows, 16 * sb),
+                "d": np.ascontiguousarray(b[:, :, 208:210]).reshape(n_rows, 2 * sb)}
     if t == GGMLType.Q4_0:
-        return {"qs": np.ascontiguousarray(b[:, :, 2:18]).reshape(n_rows, k // 2),
-                "d": np.ascontiguousarray(b[:, :, 0:2]).reshape(n_rows, k // 16)}
+        return {"qs": pm(b[:, :, 2:18] ^ 0x80, 16),
+                "d": np.ascontiguousarray(b[:, :, 0:2]).reshape(n_rows, 16 * sb)}
     if t == GGMLType.Q8_0:
-        return {"qs": np.ascontiguousarray(b[:, :, 2:34]).reshape(n_rows, k),
-                "d": np.ascontiguousarray(b[:, :, 0:2]).reshape(n_rows, k // 16)}
+        return {"qs": pm(b[:, :, 2:34], 32),
+                "d": np.ascontiguousarray(b[:, :, 0:2]).reshape(n_rows, 16 * sb)}
     raise NotImplementedError(f"repack {t.name}")
 
 
 def unrepack(streams: dict[str, np.ndarray], ggml_type: int, n_rows: int, k: int) -> np.ndarray:
     t = GGMLType(ggml_type)
     blk, nb = BLOCK_GEOMETRY[t]
-    nbk = k // blk
-    out = np.empty((n_rows, nbk, nb), np.uint8)
-    s = {n: np.asarray(v).reshape(n_rows, nbk, -1) for n, v in streams.items()}
-    if t == GGMLType.Q4_K:
-        out[:, :, 0:16] = s["meta"]
-        out[:, :, 16:144] = s["qs"]
-    elif t == GGMLType.Q6_K:
-        out[:, :, 0:128] = s["ql"]
-        out[:, :, 128:192] = s["qh"]
-        out[:, :, 192:208] = s["sc"]
-        out[:, :, 208:210] = s["d"]
-    elif t == GGMLType.Q4_0:
-        out[:, :, 0:2] = s["d"]
-        out[:, :, 2:18] = s["qs"]
-    elif t == GGMLType.Q8_0:
-        out[:, :, 0:2] = s["d"]
-        out[:, :, 2:34] = s["qs"]
-    return out.reshape(-1)
+    sb = n_superblocks(k)
+    s = {n: np.asarray(v).reshape(n_rows, -1) for n, v in streams.items()}
+
+    def bm(x, w):  # piece-major -> [rows, sb, 8 * w]
+        return x.reshape(n_rows, 8, sb, w).transpose(0, 2, 1, 3).reshape(n_rows, sb, 8 * w)
+
+    if t in (GGMLType.Q4_K, GGMLType.Q6_K):
+        out = np.empty((n_rows, sb, nb), np.uint8)
+        if t == GGMLType.Q4_K:
+            out[:, :, 0:16] = s["meta"].reshape(n_rows, sb, 16)
+            out[:, :, 16:144] = bm(s["qs"], 16) ^ 0x80
+        else:
+            out[:, :, 0:128] = bm(s["ql"], 16)
+            out[:, :, 128:192] = _q6k_qh_join(bm(s["qh"], 8).reshape(n_rows, sb, 8, 8))
+            out[:, :, 192:208] = s["sc"].reshape(n_rows, sb, 16)
+            out[:, :, 208:210] = s["d"].reshape(n_rows, sb, 2)
+        return out.reshape(-1)
+    out = np.empty((n_rows, sb * 8, nb), np.uint8)
+    out[:, :, 0:2] = s["d"].reshape(n_rows, sb * 8, 2)
+    if t == GGMLType.Q4_0:
+        out[:, :, 2:18] = bm(s["qs"], 16).reshape(n_rows, sb * 8, 16) ^ 0x80
+    else:
+        out[:, :, 2:34] = bm(s["qs"], 32).reshape(n_rows, sb * 8, 32)
+    return np.ascontiguousarray(out[:, : k // blk]).reshape(-1)

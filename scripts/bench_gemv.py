@@ -45,9 +45,16 @@ def main():
     C = native()
     s = torch.cuda.current_stream().cuda_stream
     res = []
-    mats = {name: make(qt, N, K) for name, qt, N, K, _ in SHAPES}
-    knobs = [(b, r, r1) for b in (2, 3, 4) for r in (2, 4) for r1 in (0, 1)]
-    for (name, qt, N, K, epi), (bpc, rpw, r1) in itertools.product(SHAPES, knobs):
+    keep = os.environ.get("OMX_BENCH_SHAPES", "").split(",") if os.environ.get("OMX_BENCH_SHAPES") else None
+    mats = {name: make(qt, N, K) for name, qt, N, K, _ in SHAPES if keep is None or name in keep}
+    knobs = [(b, r, 0) for b in (2, 4, 8) for r in (1, 2)]
+    if os.environ.get("OMX_BENCH_KNOBS"):  # e.g. "3,2,1" (profiling one configuration)
+        knobs = [tuple(int(v) for v in os.environ["OMX_BENCH_KNOBS"].split(","))]
+    shapes = SHAPES
+    if os.environ.get("OMX_BENCH_SHAPES"):
+        keep = os.environ["OMX_BENCH_SHAPES"].split(",")
+        shapes = [s for s in SHAPES if s[0] in keep]
+    for (name, qt, N, K, epi), (bpc, rpw, r1) in itertools.product(shapes, knobs):
         C.set_gemv_tuning(bpc, rpw, r1)
         tups, ts, nbytes = mats[name]
         x = torch.randn(1, K, device="cuda")
@@ -67,11 +74,11 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) * 1e3 / n
-        res.append((name, f"blocks/CU={bpc} rows/wave={rpw} r1={r1}", us, nbytes / us / 1e3))
+        res.append((name, f"blocks/CU={bpc} rows={rpw}", us, nbytes / us / 1e3))
         print(f"{name:10s} {res[-1][1]} {us:8.2f} us  {nbytes/us/1e3:7.1f} GB/s", flush=True)
-    C.set_gemv_tuning(3, 2, 1)
+    C.set_gemv_tuning(4, 1, 0)
     print("best per shape:")
-    for name, *_ in SHAPES:
+    for name in mats:
         b = min((r for r in res if r[0] == name), key=lambda r: r[2])
         print(f"  {name:10s} {b[1]} {b[2]:.2f} us {b[3]:.0f} GB/s")
 

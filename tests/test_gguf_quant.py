@@ -4,6 +4,7 @@ import numpy as np
 import pytest
 
 from ollama_operator_amd.gguf import GGMLType, GGUFError, GGUFWriter, read_gguf
+from ollama_operator_amd.gguf.constants import BLOCK_GEOMETRY
 from ollama_operator_amd.quant import (dequantize, pack_q4k_scales, quantize, random_blocks, repack,
                                        unpack_q4k_scales, unrepack)
 
@@ -72,13 +73,73 @@ def test_quant_error_bounded(t):
 
 
 @pytest.mark.parametrize("t", QTYPES)
-def test_repack_roundtrip(t):
+@pytest.mark.parametrize("k", [512, 288])
+def test_repack_roundtrip(t, k):
+    if k % 256 and t in (GGMLType.Q4_K, GGMLType.Q6_K):
+        pytest.skip("k-quants are whole super-blocks")
     rng = np.random.default_rng(2)
-    n, k = 8, 512
+    n = 8
     raw = random_blocks(t, n, k, rng)
     s = repack(raw, t, n, k)
-    assert sum(v.nbytes for v in s.values()) == raw.nbytes  # no extra bandwidth
+    padded = n * ((k + 255) // 256 * 256 // BLOCK_GEOMETRY[t][0]) * BLOCK_GEOMETRY[t][1]
+    assert sum(v.nbytes for v in s.values()) == padded  # no extra bandwidth beyond K padding
     np.testing.assert_array_equal(unrepack(s, t, n, k), raw)
+
+
+def _kernel_model_dequant(s, t, n, k):
+    """numpy model of how csrc/kernels/gemv.hip decodes layout-v2 streams (piece-major codes,
+    signed high nibble, Q6_K H0/H1 fields) -- pins the layout contract the HIP kernel relies on."""
+    sb = (k + 255) // 256
+    w = np.zeros((n, sb * 256), np.float32)
+    f16 = lambda b: b.view(np.float16).astype(np.float32)  # noqa: E731
+    for r in range(n):
+        for b in range(sb):
+            for t_ in range(8):
+                if t == GGMLType.Q8_0:
+                    q = s["qs"][r].reshape(8, sb, 32)[t_, b].view(np.int8).astype(np.float32)
+                    d = f16(s["d"][r].reshape(sb, 8, 2)[b, t_].copy())[0]
+                    w[r, 256 * b + 32 * t_: 256 * b + 32 * t_ + 32] = d * q
+                    continue
+                a = s["qs" if t != GGMLType.Q6_K else "ql"][r].reshape(8, sb, 16)[t_, b]
+                lo = (a & 0x0F).astype(np.float32)
+                hi16 = (a & 0xF0).view(np.int8).astype(np.float32)  # = 16 * (n - 8) for 4-bit types
+                if t == GGMLType.Q4_0:
+                    d = f16(s["d"][r].reshape(sb, 8, 2)[b, t_].copy())[0]
+                    w[r, 256 * b + 32 * t_: 256 * b + 32 * t_ + 16] = d * (lo - 8)
+                    w[r, 256 * b + 32 * t_ + 16: 256 * b + 32 * t_ + 32] = d * hi16 / 16
+                elif t == GGMLType.Q4_K:
+                    m = s["meta"][r].reshape(sb, 16)[b]
+                    d, dmin = f16(m[0:2].copy())[0], f16(m[2:4].copy())[0]
+                    sc, mn = unpack_q4k_scales(m[4:16])
+                    c, h = t_ >> 1, t_ & 1
+                    o = 256 * b + 64 * c + 16 * h
+                    w[r, o:o + 16] = d * sc[2 * c] * lo - dmin * mn[2 * c]
+                    w[r, o + 32:o + 48] = d * sc[2 * c + 1] * (hi16 / 16 + 8) - dmin * mn[2 * c + 1]
+                else:
+                    hq = s["qh"][r].reshape(8, sb, 8)[t_, b].view(np.uint32)
+                    hi = ((a >> 4) & 0x0F).astype(np.int32)
+                    ql = (a & 0x0F).astype(np.int32)
+                    for kk in range(4):  # lo dword kk: bytes j <- field kk of H0 byte j
+                        for j in range(4):
+                            i = 4 * kk + j
+                            ql[i] |= ((int(hq[0]) >> (8 * j + 2 * kk)) & 3) << 4
+                            hi[i] |= ((int(hq[1]) >> (8 * j + 2 * kk)) & 3) << 4
+                    sc = s["sc"][r].reshape(sb, 16)[b].view(np.int8).astype(np.float32)
+                    d = f16(s["d"][r].reshape(sb, 2)[b].copy())[0]
+                    nn, sub = t_ >> 2, t_ & 3
+                    o = 256 * b + 128 * nn + 16 * sub
+                    w[r, o:o + 16] = d * sc[8 * nn + sub] * (ql - 32)
+                    w[r, o + 64:o + 80] = d * sc[8 * nn + sub + 4] * (hi - 32)
+    return w[:, :k]
+
+
+@pytest.mark.parametrize("t", QTYPES)
+def test_repack_kernel_contract(t):
+    rng = np.random.default_rng(3)
+    n, k = 3, 512 if t in (GGMLType.Q4_K, GGMLType.Q6_K) else 288
+    raw = random_blocks(t, n, k, rng)
+    got = _kernel_model_dequant(repack(raw, t, n, k), t, n, k)
+    np.testing.assert_allclose(got, dequantize(raw, t, n * k).reshape(n, k), rtol=1e-5, atol=1e-6)
 
 
 @pytest.mark.parametrize("t", QTYPES)
