@@ -1,48 +1,97 @@
 // Paged-KV grouped-query attention for decode and chunked prefill.
 //
-// Grid (query, kv_head, split). One 256-thread block serves the G = H/H_kv query heads that share a
-// KV head, so each K/V row is read from HBM once per group (GQA reuse). 16 lanes cooperate on one
-// key (D/16 dims each, one 16-B load for D = 128), so a wave streams 4 keys per load instruction
-// and the 4 waves 16 keys per step; scores reduce inside the 16-lane group with xor-shuffles.
-// Online softmax per lane group, merged across groups/waves at the end. The key range of a query
-// is cut into `n_splits` equal chunks computed ON DEVICE from its length (flash-decode), so the
-// grid is fixed and the launch is hipGraph-capturable for any context length; the last split
-// block to arrive (agent-scope release/acquire ticket) merges the partials in the same launch.
+// Grid (query, kv_head, split); one 512-thread block (8 waves) serves the G = H/H_kv query heads that
+// share a KV head, so each K/V row is read once per group (GQA reuse). Design points (measured with
+// scripts/bench_attn.py, profiles/r1_attn):
+//  * 16 lanes cooperate on one key (D/16 dims each: one 16-B load for D = 128); a wave's 4 DPP rows
+//    are 4 key groups, the block's 32 groups x U = 4 slots (2 when G = 8) stream 128 keys per step.
+//  * Software pipeline: the next step's K/V loads are in flight while the current step computes
+//    (explicit register ping-pong), so a long range costs one HBM round trip, not one per step.
+//  * The split's slice of the block table is staged in LDS up front: K/V addresses never wait on a
+//    dependent global load inside the loop.
+//  * q.k reductions are 16-lane DPP sums (no LDS permutes); the online softmax is batched per step
+//    (one max/rescale per 4 keys).
+//  * Flash-decode split count is decided ON DEVICE from the length: S_eff = min(n_splits,
+//    ceil(keys / 256)). Short contexts (the common decode case) therefore run one block per head
+//    with no cross-block merge at all; long ones split, and the last split block to arrive (agent-
+//    scope ticket, sc1 write-through partials: MI355X_MICROARCH.md hand-off form, no fences) merges
+//    in the same launch. The grid is fixed, so the launch is hipGraph-capturable for any length.
 // Causal prefill uses the same kernel: each prompt token is a query with length pos + 1.
 #include "common.h"
 #include "ops.h"
 
 namespace omx {
 
+constexpr int ATT_NW = 8;               // waves per block
+constexpr int ATT_NT = 64 * ATT_NW;
+constexpr int ATT_NG = 4 * ATT_NW;      // key groups (16 lanes each) per block
+constexpr int ATT_KPS = 256;            // target keys per split
+constexpr int ATT_BTW = 1024;           // block-table entries staged in LDS per window
+
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float row16_sum_a(float v) {
+  v += dppf<0xB1>(v);
+  v += dppf<0x4E>(v);
+  v += dppf<0x141>(v);
+  v += dppf<0x140>(v);
+  return v;
+}
+
+// one key's D/16 fp16 values for this lane, loaded with the widest aligned vector
 template <int DPL>
-__device__ __forceinline__ void load_row(const f16* p, float* v) {
+struct KRow {
+  f16 v[DPL];
+};
+template <int DPL>
+__device__ __forceinline__ void load_krow(const f16* p, KRow<DPL>& r) {
   if constexpr (DPL == 8) {
-    const f16x8 t = *(const f16x8*)p;
+    const f16x8 t = __builtin_nontemporal_load((const f16x8*)p);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = (float)t[j];
+    for (int j = 0; j < 8; ++j) r.v[j] = t[j];
   } else if constexpr (DPL == 4) {
     const f16x4 t = *(const f16x4*)p;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = (float)t[j];
+    for (int j = 0; j < 4; ++j) r.v[j] = t[j];
+  } else if constexpr (DPL % 2 == 0) {
+#pragma unroll
+    for (int j = 0; j < DPL; j += 2) {
+      const f16x2 t = *(const f16x2*)(p + j);
+      r.v[j] = t[0];
+      r.v[j + 1] = t[1];
+    }
   } else {
 #pragma unroll
-    for (int j = 0; j < DPL; ++j) v[j] = (float)p[j];
+    for (int j = 0; j < DPL; ++j) r.v[j] = p[j];
   }
 }
 
-template <int D, int G>
-__global__ __launch_bounds__(256) void attn_partial_kernel(AttnParams P) {
+template <int DPL, int U>
+struct KVStep {
+  KRow<DPL> k[U], v[U];
+};
+
+// U key slots per lane group per step: 4, or 2 when 8 query heads share a KV head (registers)
+template <int D, int G, int U = (G >= 8 ? 2 : 4)>
+__global__ __launch_bounds__(ATT_NT) void attn_decode_kernel(AttnParams P) {
   constexpr int DPL = D / 16;
-  __shared__ float sm[4][G][D + 2];
-  const int qi = blockIdx.x, kvh = blockIdx.y, split = blockIdx.z, S = gridDim.z;
+  constexpr int ATT_U = U, ATT_STEP = ATT_NG * U;
+  __shared__ float sm[ATT_NW][G][D + 2];
+  __shared__ int sbt[ATT_BTW];
+  const int qi = blockIdx.x, kvh = blockIdx.y, split = blockIdx.z;
   const int seq = P.q_seq ? P.q_seq[qi] : qi;
   const int len = P.q_len[qi];
   const int kstart = P.window > 0 ? max(0, len - P.window) : 0;
   const int nk = len - kstart;
+  const int S = max(1, min((int)gridDim.z, (nk + ATT_KPS - 1) / ATT_KPS));
+  if (split >= S) return;  // block-uniform: surplus splits of a short query leave immediately
   const int chunk = (nk + S - 1) / S;
   const int t0 = kstart + split * chunk;
   const int t1 = min(len, t0 + chunk);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, tg = lane >> 4, li = lane & 15;
+  const int grp = wave * 4 + tg;
 
   float q[G][DPL];
 #pragma unroll
@@ -62,42 +111,81 @@ __global__ __launch_bounds__(256) void attn_partial_kernel(AttnParams P) {
   const int* bt = P.block_table + (long long)seq * P.max_blocks;
   const f16* kc = (const f16*)P.kc;
   const f16* vc = (const f16*)P.vc;
-  // 4 key slots per lane group per step (64 keys per block-step): all K/V loads of a step are
-  // issued before any is consumed, so one HBM round trip covers 64 keys
-  constexpr int U = 4;
-  for (int ts = t0; ts < t1; ts += 16 * U) {
-    float k[U][DPL], v[U][DPL];
-    bool ok[U];
+  const int bs = P.bs;
+
+  // block-table windows (one window covers ATT_BTW * bs keys; a single one in practice)
+  for (int w0 = t0; w0 < t1; w0 += ATT_BTW * bs) {
+    const int w1 = min(t1, w0 + ATT_BTW * bs);
+    const int b0 = w0 / bs, nb = (w1 - 1) / bs - b0 + 1;
+    __syncthreads();  // previous window's readers are done with sbt
+    for (int i = threadIdx.x; i < nb; i += ATT_NT) sbt[i] = bt[b0 + i];
+    __syncthreads();
+
+    auto issue = [&](int ts, KVStep<DPL, U>& st) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int t = ts + u * 16 + wave * 4 + tg;
-      ok[u] = t < t1;
-      const int tt = ok[u] ? t : t0;
-      const long long blk = bt[tt / P.bs];
-      const long long base = ((blk * P.n_kv + kvh) * P.bs + (tt % P.bs)) * D + li * DPL;
-      load_row<DPL>(kc + base, k[u]);
-      load_row<DPL>(vc + base, v[u]);
-    }
+      for (int u = 0; u < ATT_U; ++u) {
+        const int t = min(ts + u * ATT_NG + grp, w1 - 1);  // clamped; masked at use
+        const long long blk = sbt[t / bs - b0];
+        const long long base = ((blk * P.n_kv + kvh) * bs + (t % bs)) * D + li * DPL;
+        load_krow<DPL>(kc + base, st.k[u]);
+        load_krow<DPL>(vc + base, st.v[u]);
+      }
+    };
+    auto consume = [&](int ts, const KVStep<DPL, U>& st) {
+      float sc[ATT_U][G];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (!ok[u]) continue;  // uniform within the 16-lane group
+      for (int u = 0; u < ATT_U; ++u) {
+        const bool ok = ts + u * ATT_NG + grp < w1;  // uniform within the 16-lane group
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          float s = 0.f;
+#pragma unroll
+          for (int j = 0; j < DPL; ++j) s += q[g][j] * (float)st.k[u].v[j];
+          s = row16_sum_a(s);
+          sc[u][g] = ok ? s : -INFINITY;
+        }
+      }
 #pragma unroll
       for (int g = 0; g < G; ++g) {
-        float sc = 0.f;
+        float mn = m[g];
 #pragma unroll
-        for (int j = 0; j < DPL; ++j) sc += q[g][j] * k[u][j];
-        sc = group_sum<16>(sc);
-        const float mn = fmaxf(m[g], sc);
+        for (int u = 0; u < ATT_U; ++u) mn = fmaxf(mn, sc[u][g]);
+        if (mn == -INFINITY) continue;  // nothing visible yet in this group
         const float corr = __expf(m[g] - mn);
-        const float p = __expf(sc - mn);
-        l[g] = l[g] * corr + p;
+        float p[ATT_U], ps = 0.f;
 #pragma unroll
-        for (int j = 0; j < DPL; ++j) acc[g][j] = acc[g][j] * corr + p * v[u][j];
+        for (int u = 0; u < ATT_U; ++u) {
+          p[u] = __expf(sc[u][g] - mn);
+          ps += p[u];
+        }
+        l[g] = l[g] * corr + ps;
+#pragma unroll
+        for (int j = 0; j < DPL; ++j) {
+          float a = acc[g][j] * corr;
+#pragma unroll
+          for (int u = 0; u < ATT_U; ++u) a += p[u] * (float)st.v[u].v[j];
+          acc[g][j] = a;
+        }
         m[g] = mn;
       }
+    };
+
+    KVStep<DPL, U> A, B;
+    int ts = w0;
+    issue(ts, A);
+    while (true) {
+      if (ts + ATT_STEP < w1) issue(ts + ATT_STEP, B);
+      consume(ts, A);
+      ts += ATT_STEP;
+      if (ts >= w1) break;
+      if (ts + ATT_STEP < w1) issue(ts + ATT_STEP, A);
+      consume(ts, B);
+      ts += ATT_STEP;
+      if (ts >= w1) break;
     }
   }
-  // merge the 4 token groups of the wave (lanes li, li+16, li+32, li+48)
+
+  // merge the 4 key groups of the wave (lanes li, li+16, li+32, li+48)
 #pragma unroll
   for (int sh = 16; sh <= 32; sh <<= 1) {
 #pragma unroll
@@ -124,16 +212,16 @@ __global__ __launch_bounds__(256) void attn_partial_kernel(AttnParams P) {
     }
   }
   __syncthreads();
-  // 4 waves merge: threads (g, d) over G*D outputs
-  for (int i = threadIdx.x; i < G * D; i += 256) {
+  // merge the waves: threads over the G*D outputs
+  for (int i = threadIdx.x; i < G * D; i += ATT_NT) {
     const int g = i / D, d = i % D;
     float M = -INFINITY;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) M = fmaxf(M, sm[w][g][D]);
+    for (int w = 0; w < ATT_NW; ++w) M = fmaxf(M, sm[w][g][D]);
     float L = 0.f, A = 0.f;
     if (M != -INFINITY) {
 #pragma unroll
-      for (int w = 0; w < 4; ++w) {
+      for (int w = 0; w < ATT_NW; ++w) {
         const float c = __expf(sm[w][g][D] - M);
         L += sm[w][g][D + 1] * c;
         A += sm[w][g][d] * c;
@@ -143,7 +231,7 @@ __global__ __launch_bounds__(256) void attn_partial_kernel(AttnParams P) {
     if (S == 1) {
       P.out[(long long)qi * P.ldo + h * D + d] = L > 0.f ? A / L : 0.f;
     } else {  // write-through (sc1) stores: the hand-off below then needs no release fence
-      float* ws = P.ws + (((long long)qi * P.H + h) * S + split) * (D + 2);
+      float* ws = P.ws + (((long long)qi * P.H + h) * gridDim.z + split) * (D + 2);
       __hip_atomic_store(ws + d, A, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (d == 0) {
         __hip_atomic_store(ws + D, M, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -154,9 +242,8 @@ __global__ __launch_bounds__(256) void attn_partial_kernel(AttnParams P) {
   if (S == 1) return;
   // ---- in-launch split combine (cdna_hip_programming.md §6 Guideline 16 / MI355X_MICROARCH.md
   // "Valid forms" row 1): partials were stored sc1; every wave drains them (vmcnt(0)), the block
-  // barriers, one lane takes an agent-scope ticket. The block drawing the last ticket reads every
-  // partial with sc1 loads (no acquire needed) and merges its G heads. Saves the separate
-  // combine launch (~4.5 us per layer at batch 1).
+  // barriers, one lane takes an agent-scope ticket. The block drawing the last of S tickets reads
+  // every partial with sc1 loads (no acquire needed) and merges its G heads.
   __shared__ int s_last;
   __shared__ float sw[G][64];
   __shared__ float sL[G];
@@ -176,7 +263,7 @@ __global__ __launch_bounds__(256) void attn_partial_kernel(AttnParams P) {
     const int s = threadIdx.x;
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-      const float* ws = P.ws + (((long long)qi * P.H + kvh * G + g) * S + (s < S ? s : 0)) * (D + 2);
+      const float* ws = P.ws + (((long long)qi * P.H + kvh * G + g) * gridDim.z + (s < S ? s : 0)) * (D + 2);
       const float lv = ld1(ws + D + 1);
       const bool live = s < S && lv > 0.f;
       const float mm = live ? ld1(ws + D) : -INFINITY;
@@ -188,9 +275,9 @@ __global__ __launch_bounds__(256) void attn_partial_kernel(AttnParams P) {
     }
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < G * D; i += 256) {
+  for (int i = threadIdx.x; i < G * D; i += ATT_NT) {
     const int g = i / D, d = i % D;
-    const float* ws = P.ws + ((long long)qi * P.H + kvh * G + g) * S * (D + 2);
+    const float* ws = P.ws + ((long long)qi * P.H + kvh * G + g) * gridDim.z * (D + 2);
     float A = 0.f;
 #pragma unroll 8
     for (int s = 0; s < S; ++s) A += sw[g][s] * ld1(ws + s * (D + 2) + d);
@@ -204,10 +291,10 @@ static void launch_d(const AttnParams& P, hipStream_t s) {
   const int G = P.H / P.n_kv;
   dim3 grid(P.NQ, P.n_kv, P.n_splits);
   switch (G) {
-    case 1: hipLaunchKernelGGL((attn_partial_kernel<D, 1>), grid, dim3(256), 0, s, P); break;
-    case 2: hipLaunchKernelGGL((attn_partial_kernel<D, 2>), grid, dim3(256), 0, s, P); break;
-    case 4: hipLaunchKernelGGL((attn_partial_kernel<D, 4>), grid, dim3(256), 0, s, P); break;
-    case 8: hipLaunchKernelGGL((attn_partial_kernel<D, 8>), grid, dim3(256), 0, s, P); break;
+    case 1: hipLaunchKernelGGL((attn_decode_kernel<D, 1>), grid, dim3(ATT_NT), 0, s, P); break;
+    case 2: hipLaunchKernelGGL((attn_decode_kernel<D, 2>), grid, dim3(ATT_NT), 0, s, P); break;
+    case 4: hipLaunchKernelGGL((attn_decode_kernel<D, 4>), grid, dim3(ATT_NT), 0, s, P); break;
+    case 8: hipLaunchKernelGGL((attn_decode_kernel<D, 8>), grid, dim3(ATT_NT), 0, s, P); break;
     default: break;
   }
 }
@@ -221,7 +308,6 @@ void attention_decode(const AttnParams& P, hipStream_t s) {
     case 128: launch_d<128>(P, s); break;
     default: break;
   }
-  // split partials are merged in-launch by the last-arriving block (see attn_partial_kernel)
 }
 
 size_t attention_ws_floats(int NQ, int H, int D, int n_splits) {

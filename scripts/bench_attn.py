@@ -1,0 +1,79 @@
+"""Decode-attention microbenchmark: paged fp16 KV, one query per sequence, per-call latency vs context
+length and flash-decode split count. Also times the GEMV fixed cost (tiny N) with / without the fused
+RMSNorm prologue and an empty-ish launch, to split per-kernel overhead from bandwidth.
+Run on the GPU box:  python scripts/bench_attn.py"""
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from ollama_operator_amd.gguf import GGMLType  # noqa: E402
+from ollama_operator_amd.ops import native  # noqa: E402
+from ollama_operator_amd.quant import random_blocks, repack  # noqa: E402
+
+
+def timeit(fn, n=200):
+    for _ in range(10):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(n):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) * 1e3 / n
+
+
+def attn_sweep(C, s):
+    bs = 16
+    for H, Hkv, D in ((32, 32, 128), (32, 8, 128)):
+        for L in (64, 200, 512, 1024, 4096):
+            nblk = (L + bs - 1) // bs
+            kc = torch.randn(nblk, Hkv, bs, D, device="cuda").half()
+            vc = torch.randn(nblk, Hkv, bs, D, device="cuda").half()
+            bt = torch.arange(nblk, device="cuda", dtype=torch.int32)
+            qlen = torch.tensor([L], device="cuda", dtype=torch.int32)
+            q = torch.randn(1, H * D, device="cuda")
+            out = torch.empty(1, H * D, device="cuda")
+            row = []
+            for S in (1, 2, 4, 8, 16, 32):
+                ws = torch.empty(max(1, C.attention_ws_floats(1, H, D, S)), device="cuda")
+                cnt = torch.zeros(Hkv, device="cuda", dtype=torch.int32)
+                fn = lambda: C.attention(q.data_ptr(), H * D, kc.data_ptr(), vc.data_ptr(), bt.data_ptr(), nblk,  # noqa
+                                         0, qlen.data_ptr(), 1, H, Hkv, D, bs, D ** -0.5, 0, out.data_ptr(), H * D,
+                                         ws.data_ptr(), S, cnt.data_ptr(), s)
+                row.append(f"S={S}:{timeit(fn):6.2f}")
+            print(f"attn H={H} Hkv={Hkv} D={D} L={L:5d}  " + "  ".join(row) + "  (us)", flush=True)
+
+
+def gemv_fixed(C, s):
+    rng = np.random.default_rng(0)
+    K = 4096
+    for N in (64, 1024, 4096):
+        raw = random_blocks(GGMLType.Q4_K, N, K, rng)
+        st = repack(raw, GGMLType.Q4_K, N, K)
+        ts = [torch.from_numpy(np.ascontiguousarray(st[n])).cuda() for n in ("qs", "meta")]
+        tup = (ts[0].data_ptr(), ts[1].data_ptr(), 0, 0, N, K, int(GGMLType.Q4_K))
+        x = torch.randn(1, K, device="cuda")
+        nw = torch.ones(K, device="cuda")
+        y = torch.zeros(1, N, device="cuda")
+        for norm in (0, 1):
+            fn = lambda: C.gemv(tup, 1, x.data_ptr(), K, norm, nw.data_ptr(), 0, 1e-5, 0, y.data_ptr(), N, 0, 0, {}, s)  # noqa
+            print(f"gemv Q4_K N={N:5d} K={K} norm={norm}: {timeit(fn):6.2f} us (MALL-resident weights)", flush=True)
+    a = torch.zeros(256, device="cuda")
+    b = torch.zeros(256, device="cuda")
+    print(f"add_inplace 256 floats (launch floor): {timeit(lambda: C.add_inplace(a.data_ptr(), b.data_ptr(), 256, s)):6.2f} us")
+
+
+def main():
+    C = native()
+    s = torch.cuda.current_stream().cuda_stream
+    gemv_fixed(C, s)
+    attn_sweep(C, s)
+
+
+if __name__ == "__main__":
+    main()
