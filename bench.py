@@ -76,7 +76,8 @@ def main():
 
     ctx = a.prompt + a.warmup + a.steps + 64
     t_load = time.perf_counter()
-    runner = Runner(path, device=f"cuda:{local}", max_batch=64, max_seqs=1, ctx=ctx)
+    runner = Runner(path, device=f"cuda:{local}", max_batch=512, max_seqs=1, ctx=ctx)
+    runner.warmup()  # load-time decode-graph capture, as the server does at model load
     torch.cuda.synchronize()
     load_s = time.perf_counter() - t_load
 

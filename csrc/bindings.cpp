@@ -114,6 +114,11 @@ PYBIND11_MODULE(_C, m) {
     P.bias = Pp<const float>(bias);
     P.row_offset = row_offset;
     P.n_sel = 1;
+    if (qkv.contains("xws")) P.xws = Pp<void>(qkv["xws"].cast<uintptr_t>());  // enables the GEMM path
+    if (qkv.contains("gws")) {  // split-K slabs for small-M GEMMs
+      P.gws = Pp<float>(qkv["gws"].cast<uintptr_t>());
+      P.gws_elems = qkv["gws_elems"].cast<long long>();
+    }
     if (epi == EPI_QKV) {
       P.pos = Pp<const int>(qkv["pos"].cast<uintptr_t>());
       P.slot = Pp<const int>(qkv["slot"].cast<uintptr_t>());
@@ -278,6 +283,9 @@ PYBIND11_MODULE(_C, m) {
         w.ew = Pp<float>(ptr("ew"));
         w.attn_ws = Pp<float>(ptr("attn_ws"));
         w.attn_cnt = Pp<int>(ptr("attn_cnt"));
+        w.x16 = Pp<void>(ptr("x16"));
+        w.gws = Pp<float>(ptr("gws"));
+        w.gws_elems = d.contains("gws_elems") ? d["gws_elems"].cast<long long>() : 0;
         w.max_B = d["max_B"].cast<int>();
         w.n_splits = d["n_splits"].cast<int>();
       })

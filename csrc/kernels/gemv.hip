@@ -28,6 +28,7 @@
 // Reference parity: the reference delegates all of this to llama.cpp inside `ollama/ollama`
 // (reference pkg/model/pod.go:10-12); numerics are checked against quant.py + an fp32 torch GEMV.
 #include "common.h"
+#include "epilogue.h"
 #include "ops.h"
 
 namespace omx {
@@ -343,59 +344,7 @@ __device__ __forceinline__ void finish_rows(const GemvParams& P, float (&acc)[R]
       const int n = row0 + r;
       const int bb = b0 + b;
       if (n >= N || bb >= P.B) continue;
-      float v = acc[r][b];
-      const float pv0 = part[r][b];
-      const int vn = n + P.row_offset;  // row index in the virtual (concatenated) matrix
-      switch (P.epi) {
-        case EPI_STORE:
-          if (P.bias) v += P.bias[vn];
-          P.y[(long long)bb * P.ldy + vn] = v;
-          break;
-        case EPI_ADD: {
-          if (P.bias) v += P.bias[vn];
-          if (P.expert_w) v *= P.expert_w[bb * P.n_sel + blockIdx.z];
-          float* dst = P.y + (long long)bb * P.ldy + vn;
-          if (P.expert_ids && P.n_sel > 1) atomicAdd(dst, v);
-          else *dst += v;
-          break;
-        }
-        case EPI_GELU:
-          if (P.bias) v += P.bias[vn];
-          P.y[(long long)bb * P.ldy + vn] = gelu_tanh(v);
-          break;
-        case EPI_GLU:
-          if ((vn & 1) == 0)  // even row = gate, odd row = up
-            P.y[(long long)bb * P.ldy + (long long)blockIdx.z * P.y_sel_stride + vn / 2] = silu(v) * pv0;
-          break;
-        case EPI_QKV: {
-          const int Eq = P.Eq, Ekv = P.Ekv, D = P.D;
-          int which, hh, d;
-          if (vn < Eq) { which = 0; hh = vn / D; d = vn % D; }
-          else if (vn < Eq + Ekv) { which = 1; hh = (vn - Eq) / D; d = (vn - Eq) % D; }
-          else { which = 2; hh = (vn - Eq - Ekv) / D; d = (vn - Eq - Ekv) % D; }
-          if (P.bias) v += P.bias[vn];
-          float out = v;
-          if (which < 2 && d < P.n_rot) {
-            float pv = pv0;
-            if (P.bias) pv += P.bias[vn ^ 1];
-            const float ang = (float)P.pos[bb] * P.inv_freq[d >> 1];
-            float sn, cs;
-            sincosf(ang, &sn, &cs);
-            out = (d & 1) ? (pv * sn + v * cs) : (v * cs - pv * sn);
-          }
-          if (which == 0) {
-            P.y[(long long)bb * P.ldy + vn] = out;
-          } else {
-            const int slot = P.slot[bb];
-            const long long blk = slot / P.bs, off = slot % P.bs;
-            const long long idx = ((blk * P.n_kv + hh) * P.bs + off) * D + d;
-            // two explicit stores: a pointer select here is lowered to an indexed scratch array
-            if (which == 1) ((f16*)P.kc)[idx] = (f16)out;
-            else ((f16*)P.vc)[idx] = (f16)out;
-          }
-          break;
-        }
-      }
+      epi_apply(P, bb, n + P.row_offset, acc[r][b], part[r][b], blockIdx.z);
     }
   }
 }
@@ -535,6 +484,10 @@ static void launch_q(const GemvParams& P, hipStream_t s) {
 }
 
 void gemv(const GemvParams& P, hipStream_t s) {
+  if (gemm_eligible(P)) {
+    gemm(P, s);
+    return;
+  }
   switch (P.w.qtype) {
     case QT_Q4_K: launch_q<QT_Q4_K>(P, s); break;
     case QT_Q6_K: launch_q<QT_Q6_K>(P, s); break;

@@ -40,9 +40,19 @@ struct GemvParams {
   int x_per_sel;               // x has one row-block per selected expert (down proj)
   long long x_sel_stride;      // elements between experts' x (within batch row b)
   long long y_sel_stride;      // elements between experts' y (EPI_GLU output)
+  // prefill GEMM path: fp16 activation scratch, >= B * K halves (null -> always the GEMV)
+  void* xws;
+  // split-K partial slabs for small-M GEMMs: fp32 [splits][B][N], capacity gws_elems (0 -> no split)
+  float* gws;
+  long long gws_elems;
 };
 
+// y = epi(W x): the quantised GEMV for small B (decode), the MFMA dequant GEMM for B >= GEMM_MIN_B
+// when an fp16 activation workspace is given (prefill); same epilogues either way.
 void gemv(const GemvParams& P, hipStream_t s);
+constexpr int GEMM_MIN_B = 16;
+bool gemm_eligible(const GemvParams& P);
+void gemm(const GemvParams& P, hipStream_t s);
 
 // launch-shape knobs for the decode GEMV (tuned on MI355X; see scripts/bench_gemv.py)
 struct GemvTuning {

@@ -5,8 +5,11 @@
 
 namespace omx {
 
-static GemvParams base_params(const QMat& w, int B, const float* x, int ldx) {
+static GemvParams base_params(const QMat& w, int B, const float* x, int ldx, const Workspace& ws) {
   GemvParams P{};
+  P.xws = ws.x16;
+  P.gws = ws.gws;
+  P.gws_elems = ws.gws_elems;
   P.w = w;
   P.B = B;
   P.x = x;
@@ -25,7 +28,7 @@ void Executor::attn_block(int i, const StepInputs& in, hipStream_t s) {
   const int B = in.B, E = cfg.E, Eq = cfg.H * cfg.D, Ekv = cfg.Hkv * cfg.D;
   const bool phi = cfg.arch == 1;
   // --- QKV projection: fused norm prologue, RoPE + paged K/V scatter epilogue
-  GemvParams P = base_params(L.wqk, B, ws.resid, E);
+  GemvParams P = base_params(L.wqk, B, ws.resid, E, ws);
   P.norm = phi ? NORM_LAYER : NORM_RMS;
   P.norm_w = L.attn_norm;
   P.norm_b = L.attn_norm_b;
@@ -53,7 +56,7 @@ void Executor::attn_block(int i, const StepInputs& in, hipStream_t s) {
     gemv(V, s);
   }
   if (phi) {  // parallel block: FFN up reads the same normed input, before O touches resid
-    GemvParams U = base_params(L.wgu, B, ws.resid, E);
+    GemvParams U = base_params(L.wgu, B, ws.resid, E, ws);
     U.norm = NORM_LAYER;
     U.norm_w = L.attn_norm;
     U.norm_b = L.attn_norm_b;
@@ -88,7 +91,7 @@ void Executor::attn_block(int i, const StepInputs& in, hipStream_t s) {
   A.counters = ws.attn_cnt;
   attention_decode(A, s);
   // --- output projection (+ residual, or partial sum under TP)
-  GemvParams O = base_params(L.wo, B, ws.abuf, Eq);
+  GemvParams O = base_params(L.wo, B, ws.abuf, Eq, ws);
   O.bias = L.bo;
   if (cfg.tp > 1) {
     O.epi = EPI_STORE;
@@ -107,7 +110,7 @@ void Executor::ffn_block(int i, const StepInputs& in, hipStream_t s) {
   float* dst = cfg.tp > 1 ? ws.ypart : ws.resid;
   const int dst_epi = cfg.tp > 1 ? EPI_STORE : EPI_ADD;
   if (cfg.arch == 1) {  // phi2: up+GELU already done in attn_block
-    GemvParams Dn = base_params(L.wdown, B, ws.hbuf, F);
+    GemvParams Dn = base_params(L.wdown, B, ws.hbuf, F, ws);
     Dn.epi = dst_epi;
     Dn.bias = L.bdown;
     Dn.y = dst;
@@ -117,7 +120,7 @@ void Executor::ffn_block(int i, const StepInputs& in, hipStream_t s) {
   }
   if (cfg.n_expert > 0) {
     const int X = cfg.n_expert, k = cfg.n_expert_used;
-    GemvParams R = base_params(L.router, B, ws.resid, E);
+    GemvParams R = base_params(L.router, B, ws.resid, E, ws);
     R.norm = NORM_RMS;
     R.norm_w = L.ffn_norm;
     R.eps = cfg.eps;
@@ -126,7 +129,7 @@ void Executor::ffn_block(int i, const StepInputs& in, hipStream_t s) {
     R.ldy = X;
     gemv(R, s);
     moe_route(ws.rlogits, B, X, k, ws.eids, ws.ew, s);
-    GemvParams G = base_params(L.gu_exps, B, ws.resid, E);
+    GemvParams G = base_params(L.gu_exps, B, ws.resid, E, ws);
     G.norm = NORM_RMS;
     G.norm_w = L.ffn_norm;
     G.eps = cfg.eps;
@@ -138,7 +141,7 @@ void Executor::ffn_block(int i, const StepInputs& in, hipStream_t s) {
     G.y_sel_stride = F;
     gemv(G, s);
     if (cfg.tp > 1) hipMemsetAsync(ws.ypart, 0, sizeof(float) * (size_t)B * E, s);
-    GemvParams Dn = base_params(L.down_exps, B, ws.hbuf, k * F);
+    GemvParams Dn = base_params(L.down_exps, B, ws.hbuf, k * F, ws);
     Dn.epi = EPI_ADD;  // expert-weighted, atomically accumulated
     Dn.y = dst;
     Dn.ldy = E;
@@ -150,7 +153,7 @@ void Executor::ffn_block(int i, const StepInputs& in, hipStream_t s) {
     gemv(Dn, s);
     return;
   }
-  GemvParams G = base_params(L.wgu, B, ws.resid, E);
+  GemvParams G = base_params(L.wgu, B, ws.resid, E, ws);
   G.norm = NORM_RMS;
   G.norm_w = L.ffn_norm;
   G.eps = cfg.eps;
@@ -158,7 +161,7 @@ void Executor::ffn_block(int i, const StepInputs& in, hipStream_t s) {
   G.y = ws.hbuf;
   G.ldy = F;
   gemv(G, s);
-  GemvParams Dn = base_params(L.wdown, B, ws.hbuf, F);
+  GemvParams Dn = base_params(L.wdown, B, ws.hbuf, F, ws);
   Dn.epi = dst_epi;
   Dn.y = dst;
   Dn.ldy = E;
@@ -173,7 +176,7 @@ void Executor::head(const StepInputs& in, hipStream_t s) {
     gather_rows(ws.resid, E, in.logit_idx, in.n_logits, E, ws.lbuf, s);
     x = ws.lbuf;
   }
-  GemvParams P = base_params(lm_head, in.n_logits, x, E);
+  GemvParams P = base_params(lm_head, in.n_logits, x, E, ws);
   P.norm = cfg.arch == 1 ? NORM_LAYER : NORM_RMS;
   P.norm_w = out_norm;
   P.norm_b = out_norm_b;

@@ -54,6 +54,9 @@ struct Workspace {
   float* ew = nullptr;       // [maxB][n_sel]
   float* attn_ws = nullptr;  // split-K workspace
   int* attn_cnt = nullptr;   // [maxB][Hkv] split arrival tickets (zero-initialised)
+  void* x16 = nullptr;       // [maxB][max K] fp16 activations for the prefill MFMA GEMM
+  float* gws = nullptr;      // split-K partial slabs for small-M prefill GEMMs
+  long long gws_elems = 0;
   int max_B = 0;
   int n_splits = 1;
 };

@@ -27,6 +27,7 @@ from .sampling import SamplingOptions, sample_host
 from .weights import DeviceWeights
 
 HIST_CAP = 256
+GEMM_SPLIT_WS_FLOATS = 8 << 20  # 32 MiB of fp32 split-K slabs (prefill GEMMs at small M)
 
 
 class NativeExec:
@@ -55,7 +56,9 @@ class NativeExec:
             e.set_layer(i, d)
         e.set_workspace(dict(resid=p(r.resid), qbuf=p(r.qbuf), abuf=p(r.abuf), hbuf=p(r.hbuf), ypart=p(r.ypart),
                              lbuf=p(r.lbuf), rlogits=p(r.rlogits), eids=p(r.eids), ew=p(r.ew),
-                             attn_ws=p(r.attn_ws), attn_cnt=p(r.attn_cnt), max_B=r.max_batch, n_splits=1))
+                             attn_ws=p(r.attn_ws), attn_cnt=p(r.attn_cnt), x16=p(r.x16), gws=p(r.gws),
+                             gws_elems=r.gws.numel(), max_B=r.max_batch,
+                             n_splits=1))
         self.inputs = dict(tokens=p(r.d_tokens), pos=p(r.d_pos), slot=p(r.d_slot), q_len=p(r.d_qlen),
                            q_seq=p(r.d_qseq), block_table=p(r.d_block_table), max_blocks=r.max_blocks,
                            bs=r.block_size, logits=p(r.logits))
@@ -116,6 +119,10 @@ class Runner:
         self.rlogits = torch.zeros(max_batch, max(1, cfg.n_expert), **f32)
         self.eids = torch.zeros(max_batch, ksel, **i32)
         self.ew = torch.zeros(max_batch, ksel, **f32)
+        # fp16 activations for the prefill MFMA GEMM (any GEMM input: E, H*D, F, k*F wide)
+        self.x16 = torch.zeros(max_batch * max(E, Eq, ksel * Fl), device=dev, dtype=torch.float16)
+        # split-K partial slabs of small-M prefill GEMMs (the kernel picks splits that fit)
+        self.gws = torch.zeros(GEMM_SPLIT_WS_FLOATS if str(dev).startswith("cuda") else 1, **f32)
         ws = max(self._ws_floats(B) for B in range(1, max_batch + 1))
         self.attn_ws = torch.zeros(max(ws, 1), **f32)
         self.attn_cnt = torch.zeros(max_batch * loc["Hkv"], **i32)  # self re-arming tickets
@@ -314,6 +321,14 @@ class Runner:
                 self._decode_body(B)
             self.graphs[B] = g
         return g
+
+    def warmup(self) -> None:
+        """Load-time warm-up (as Ollama does at model load): capture the batch-1 decode graph so the
+        first request's time-to-first-token does not pay for it. Scratch KV writes land in slot 0,
+        which any sequence overwrites at prefill before reading."""
+        if self.is_gpu and self.use_graphs:
+            self._graph(1)
+            torch.cuda.synchronize()
 
     def decode_step(self, sid: int) -> None:
         """One token for sequence `sid` whose input token (not yet in `tokens`) is already in

@@ -136,8 +136,10 @@ class ModelManager:
         tok = from_gguf_metadata(g.metadata)
         g.close()
         ctx_cap = int(os.environ.get("OMX_MAX_CTX", "0")) or None
-        runner = Runner(path, device=self.device, max_batch=int(os.environ.get("OMX_PREFILL_CHUNK", "64")),
+        # prefill chunk = MFMA GEMM M dimension (weights cross HBM once per chunk)
+        runner = Runner(path, device=self.device, max_batch=int(os.environ.get("OMX_PREFILL_CHUNK", "512")),
                         max_seqs=2, ctx=min(num_ctx, ctx_cap) if ctx_cap else num_ctx)
+        runner.warmup()
         return LoadedModel(name=name, digest=m.digest, path=path, runner=runner, tokenizer=tok,
                            template=self.store.text_layer(m, MT_TEMPLATE), system=self.store.text_layer(m, MT_SYSTEM),
                            params=self.store.params(m), num_ctx=runner.ctx, size=os.path.getsize(path),

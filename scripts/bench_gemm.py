@@ -1,0 +1,55 @@
+"""Prefill MFMA dequant-GEMM microbenchmark (csrc/kernels/gemm.hip) on Llama-2-7B Q4_K_M shapes:
+time per call and achieved TFLOP/s vs M (prompt tokens). Run on the GPU box:
+  python scripts/bench_gemm.py            (OMX_BENCH_SHAPES / OMX_BENCH_M filter for PMC runs)"""
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from ollama_operator_amd.gguf import GGMLType  # noqa: E402
+from ollama_operator_amd.ops import native  # noqa: E402
+from ollama_operator_amd.quant import REPACK_STREAMS, random_blocks, repack  # noqa: E402
+
+SHAPES = [("qkv", GGMLType.Q4_K, 12288, 4096), ("o", GGMLType.Q4_K, 4096, 4096),
+          ("gate_up", GGMLType.Q4_K, 22016, 4096), ("down_q4k", GGMLType.Q4_K, 4096, 11008),
+          ("down_q6k", GGMLType.Q6_K, 4096, 11008), ("q8_0", GGMLType.Q8_0, 4096, 4096)]
+
+
+def main():
+    C = native()
+    s = torch.cuda.current_stream().cuda_stream
+    keep = os.environ.get("OMX_BENCH_SHAPES")
+    ms = [int(v) for v in os.environ.get("OMX_BENCH_M", "128,512,2048").split(",")]
+    for name, qt, N, K in SHAPES:
+        if keep and name not in keep.split(","):
+            continue
+        st = repack(random_blocks(qt, N, K, np.random.default_rng(0)), qt, N, K)
+        ts = [torch.from_numpy(np.ascontiguousarray(st[n])).cuda() for n in REPACK_STREAMS[qt]]
+        p = [t.data_ptr() for t in ts] + [0] * (4 - len(ts))
+        tup = (p[0], p[1], p[2], p[3], N, K, int(qt))
+        for M in ms:
+            x = torch.randn(M, K, device="cuda")
+            y = torch.zeros(M, N, device="cuda")
+            xws = torch.empty(M * K, device="cuda", dtype=torch.float16)
+            gws = torch.empty(8 << 20, device="cuda")  # the runner's split-K workspace
+            fn = lambda: C.gemv(tup, M, x.data_ptr(), K, 0, 0, 0, 1e-5, 0, y.data_ptr(), N, 0, 0,  # noqa: E731
+                                {"xws": xws.data_ptr(), "gws": gws.data_ptr(), "gws_elems": gws.numel()}, s)
+            for _ in range(3):
+                fn()
+            torch.cuda.synchronize()
+            n = 20
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(n):
+                fn()
+            e1.record()
+            torch.cuda.synchronize()
+            us = e0.elapsed_time(e1) * 1e3 / n
+            print(f"{name:9s} {qt.name:5s} N={N:6d} K={K:6d} M={M:5d}: {us:9.1f} us  "
+                  f"{2 * M * N * K / us / 1e6:7.1f} TFLOP/s", flush=True)
+
+
+if __name__ == "__main__":
+    main()

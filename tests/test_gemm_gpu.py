@@ -1,0 +1,131 @@
+"""GPU numerics of the prefill MFMA dequant GEMM path (csrc/kernels/gemm.hip): the same `gemv` entry
+with an fp16 activation workspace and B >= GEMM_MIN_B, against a plain fp32 PyTorch reference on
+the dequantised weights. Covers every quant type, partial M/N tiles, K padding (Q4_0/Q8_0 with
+K % 256 != 0) and every fused epilogue."""
+import math
+
+import pytest
+import torch
+
+from ollama_operator_amd.gguf import GGMLType
+from test_kernels_gpu import QM, QTYPES, C, S, rel
+
+pytestmark = pytest.mark.gpu
+
+
+def gemm(m, x, norm=0, nw=None, nb=None, epi=0, y=None, bias=None, extra=None, eps=1e-5, split=True):
+    """split=True gives the kernel a split-K workspace (small M then runs split-K + finalize)."""
+    B, K = x.shape
+    xws = torch.empty(B * K, device="cuda", dtype=torch.float16)
+    gws = torch.empty(8 << 20, device="cuda")
+    p = lambda t: t.data_ptr() if t is not None else 0  # noqa: E731
+    d = dict(extra or {})
+    d["xws"] = xws.data_ptr()
+    if split:
+        d["gws"], d["gws_elems"] = gws.data_ptr(), gws.numel()
+    C().gemv(m.tup, B, p(x), K, norm, p(nw), p(nb), eps, epi, p(y), y.shape[1], p(bias), 0, d, S())
+    torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("qt", QTYPES)
+@pytest.mark.parametrize("B", [16, 40, 130])
+@pytest.mark.parametrize("K", [256, 4096, 11008, 288])
+@pytest.mark.parametrize("split", [True, False])
+def test_gemm_store(qt, B, K, split):
+    if K == 288 and qt in (GGMLType.Q4_K, GGMLType.Q6_K):
+        pytest.skip("k-quant rows are whole super-blocks")
+    N = 384 + 64  # partial N tile
+    m = QM(qt, N, K, seed=K + B)
+    x = torch.randn(B, K, device="cuda")
+    y = torch.zeros(B, N, device="cuda")
+    gemm(m, x, y=y, split=split)
+    assert rel(y, x @ m.w.T) < 1e-2
+
+
+def test_gemm_rmsnorm_add_bias():
+    N, K, B = 512, 2048, 33
+    m = QM(GGMLType.Q4_K, N, K, seed=3)
+    x = torch.randn(B, K, device="cuda") * 3
+    nw = torch.rand(K, device="cuda") + 0.5
+    bias = torch.randn(N, device="cuda")
+    y0 = torch.randn(B, N, device="cuda")
+    y = y0.clone()
+    gemm(m, x, norm=1, nw=nw, epi=1, y=y, bias=bias)
+    xn = x * torch.rsqrt(x.pow(2).mean(-1, keepdim=True) + 1e-5) * nw
+    ref = y0 + xn @ m.w.T + bias
+    assert rel(y - y0, ref - y0) < 1e-2
+
+
+def test_gemm_layernorm_gelu():
+    N, K, B = 512, 2560, 20
+    m = QM(GGMLType.Q4_0, N, K, seed=4)
+    x = torch.randn(B, K, device="cuda") + 0.3
+    nw, nb = torch.rand(K, device="cuda") + 0.5, torch.randn(K, device="cuda") * 0.1
+    bias = torch.randn(N, device="cuda") * 0.1
+    y = torch.zeros(B, N, device="cuda")
+    gemm(m, x, norm=2, nw=nw, nb=nb, epi=3, y=y, bias=bias)
+    xn = torch.nn.functional.layer_norm(x, (K,), nw, nb, 1e-5)
+    h = xn @ m.w.T + bias
+    ref = 0.5 * h * (1 + torch.tanh(math.sqrt(2 / math.pi) * (h + 0.044715 * h ** 3)))
+    assert rel(y, ref) < 1e-2
+
+
+@pytest.mark.parametrize("qt", [GGMLType.Q4_K, GGMLType.Q6_K])
+def test_gemm_glu(qt):
+    F, K, B = 320, 1024, 50
+    m = QM(qt, 2 * F, K, seed=5)
+    x = torch.randn(B, K, device="cuda")
+    y = torch.zeros(B, F, device="cuda")
+    gemm(m, x, epi=2, y=y)
+    gu = x @ m.w.T
+    ref = torch.nn.functional.silu(gu[:, 0::2]) * gu[:, 1::2]
+    assert rel(y, ref) < 1.5e-2
+
+
+@pytest.mark.parametrize("D,n_rot", [(128, 128), (80, 32)])
+def test_gemm_qkv_rope_kv_scatter(D, n_rot):
+    H, Hkv, K, B, bs = 4, 2, 512, 24, 16
+    Eq, Ekv = H * D, Hkv * D
+    N = Eq + 2 * Ekv
+    m = QM(GGMLType.Q4_K, N, K, seed=D)
+    x = torch.randn(B, K, device="cuda")
+    q = torch.zeros(B, Eq, device="cuda")
+    nblk = 4
+    kc = torch.zeros(nblk, Hkv, bs, D, device="cuda", dtype=torch.float16)
+    vc = torch.zeros_like(kc)
+    pos = torch.arange(B, device="cuda", dtype=torch.int32) + 7
+    slot = torch.arange(B, device="cuda", dtype=torch.int32) + 9  # distinct slots across 3 blocks
+    inv = (10000.0 ** (-torch.arange(0, n_rot // 2, dtype=torch.float64) * 2 / n_rot)).float().cuda()
+    extra = dict(pos=pos.data_ptr(), slot=slot.data_ptr(), kc=kc.data_ptr(), vc=vc.data_ptr(), inv_freq=inv.data_ptr(),
+                 Eq=Eq, Ekv=Ekv, D=D, n_rot=n_rot, n_kv=Hkv, bs=bs)
+    gemm(m, x, epi=4, y=q, extra=extra)
+    y = x @ m.w.T
+
+    def rope(t, nh):
+        t = t.view(B, nh, D).clone()
+        ang = pos.double()[:, None] * inv.double()[None, :]
+        c, s = torch.cos(ang).float()[:, None, :], torch.sin(ang).float()[:, None, :]
+        a, b = t[..., 0:n_rot:2].clone(), t[..., 1:n_rot:2].clone()
+        t[..., 0:n_rot:2] = a * c - b * s
+        t[..., 1:n_rot:2] = a * s + b * c
+        return t
+    assert rel(q.view(B, H, D), rope(y[:, :Eq], H)) < 1e-2
+    kr = rope(y[:, Eq:Eq + Ekv], Hkv)
+    vr = y[:, Eq + Ekv:].view(B, Hkv, D)
+    for b in range(B):
+        blk, off = int(slot[b]) // bs, int(slot[b]) % bs
+        assert rel(kc[blk, :, off].float(), kr[b]) < 1.2e-2
+        assert rel(vc[blk, :, off].float(), vr[b]) < 1.2e-2
+
+
+def test_gemm_matches_batched_gemv():
+    """Both B > 1 paths of the same matrix agree (GEMM fp16 vs GEMV int8-dot activations)."""
+    N, K, B = 1024, 4096, 64
+    m = QM(GGMLType.Q4_K, N, K, seed=11)
+    x = torch.randn(B, K, device="cuda")
+    y1 = torch.zeros(B, N, device="cuda")
+    y2 = torch.zeros(B, N, device="cuda")
+    gemm(m, x, y=y1)
+    C().gemv(m.tup, B, x.data_ptr(), K, 0, 0, 0, 1e-5, 0, y2.data_ptr(), N, 0, 0, {}, S())
+    torch.cuda.synchronize()
+    assert rel(y1, y2) < 1e-2
