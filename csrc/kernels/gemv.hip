@@ -35,11 +35,13 @@ namespace omx {
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
-constexpr int GEMV_NT = 256;  // 4 waves
+constexpr int GEMV_NW = 4;  // waves per block (8-wave blocks measured slower: profiles/r1_pmc)
+constexpr int GEMV_NT = 64 * GEMV_NW;
 constexpr int XPAD = 17;      // LDS x slots per super-block: 16 groups + 1 pad
 
 GemvTuning g_tune;
-void set_gemv_tuning(int blocks_per_cu, int rows, int) {
+void set_gemv_tuning(int blocks_per_cu, int rows, int debug) {
+  g_tune.debug = debug > 0 ? debug : 0;
   if (blocks_per_cu > 0) g_tune.blocks_per_cu = blocks_per_cu;
   if (rows == 1 || rows == 2) g_tune.rows = rows;
 }
@@ -350,13 +352,15 @@ __device__ __forceinline__ void finish_rows(const GemvParams& P, float (&acc)[R]
 }
 
 // ---------------------------------------------------------------------------------------------
-// Block = 4 waves x 4 row groups x R rows = 16R rows per tile. Work unit = (tile, K chunk of
+// Block = GEMV_NW waves x 4 row groups x R rows per tile. Work unit = (tile, K chunk of
 // 16*NSB super-blocks); blocks are persistent over units (tile += gridDim.x).
-template <int QT, int NSB, int R, int BT>
+// DBG (microbenchmark only, scripts/bench_gemv.py): bit 0 = replace the dot products by an XOR of
+// the loaded words (memory path alone), bit 1 = skip the activation prologue
+template <int QT, int NSB, int R, int BT, int DBG = 0>
 __global__ __launch_bounds__(GEMV_NT) void qgemv_kernel(GemvParams P) {
   constexpr int PB = QT == QT_Q8_0 ? 8 : QT == QT_Q6_K ? 6 : 4;  // VGPRs per piece
   constexpr bool DB = R * NSB * (8 * PB + 5) <= 80;               // room for a prefetch tile
-  constexpr int ROWS_W = 4 * R, ROWS_B = 4 * ROWS_W;
+  constexpr int ROWS_W = 4 * R, ROWS_B = GEMV_NW * ROWS_W;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const QMat& w = P.w;
   const int K = w.K, N = w.N, SB = n_sb(K);
@@ -384,6 +388,7 @@ __global__ __launch_bounds__(GEMV_NT) void qgemv_kernel(GemvParams P) {
 
 #pragma unroll
   for (int b = 0; b < BT; ++b) {
+    if (DBG & 2) break;
     if (b0 + b < P.B) {
       stage_x<GEMV_NT>(P, x + (long long)(b0 + b) * P.ldx, K, SB, lq + b * XS, lf + b * XS, red);
     } else {
@@ -415,7 +420,14 @@ __global__ __launch_bounds__(GEMV_NT) void qgemv_kernel(GemvParams P) {
       int nt = tile, ncc = c + 1;
       if (ncc == nc) { ncc = 0; nt += gridDim.x; }
       if (nt < n_tiles) load_wtile<QT, NSB, R>(w, row_base, nt * ROWS_B + rbase, N, SB, ncc * 16 * NSB, s, nxt);
-      compute_wtile<QT, NSB, R, BT>(cur, SB, c * 16 * NSB, s, lq, lf, XS, acc);
+      if constexpr (DBG & 1) {
+        unsigned v = 0;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) v ^= cur.a[0][0][t].x ^ cur.a[0][0][t].w;
+        acc[0][0] += (float)(v & 1);
+      } else {
+        compute_wtile<QT, NSB, R, BT>(cur, SB, c * 16 * NSB, s, lq, lf, XS, acc);
+      }
       if (c == nc - 1) finish(tile);
       tile = nt;
       c = ncc;
@@ -435,19 +447,185 @@ __global__ __launch_bounds__(GEMV_NT) void qgemv_kernel(GemvParams P) {
   }
 }
 
-static size_t lds_bytes(int K, int BT) { return (size_t)BT * ((K + 255) / 256) * XPAD * 24 + 64; }
+// ---------------------------------------------------------------------------------------------
+// Decode kernel, "all in flight" (B = 1, one K chunk). scripts/bench_gemv.py DBG variants showed the
+// persistent kernel above streams at the HBM ceiling only without its prologue and its dot products
+// (gate_up 9.0 us vs 15.1 us): vector loads return in issue order, so the prologue's activation
+// loads -- issued after the weight tiles -- waited for every tile, and the 2-deep register ping-pong
+// then left HBM idle while tiles computed. Here each thread first loads its activation groups (and
+// norm weights) into registers, THEN issues the loads of all J weight tiles of its block, computes
+// the norm + int8 quantisation from registers while the weights stream, and consumes the tiles in
+// order with counted vmcnt waits (fully unrolled), so HBM sees the whole matrix requested up front.
+template <int QT, int NSB, int R, int J>
+__global__ __launch_bounds__(GEMV_NT) void qgemv_flight_kernel(GemvParams P) {
+  constexpr int ROWS_B = GEMV_NW * 4 * R;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const QMat& w = P.w;
+  const int K = w.K, N = w.N, SB = n_sb(K);
+  const int XS = SB * XPAD;
+  i32x4* lq = (i32x4*)smem;
+  f32x2* lf = (f32x2*)(smem + (size_t)XS * 16);
+  float* red = (float*)(lf + XS);
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = lane >> 4, s = lane & 15;
+  const int n_tiles = (N + ROWS_B - 1) / ROWS_B;
+  const int rbase = wave * (4 * R) + g * R;
 
-template <int QT, int NSB, int R, int BT>
+  long long row_base = 0;
+  const float* x = P.x;
+  if (P.expert_ids) {  // MoE: blockIdx.z = k-th selected expert
+    const int e = P.expert_ids[blockIdx.z];
+    row_base = (long long)e * N;
+    if (P.x_per_sel) x = P.x + (long long)blockIdx.z * P.x_sel_stride;
+  }
+
+  // 1. this thread's activation groups g = tid + 256 i (i < NSB) and norm weights -> registers
+  const bool nrm = P.norm != NORM_NONE, lnb = P.norm == NORM_LAYER && P.norm_b;
+  f32x4 xv[NSB][4], nw[NSB][4], nb[NSB][4];
+  // unconditional loads from clamped / stand-in addresses (a conditional load would make the compiler
+  // drain it before the weight loads are issued); out-of-range values are masked at use
+  const float* nwp = nrm ? P.norm_w : x;
+  const float* nbp = lnb ? P.norm_b : x;
+#pragma unroll
+  for (int i = 0; i < NSB; ++i) {
+    const int gi = min(tid + GEMV_NT * i, K / 16 - 1);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      xv[i][j] = *(const f32x4*)(x + 16 * gi + 4 * j);
+      nw[i][j] = *(const f32x4*)(nwp + 16 * gi + 4 * j);
+      nb[i][j] = *(const f32x4*)(nbp + 16 * gi + 4 * j);
+    }
+  }
+  // 2. every weight tile of this block in flight (surplus slots re-read the last tile, unused)
+  WTile<QT, NSB, R> T[J];
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const int t = min((int)blockIdx.x + j * (int)gridDim.x, n_tiles - 1);
+    load_wtile<QT, NSB, R>(w, row_base, t * ROWS_B + rbase, N, SB, 0, s, T[j]);
+  }
+  // 3. norm statistics + quantisation from registers while the weights stream
+#pragma unroll
+  for (int i = 0; i < NSB; ++i) {
+    const bool ok = 16 * (tid + GEMV_NT * i) < K;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (!ok) xv[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      if (!nrm) nw[i][j] = (f32x4){1.f, 1.f, 1.f, 1.f};
+      if (!lnb) nb[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    }
+  }
+  float mean = 0.f, rstd = 1.f;
+  if (nrm) {
+    float sm = 0.f, ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < NSB; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const f32x4 v = xv[i][j];
+        sm += v.x + v.y + v.z + v.w;
+        ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+      }
+    ss = block_sum<GEMV_NT>(ss, red);
+    if (P.norm == NORM_LAYER) {
+      sm = block_sum<GEMV_NT>(sm, red);
+      mean = sm / K;
+      rstd = rsqrtf(fmaxf(ss / K - mean * mean, 0.f) + P.eps);
+    } else {
+      rstd = rsqrtf(ss / K + P.eps);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NSB; ++i) {
+    const int gi = tid + GEMV_NT * i;
+    if (gi >= SB * 16) continue;
+    const int slot = (gi >> 4) * XPAD + (gi & 15);
+    float v[16];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      f32x4 t = xv[i][j];
+      if (nrm) t = (t - mean) * rstd * nw[i][j] + nb[i][j];
+      v[4 * j] = t.x; v[4 * j + 1] = t.y; v[4 * j + 2] = t.z; v[4 * j + 3] = t.w;
+    }
+    if (16 * gi >= K) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) v[j] = 0.f;
+    }
+    float amax = 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) amax = fmaxf(amax, fabsf(v[j]));
+    const float d = amax / 127.f;
+    const float id = amax > 0.f ? 127.f / amax : 0.f;
+    int qsum = 0;
+    i32x4 pk;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      int word = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int q = (int)rintf(v[4 * j + k] * id);
+        qsum += q;
+        word |= (q & 0xFF) << (8 * k);
+      }
+      pk[j] = word;
+    }
+    lq[slot] = pk;
+    lf[slot] = (f32x2){d, d * (float)qsum};
+  }
+  __syncthreads();
+  // 4. consume the tiles in issue order
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const int t = (int)blockIdx.x + j * (int)gridDim.x;
+    if (t >= n_tiles) break;  // block-uniform
+    float acc[R][1];
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r][0] = 0.f;
+    compute_wtile<QT, NSB, R, 1>(T[j], SB, 0, s, lq, lf, XS, acc);
+    finish_rows<R, 1>(P, acc, t * ROWS_B + rbase, N, 0, s);
+  }
+}
+
+// register tiles a block keeps in flight: ~150 VGPRs of weight tiles per lane
+template <int QT, int NSB, int R>
+constexpr int flight_jmax() {
+  constexpr int PB = QT == QT_Q8_0 ? 8 : QT == QT_Q6_K ? 6 : 4;
+  constexpr int regs = R * NSB * (8 * PB + 5);
+  return regs * 3 <= 150 ? 3 : regs * 2 <= 150 ? 2 : 1;
+}
+
+static size_t lds_bytes(int K, int BT) { return (size_t)BT * ((K + 255) / 256) * XPAD * 24 + 4 * GEMV_NW; }
+
+template <int QT, int NSB, int R, int BT, int DBG = 0>
 static void launch_t(const GemvParams& P, hipStream_t s) {
   const int N = P.w.N;
-  const int tiles = (N + 16 * R - 1) / (16 * R);
+  const int tiles = (N + 4 * GEMV_NW * R - 1) / (4 * GEMV_NW * R);
   const int by = (P.B + BT - 1) / BT;
   const int bz = P.expert_ids ? P.n_sel : 1;
   int gx = tiles;
   const int slots = 256 * g_tune.blocks_per_cu;
   const int cap = slots / (by * bz) > 0 ? slots / (by * bz) : 1;
   if (gx > cap) gx = cap;
-  hipLaunchKernelGGL((qgemv_kernel<QT, NSB, R, BT>), dim3(gx, by, bz), dim3(GEMV_NT), lds_bytes(P.w.K, BT), s, P);
+  hipLaunchKernelGGL((qgemv_kernel<QT, NSB, R, BT, DBG>), dim3(gx, by, bz), dim3(GEMV_NT), lds_bytes(P.w.K, BT), s, P);
+}
+
+template <int QT, int NSB, int R, int J>
+static void launch_flight_j(const GemvParams& P, int gx, hipStream_t s) {
+  const int bz = P.expert_ids ? P.n_sel : 1;
+  hipLaunchKernelGGL((qgemv_flight_kernel<QT, NSB, R, J>), dim3(gx, 1, bz), dim3(GEMV_NT), lds_bytes(P.w.K, 1), s, P);
+}
+
+// grid: at least one block per CU while the matrix has the tiles, then up to J tiles per block
+template <int QT, int NSB, int R>
+static void launch_flight(const GemvParams& P, hipStream_t s) {
+  constexpr int JM = flight_jmax<QT, NSB, R>();
+  const int tiles = (P.w.N + 4 * GEMV_NW * R - 1) / (4 * GEMV_NW * R);
+  const int bz = P.expert_ids ? P.n_sel : 1;
+  const int want = (256 * g_tune.blocks_per_cu + bz - 1) / bz;  // blocks per (z) slice
+  int J = (tiles + want - 1) / want;
+  J = J < 1 ? 1 : J > JM ? JM : J;
+  const int gx = (tiles + J - 1) / J;
+  if (J == 1) launch_flight_j<QT, NSB, R, 1>(P, gx, s);
+  else if (J == 2) launch_flight_j<QT, NSB, R, (JM >= 2 ? 2 : 1)>(P, gx, s);
+  else launch_flight_j<QT, NSB, R, JM>(P, gx, s);
 }
 
 template <int QT, int R, int BT>
@@ -471,7 +649,26 @@ static void launch_nsb(const GemvParams& P, hipStream_t s) {
 
 template <int QT>
 static void launch_q(const GemvParams& P, hipStream_t s) {
+  if constexpr (QT == QT_Q4_K) {
+    if (g_tune.debug && P.B == 1 && (P.w.K + 255) / 256 <= 16) {
+      switch (g_tune.debug) {
+        case 1: launch_t<QT, 1, 1, 1, 1>(P, s); return;
+        case 2: launch_t<QT, 1, 1, 1, 2>(P, s); return;
+        default: launch_t<QT, 1, 1, 1, 3>(P, s); return;
+      }
+    }
+  }
   if (P.B == 1 || P.expert_ids != nullptr) {  // decode (and MoE: experts differ per batch row)
+    const int need = ((P.w.K + 255) / 256 + 15) / 16;
+    if (P.B == 1 && need <= 4) {  // whole K in one chunk: all-in-flight kernel
+      if (g_tune.rows == 2 && need == 1) { launch_flight<QT, 1, 2>(P, s); return; }
+      switch (need) {
+        case 1: launch_flight<QT, 1, 1>(P, s); return;
+        case 2: launch_flight<QT, 2, 1>(P, s); return;
+        case 3: launch_flight<QT, 3, 1>(P, s); return;
+        default: launch_flight<QT, 4, 1>(P, s); return;
+      }
+    }
     if (g_tune.rows == 2) launch_nsb<QT, 2, 1>(P, s);
     else launch_nsb<QT, 1, 1>(P, s);
     return;

@@ -58,9 +58,10 @@ void gemm(const GemvParams& P, hipStream_t s);
 struct GemvTuning {
   int blocks_per_cu = 4;  // persistent-grid cap = 256 CUs x this (scripts/bench_gemv.py sweep)
   int rows = 1;           // rows per 16-lane row group in B == 1 launches (1 or 2)
+  int debug = 0;          // microbenchmark-only kernel variants (gemv.hip DBG)
 };
 extern GemvTuning g_tune;
-void set_gemv_tuning(int blocks_per_cu, int rows, int reserved);
+void set_gemv_tuning(int blocks_per_cu, int rows, int debug);
 
 // Dequantize rows of a repacked matrix (embedding gather / fp16 copies)
 void embed_rows(const QMat& w, const int* rows, int n, float* out, int ldo, hipStream_t s);

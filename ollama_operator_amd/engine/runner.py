@@ -326,9 +326,17 @@ class Runner:
         """Load-time warm-up (as Ollama does at model load): capture the batch-1 decode graph so the
         first request's time-to-first-token does not pay for it. Scratch KV writes land in slot 0,
         which any sequence overwrites at prefill before reading."""
-        if self.is_gpu and self.use_graphs:
+        if not self.is_gpu:
+            return
+        # one short prompt through the prefill path (GEMM + prep/finalize kernels resolved once)
+        sid = self.new_sequence()
+        try:
+            self.prefill(sid, [self.cfg.bos_id] * min(self.max_batch, 32))
+        finally:
+            self.free_sequence(sid)
+        if self.use_graphs:
             self._graph(1)
-            torch.cuda.synchronize()
+        torch.cuda.synchronize()
 
     def decode_step(self, sid: int) -> None:
         """One token for sequence `sid` whose input token (not yet in `tokens`) is already in

@@ -47,7 +47,9 @@ def main():
     res = []
     keep = os.environ.get("OMX_BENCH_SHAPES", "").split(",") if os.environ.get("OMX_BENCH_SHAPES") else None
     mats = {name: make(qt, N, K) for name, qt, N, K, _ in SHAPES if keep is None or name in keep}
-    knobs = [(b, r, 0) for b in (2, 4, 8) for r in (1, 2)]
+    knobs = [(b, r, 0) for b in (1, 2, 4) for r in (1, 2)]
+    if os.environ.get("OMX_BENCH_DEBUG"):  # memory-path experiments on the Q4_K K=4096 kernel
+        knobs = [(b, 1, d) for b in (2, 4) for d in (0, 1, 2, 3)]
     if os.environ.get("OMX_BENCH_KNOBS"):  # e.g. "3,2,1" (profiling one configuration)
         knobs = [tuple(int(v) for v in os.environ["OMX_BENCH_KNOBS"].split(","))]
     shapes = SHAPES
@@ -74,7 +76,7 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) * 1e3 / n
-        res.append((name, f"blocks/CU={bpc} rows={rpw}", us, nbytes / us / 1e3))
+        res.append((name, f"blocks/CU={bpc} rows={rpw} dbg={r1}", us, nbytes / us / 1e3))
         print(f"{name:10s} {res[-1][1]} {us:8.2f} us  {nbytes/us/1e3:7.1f} GB/s", flush=True)
     C.set_gemv_tuning(4, 1, 0)
     print("best per shape:")
