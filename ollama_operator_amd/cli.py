@@ -83,10 +83,24 @@ def _progress(events):
 
 def cmd_serve(a):
     import uvicorn
+    from .parallel.tp import tp_size_from_env
     from .server.app import create_app
     _, host, port = parse_host(os.environ.get("OLLAMA_HOST"), for_server=True)
-    uvicorn.run(create_app(), host=host, port=port, log_level=os.environ.get("OMX_LOG_LEVEL", "info"),
-                timeout_keep_alive=300)
+    manager = None
+    world = None
+    tp = tp_size_from_env()
+    if tp > 1:  # OMX_TP: spawn the worker ranks before this process touches the GPU
+        from .parallel.tp import shutdown_leader, start_leader
+        from .server.manager import ModelManager
+        from .server.store import ModelStore
+        world = start_leader(tp)
+        manager = ModelManager(ModelStore(), tp_world=world)
+    try:
+        uvicorn.run(create_app(store=manager.store if manager else None, manager=manager), host=host, port=port,
+                    log_level=os.environ.get("OMX_LOG_LEVEL", "info"), timeout_keep_alive=300)
+    finally:
+        if world is not None:
+            shutdown_leader(world)
 
 
 def cmd_pull(a):

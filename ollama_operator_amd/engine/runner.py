@@ -22,6 +22,7 @@ import torch
 
 from ..ops import has_native, native, stream_handle
 from ..ops.reference import TorchExecutor
+from ..utils.trace import trace_range
 from .kv_cache import PagedKV
 from .sampling import SamplingOptions, sample_host
 from .weights import DeviceWeights
@@ -85,7 +86,8 @@ class StepTimes:
 class Runner:
     def __init__(self, model_path: str, device: str | None = None, max_batch: int = 64, max_seqs: int = 4,
                  ctx: int | None = None, block_size: int = 16, tp_rank: int = 0, tp_size: int = 1,
-                 tp_group=None, use_graphs: bool | None = None, weights: DeviceWeights | None = None):
+                 tp_group=None, use_graphs: bool | None = None, weights: DeviceWeights | None = None,
+                 tp_ctrl=None):
         t0 = time.perf_counter()
         if device is None:
             device = f"cuda:{torch.cuda.current_device()}" if torch.cuda.is_available() else "cpu"
@@ -94,6 +96,8 @@ class Runner:
         if self.is_gpu:
             native()  # fail loudly: no silent torch fallback on a GPU box
         self.tp_rank, self.tp_size, self.tp_group = tp_rank, tp_size, tp_group
+        # TP serving (parallel/tp.py): rank 0 signals each decode step, followers mirror it
+        self.tp_ctrl = tp_ctrl
         self.w = weights or DeviceWeights(model_path, self.device, tp_rank, tp_size)
         cfg = self.cfg = self.w.cfg
         loc = self.w.local
@@ -148,8 +152,8 @@ class Runner:
         self.s_out = torch.zeros(max_batch, **i32)
         self.kv = PagedKV(n_blocks, block_size, max_seqs, self.max_blocks)
         self.exe = NativeExec(self) if self.is_gpu else TorchExecutor(self)
-        if use_graphs is None:
-            use_graphs = self.is_gpu and os.environ.get("OMX_NO_GRAPH", "0") != "1"
+        if use_graphs is None:  # TP steps run Python-level collectives between executor stages
+            use_graphs = self.is_gpu and tp_size == 1 and os.environ.get("OMX_NO_GRAPH", "0") != "1"
         self.use_graphs = use_graphs
         self.graphs: dict[int, torch.cuda.CUDAGraph] = {}
         self._host_sampler: dict[int, tuple] = {}
@@ -173,7 +177,8 @@ class Runner:
     # ------------------------------------------------------------------ forward
     def _all_reduce_add(self, B: int):
         import torch.distributed as dist
-        dist.all_reduce(self.ypart[:B], group=self.tp_group)
+        with trace_range("tp all_reduce"):
+            dist.all_reduce(self.ypart[:B], group=self.tp_group)
         self.resid[:B] += self.ypart[:B]
 
     def forward(self, B: int, n_logits: int, use_idx: bool = False):
@@ -240,7 +245,8 @@ class Runner:
             arr = np.stack([pos, slots, pos + 1, np.full(B, s.row, np.int32),
                             np.full(B, B - 1, np.int32)]).astype(np.int32)
             self._upload(arr, np.asarray(chunk, np.int32))
-            self.forward(B, 1 if (last and want_logits) else 0, use_idx=True)
+            with trace_range(f"prefill B={B}"):
+                self.forward(B, 1 if (last and want_logits) else 0, use_idx=True)
         s.tokens.extend(tokens)
 
     def embed(self, tokens: list[int]) -> np.ndarray:
@@ -348,10 +354,11 @@ class Runner:
             self._sync_block_table(sid)
         arr = np.array([[pos], [self.kv.slot(sid, pos)], [pos + 1], [s.row], [0]], np.int32)
         self._upload(arr, None)
-        if self.use_graphs:
-            self._graph(1).replay()
-        else:
-            self._decode_body(1)
+        with trace_range("decode"):
+            if self.use_graphs:
+                self._graph(1).replay()
+            else:
+                self._decode_body(1)
 
     def generate(self, sid: int, prompt: list[int], options: SamplingOptions | None = None,
                  max_tokens: int = 128, stop: Callable[[int], bool] | None = None,
@@ -382,11 +389,18 @@ class Runner:
         n = 0
         tok = first
         max_tokens = min(max_tokens, self.ctx - st.length)
+        ctrl = self.tp_ctrl
+        follower = ctrl is not None and not ctrl.leader
         try:
             while True:
                 n += 1
-                done = n >= max_tokens or (stop is not None and stop(tok))
+                if follower:  # the leader decides (its server applies stop strings on text)
+                    done = not ctrl.wait()
+                else:
+                    done = n >= max_tokens or (stop is not None and stop(tok))
                 if not done:
+                    if ctrl is not None and ctrl.leader:
+                        ctrl.signal(True)
                     # enqueue the next step before handing this token out: the GPU runs one step
                     # ahead of the host (detokenize / stream / stop checks overlap the forward)
                     self.decode_step(sid)
@@ -404,6 +418,8 @@ class Runner:
                 else:
                     tok = int(self.s_out[0])
         finally:
+            if ctrl is not None and ctrl.leader:
+                ctrl.signal(False)  # generation over (also when the consumer closed us early)
             if times is not None:
                 times.gen_tokens = n
                 times.gen_s = time.perf_counter() - t1

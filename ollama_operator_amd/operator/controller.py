@@ -37,10 +37,12 @@ class WorkQueue:
     def add(self, key: str, delay: float = 0.0):
         with self.cv:
             t = time.monotonic() + delay
-            if key in self.processing:
+            if key in self.processing and delay == 0.0:
+                # an event during processing: reprocess right after done(); a delayed requeue
+                # (RequeueAfter) is a timer and must NOT mark the key dirty, or every "wait 5 s"
+                # turns into an immediate hot loop
                 self.dirty.add(key)
-                if delay == 0.0:
-                    return
+                return
             if key in self.due and self.due[key] <= t:
                 return
             self.due[key] = t

@@ -1,0 +1,213 @@
+"""Tensor-parallel serving: one pod, one process per GPU.
+
+`ollama serve` with `OMX_TP=N` (set by the operator from `spec.tensorParallelSize`,
+ollama_operator_amd/operator/resources.py) runs rank 0 inside the HTTP server process and spawns
+ranks 1..N-1 as worker processes -- BEFORE anything in the server touches the GPU (no process is
+forked or exec'ed from a GPU-initialised parent). All ranks then join:
+  * the compute group (RCCL = backend "nccl" on ROCm, over xGMI): the runner's all-reduce of the
+    row-parallel partial sums and the all-gather of vocab-sharded logits (engine/runner.py);
+  * a gloo control group: rank 0 broadcasts every runner call (load / new_sequence / generate /
+    embed / ...) to the workers, and one continue/stop flag per decode step.
+Sampling needs no token broadcast: every rank holds the all-gathered full logits and the same
+sampler state with the same resolved seed, so every rank samples the same token; only the stop
+decision (taken by the server on detokenised text) crosses the control group, which keeps the
+pipelined generate (engine/runner.py `generate`) in lockstep even when the client stops early.
+A failed rank kills the pod (no partial recovery inside a TP group).
+"""
+from __future__ import annotations
+
+import dataclasses
+import os
+import socket
+import subprocess
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ENV_TP = "OMX_TP"
+
+
+def tp_size_from_env() -> int:
+    return max(1, int(os.environ.get(ENV_TP, "1") or 1))
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+class TPControl:
+    """Leader -> follower command / step-flag channel over a gloo group."""
+
+    def __init__(self, group, leader: bool):
+        self.group = group
+        self.leader = leader
+        self._flag = torch.zeros(1, dtype=torch.int32)
+
+    def send_cmd(self, cmd: dict) -> None:
+        assert self.leader
+        dist.broadcast_object_list([cmd], src=0, group=self.group)
+
+    def recv_cmd(self) -> dict:
+        box = [None]
+        dist.broadcast_object_list(box, src=0, group=self.group)
+        return box[0]
+
+    def signal(self, go: bool) -> None:  # leader: one decode step will follow (1) / generation over (0)
+        self._flag[0] = 1 if go else 0
+        dist.broadcast(self._flag, src=0, group=self.group)
+
+    def wait(self) -> bool:  # follower
+        dist.broadcast(self._flag, src=0, group=self.group)
+        return bool(self._flag[0])
+
+
+@dataclasses.dataclass
+class TPWorld:
+    rank: int
+    size: int
+    device: str
+    compute_group: object
+    ctrl: TPControl
+    workers: list
+
+
+def _device_for(local_rank: int) -> str:
+    if torch.cuda.is_available():
+        return f"cuda:{local_rank % torch.cuda.device_count()}"
+    return "cpu"
+
+
+def _backend() -> str:
+    b = os.environ.get("OMX_TP_BACKEND")
+    if b:
+        return b
+    return "nccl" if torch.cuda.is_available() else "gloo"
+
+
+def _init_groups(rank: int, size: int, addr: str, port: int) -> tuple:
+    dev = _device_for(rank)
+    if dev.startswith("cuda"):
+        torch.cuda.set_device(torch.device(dev))
+    dist.init_process_group(_backend(), init_method=f"tcp://{addr}:{port}", rank=rank, world_size=size)
+    ctrl_group = dist.new_group(backend="gloo")
+    return dev, dist.group.WORLD, ctrl_group
+
+
+def start_leader(size: int) -> TPWorld:
+    """Server process (rank 0): spawn workers first (GPU untouched so far), then join the groups."""
+    addr, port = "127.0.0.1", _free_port()
+    workers = []
+    for r in range(1, size):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(size), MASTER_ADDR=addr,
+                   MASTER_PORT=str(port))
+        workers.append(subprocess.Popen([sys.executable, "-m", "ollama_operator_amd.parallel.tp_worker"], env=env))
+    dev, compute, ctrl = _init_groups(0, size, addr, port)
+    return TPWorld(0, size, dev, compute, TPControl(ctrl, leader=True), workers)
+
+
+def shutdown_leader(world: TPWorld) -> None:
+    try:
+        world.ctrl.send_cmd({"op": "exit"})
+    except Exception:  # noqa: BLE001 - workers may already be gone
+        pass
+    for p in world.workers:
+        try:
+            p.wait(timeout=30)
+        except subprocess.TimeoutExpired:
+            p.kill()
+
+
+class TPRunnerProxy:
+    """Rank-0 face of a tensor-parallel model: mirrors each call to the workers, then runs it on
+    the local rank-0 `Runner` (duck-types the Runner API the server uses)."""
+
+    def __init__(self, world: TPWorld, runner, load_cmd: dict):
+        self.world = world
+        self.r = runner
+        self.load_cmd = load_cmd
+
+    def __getattr__(self, name):  # read-only attributes (cfg, ctx, is_gpu, ...)
+        return getattr(self.r, name)
+
+    def _mirror(self, op: str, **kw):
+        self.world.ctrl.send_cmd({"op": op, **kw})
+
+    def new_sequence(self) -> int:
+        self._mirror("new_sequence")
+        return self.r.new_sequence()
+
+    def free_sequence(self, sid: int) -> None:
+        self._mirror("free_sequence", sid=sid)
+        self.r.free_sequence(sid)
+
+    def warmup(self) -> None:
+        self._mirror("warmup")
+        self.r.warmup()
+
+    def embed(self, tokens: list[int]):
+        self._mirror("embed", tokens=list(tokens))
+        return self.r.embed(tokens)
+
+    def generate(self, sid: int, prompt: list[int], options=None, max_tokens: int = 128, stop=None, times=None):
+        from ..engine.sampling import SamplingOptions
+        o = options or SamplingOptions()
+        o = dataclasses.replace(o, seed=o.resolved_seed())  # every rank must draw the same stream
+        self._mirror("generate", sid=sid, prompt=list(prompt), options=o, max_tokens=max_tokens)
+        return self.r.generate(sid, prompt, o, max_tokens=max_tokens, stop=stop, times=times)
+
+    def close(self) -> None:
+        self._mirror("unload")
+
+
+def load_tp_runner(world: TPWorld, path: str, max_batch: int, max_seqs: int, ctx: int):
+    from ..engine.runner import Runner
+    cmd = dict(path=path, max_batch=max_batch, max_seqs=max_seqs, ctx=ctx)
+    world.ctrl.send_cmd({"op": "load", **cmd})
+    r = Runner(path, device=world.device, max_batch=max_batch, max_seqs=max_seqs, ctx=ctx, tp_rank=0,
+               tp_size=world.size, tp_group=world.compute_group, tp_ctrl=world.ctrl)
+    return TPRunnerProxy(world, r, cmd)
+
+
+def worker_main() -> None:
+    rank, size = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    dev, compute, ctrl_group = _init_groups(rank, size, os.environ["MASTER_ADDR"], int(os.environ["MASTER_PORT"]))
+    ctrl = TPControl(ctrl_group, leader=False)
+    from ..engine.runner import Runner
+    runner = None
+    while True:
+        try:
+            cmd = ctrl.recv_cmd()
+        except RuntimeError as e:  # the leader (server process) is gone: the TP group is over
+            print(f"tp rank {rank}: control channel closed ({e.__class__.__name__}); exiting", flush=True)
+            os._exit(0)
+        op = cmd["op"]
+        if op == "exit":
+            break
+        if op == "load":
+            runner = Runner(cmd["path"], device=dev, max_batch=cmd["max_batch"], max_seqs=cmd["max_seqs"],
+                            ctx=cmd["ctx"], tp_rank=rank, tp_size=size, tp_group=compute, tp_ctrl=ctrl)
+        elif op == "unload":
+            runner = None
+            if dev.startswith("cuda"):
+                torch.cuda.empty_cache()
+        elif op == "warmup":
+            runner.warmup()
+        elif op == "new_sequence":
+            runner.new_sequence()
+        elif op == "free_sequence":
+            runner.free_sequence(cmd["sid"])
+        elif op == "embed":
+            runner.embed(cmd["tokens"])
+        elif op == "generate":
+            for _ in runner.generate(cmd["sid"], cmd["prompt"], cmd["options"], max_tokens=cmd["max_tokens"]):
+                pass
+        else:
+            raise RuntimeError(f"unknown TP command {op}")
+    dist.barrier(group=ctrl_group)
+    time.sleep(0.1)

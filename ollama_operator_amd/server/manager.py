@@ -72,10 +72,14 @@ class GenResult:
 
 
 class ModelManager:
-    def __init__(self, store: ModelStore, device: str | None = None, max_loaded: int | None = None):
+    def __init__(self, store: ModelStore, device: str | None = None, max_loaded: int | None = None,
+                 tp_world=None):
         self.store = store
         self.device = device
+        self.tp_world = tp_world  # parallel.tp.TPWorld when serving with OMX_TP > 1
         self.max_loaded = max_loaded or int(os.environ.get("OLLAMA_MAX_LOADED_MODELS", "3"))
+        if tp_world is not None:
+            self.max_loaded = 1  # the worker ranks hold one model
         self.loaded: dict[str, LoadedModel] = {}
         self.mu = threading.Lock()
         self.stats = {"requests": 0, "tokens_generated": 0, "prompt_tokens": 0}
@@ -90,6 +94,8 @@ class ModelManager:
     def _unload(self, key: str):
         lm = self.loaded.pop(key, None)
         if lm is not None:
+            if hasattr(lm.runner, "close"):  # TP: the worker ranks drop their shards too
+                lm.runner.close()
             del lm.runner
             try:
                 import torch
@@ -136,9 +142,14 @@ class ModelManager:
         tok = from_gguf_metadata(g.metadata)
         g.close()
         ctx_cap = int(os.environ.get("OMX_MAX_CTX", "0")) or None
+        ctx = min(num_ctx, ctx_cap) if ctx_cap else num_ctx
         # prefill chunk = MFMA GEMM M dimension (weights cross HBM once per chunk)
-        runner = Runner(path, device=self.device, max_batch=int(os.environ.get("OMX_PREFILL_CHUNK", "512")),
-                        max_seqs=2, ctx=min(num_ctx, ctx_cap) if ctx_cap else num_ctx)
+        chunk = int(os.environ.get("OMX_PREFILL_CHUNK", "512"))
+        if self.tp_world is not None:  # tensor parallel: every rank loads its shard (parallel/tp.py)
+            from ..parallel.tp import load_tp_runner
+            runner = load_tp_runner(self.tp_world, path, max_batch=chunk, max_seqs=2, ctx=ctx)
+        else:
+            runner = Runner(path, device=self.device, max_batch=chunk, max_seqs=2, ctx=ctx)
         runner.warmup()
         return LoadedModel(name=name, digest=m.digest, path=path, runner=runner, tokenizer=tok,
                            template=self.store.text_layer(m, MT_TEMPLATE), system=self.store.text_layer(m, MT_SYSTEM),

@@ -166,6 +166,26 @@ def test_workqueue_dedupe_delay_backoff():
     assert q.get(1.0) == "c"
 
 
+def test_workqueue_requeue_after_during_processing_is_a_timer():
+    """RequeueAfter issued while the key is being processed must wait its delay (regression: it
+    used to mark the key dirty, so done() re-queued it at once -- a hot reconcile loop that the
+    process-level apply->ready e2e exposed as thousands of Waiting* events)."""
+    q = WorkQueue()
+    q.add("m")
+    assert q.get(0.05) == "m"
+    q.add("m", delay=0.3)  # what process_one does with Result.requeue_after
+    q.done("m")
+    assert q.get(0.1) is None
+    assert q.get(0.5) == "m"
+    q.done("m")
+    # an event during processing still triggers an immediate re-run
+    q.add("m")
+    assert q.get(0.05) == "m"
+    q.add("m")
+    q.done("m")
+    assert q.get(0.05) == "m"
+
+
 def test_manager_event_driven():
     k = FakeKube()
     mgr = Manager(k, poll_s=600)
