@@ -286,6 +286,9 @@ PYBIND11_MODULE(_C, m) {
         w.x16 = Pp<void>(ptr("x16"));
         w.gws = Pp<float>(ptr("gws"));
         w.gws_elems = d.contains("gws_elems") ? d["gws_elems"].cast<long long>() : 0;
+        w.moe_rows = Pp<int>(ptr("moe_rows"));
+        w.moe_tiles = Pp<int>(ptr("moe_tiles"));
+        w.moe_ntiles = Pp<int>(ptr("moe_ntiles"));
         w.max_B = d["max_B"].cast<int>();
         w.n_splits = d["n_splits"].cast<int>();
       })

@@ -46,7 +46,9 @@ static_assert((size_t)GM_BM * GM_LDC * sizeof(float) <= GM_LDS, "epilogue tile m
 __global__ __launch_bounds__(256) void prep_x16_kernel(GemvParams P, f16* out) {
   __shared__ float red[4];
   const int b = blockIdx.x, K = P.w.K;
-  const float* x = P.x + (long long)b * P.ldx;
+  // MoE grouped GEMM: sorted row b reads the token of its (token, expert) pair
+  const int src = P.moe_gather ? P.moe_rows[b] / P.n_sel : b;
+  const float* x = P.x + (long long)src * P.ldx;
   float mean = 0.f, rstd = 1.f;
   if (P.norm != NORM_NONE) {
     float s = 0.f, ss = 0.f;
@@ -235,20 +237,30 @@ __device__ __forceinline__ void dequant_store(const WRaw<QT>& R, int ks, int pp,
   }
 }
 
-template <int QT>
+template <int QT, bool GROUPED = false>
 __global__ __launch_bounds__(GM_NT) void qgemm_kernel(GemvParams P, const f16* __restrict__ X) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   f16* Xs = (f16*)smem;             // [BM][LD]
   f16* Ws = Xs + GM_BM * GM_LD;     // [BN][LD]
   const QMat& w = P.w;
-  const int M = P.B, N = w.N, K = w.K, SB = n_sb(K);
+  int M = P.B;
+  const int N = w.N, K = w.K, SB = n_sb(K);
   const int nks = (K + GM_BK - 1) / GM_BK;  // K steps (last may be zero-padded: Q4_0 / Q8_0 only)
   const int sk = gridDim.z, z = blockIdx.z;  // split-K: this block's K-step range
   const int ks0 = (int)((long long)z * nks / sk), ks1 = (int)((long long)(z + 1) * nks / sk);
-  const int m0 = blockIdx.y * GM_BM, n0 = blockIdx.x * GM_BN;
+  int m0 = blockIdx.y * GM_BM;
+  long long row_base = 0;
+  if constexpr (GROUPED) {  // one expert-homogeneous tile of sorted rows per blockIdx.y
+    if ((int)blockIdx.y >= *P.moe_ntiles) return;  // block-uniform
+    const int* tt = P.moe_tiles + 3 * blockIdx.y;
+    row_base = (long long)tt[0] * N;
+    m0 = tt[1];
+    M = tt[1] + tt[2];  // rows of this tile: [m0, M)
+  }
+  const int n0 = blockIdx.x * GM_BN;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int srow = tid >> 1, spart = tid & 1;  // staging: row of the tile, which half of it
-  const long long wrow = min(n0 + srow, N - 1);
+  const long long wrow = row_base + min(n0 + srow, N - 1);
   const f16* xrow = X + (long long)min(m0 + srow, M - 1) * K;
 
   WRaw<QT> wr;
@@ -327,7 +339,14 @@ __global__ __launch_bounds__(GM_NT) void qgemm_kernel(GemvParams P, const f16* _
   for (int e = tid; e < GM_BM * GM_BN; e += GM_NT) {
     const int m = e / GM_BN, n = e % GM_BN;
     const int gm = m0 + m, gn = n0 + n;
-    if (gm < M && gn < N) epi_apply(P, gm, gn + P.row_offset, Cs[m * GM_LDC + n], Cs[m * GM_LDC + (n ^ 1)], 0);
+    if (gm >= M || gn >= N) continue;
+    int bb = gm, zsel = 0;
+    if (GROUPED && P.moe_scatter) {  // back to the token; routing weight + atomics in epi_apply
+      const int pair = P.moe_rows[gm];
+      bb = pair / P.n_sel;
+      zsel = pair % P.n_sel;
+    }
+    epi_apply(P, bb, gn + P.row_offset, Cs[m * GM_LDC + n], Cs[m * GM_LDC + (n ^ 1)], zsel);
   }
 }
 
@@ -371,6 +390,24 @@ static void launch_gemm(const GemvParams& P, const f16* x16, hipStream_t s) {
     const long long pairs = (long long)P.B * ((P.w.N + 1) / 2);
     const int blocks = (int)((pairs + 255) / 256 < 2048 ? (pairs + 255) / 256 : 2048);
     hipLaunchKernelGGL(gemm_finalize_kernel, dim3(blocks), dim3(256), 0, s, P, sk);
+  }
+}
+
+template <int QT>
+static void launch_moe(const GemvParams& P, const f16* x16, hipStream_t s) {
+  const int nt = (P.w.N + GM_BN - 1) / GM_BN;
+  hipLaunchKernelGGL((qgemm_kernel<QT, true>), dim3(nt, P.moe_max_tiles, 1), dim3(GM_NT), GM_LDS, s, P, x16);
+}
+
+void moe_gemm(const GemvParams& P, hipStream_t s) {
+  f16* x16 = (f16*)P.xws;
+  hipLaunchKernelGGL(prep_x16_kernel, dim3(P.B), dim3(256), 0, s, P, x16);
+  switch (P.w.qtype) {
+    case QT_Q4_K: launch_moe<QT_Q4_K>(P, x16, s); break;
+    case QT_Q6_K: launch_moe<QT_Q6_K>(P, x16, s); break;
+    case QT_Q4_0: launch_moe<QT_Q4_0>(P, x16, s); break;
+    case QT_Q8_0: launch_moe<QT_Q8_0>(P, x16, s); break;
+    default: break;
   }
 }
 

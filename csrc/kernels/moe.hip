@@ -44,3 +44,60 @@ void gather_rows(const float* x, int ld, const int* idx, int rows, int n, float*
 }
 
 }  // namespace omx
+
+namespace omx {
+
+// ---------------------------------------------------------------------------------------------
+// Prefill grouping for the MFMA grouped GEMM (gemm.hip GROUPED): sort the B*k (token, expert)
+// pairs by expert -- deterministic positions (pairs keep their original order inside an expert,
+// via wave ballots + a block scan, no atomics) -- and cut each expert's rows into tiles of <= 128
+// rows: tiles[t] = {expert, first sorted row, rows}. One block; B*k <= 1024 * MOE_SORT_PAIRS.
+constexpr int MOE_SORT_NT = 1024;
+
+__global__ __launch_bounds__(MOE_SORT_NT) void moe_sort_kernel(const int* eids, int n_pairs, int X, int* rows,
+                                                               int* tiles, int* n_tiles, int tile_m) {
+  __shared__ int wave_cnt[MOE_SORT_NT / 64];
+  __shared__ int base_s;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid == 0) base_s = 0;
+  int n_t = 0;  // thread 0: tiles emitted
+  __syncthreads();
+  for (int e = 0; e < X; ++e) {
+    const int base = base_s;
+    int run = 0;  // pairs of expert e in earlier chunks
+    for (int c0 = 0; c0 < n_pairs; c0 += MOE_SORT_NT) {
+      const int i = c0 + tid;
+      const bool mine = i < n_pairs && eids[i] == e;
+      const unsigned long long m = __ballot(mine);
+      const int before = __popcll(m & ((1ull << lane) - 1ull));
+      if (lane == 0) wave_cnt[wave] = __popcll(m);
+      __syncthreads();
+      int woff = 0, tot = 0;
+      for (int w = 0; w < MOE_SORT_NT / 64; ++w) {
+        if (w < wave) woff += wave_cnt[w];
+        tot += wave_cnt[w];
+      }
+      if (mine) rows[base + run + woff + before] = i;
+      run += tot;
+      __syncthreads();
+    }
+    if (tid == 0) {
+      for (int r0 = 0; r0 < run; r0 += tile_m) {
+        tiles[3 * n_t] = e;
+        tiles[3 * n_t + 1] = base + r0;
+        tiles[3 * n_t + 2] = min(tile_m, run - r0);
+        ++n_t;
+      }
+      base_s = base + run;
+    }
+    __syncthreads();
+  }
+  if (tid == 0) *n_tiles = n_t;
+}
+
+void moe_sort(const int* eids, int n_pairs, int X, int* rows, int* tiles, int* n_tiles, int tile_m, hipStream_t s) {
+  hipLaunchKernelGGL(moe_sort_kernel, dim3(1), dim3(MOE_SORT_NT), 0, s, eids, n_pairs, X, rows, tiles, n_tiles,
+                     tile_m);
+}
+
+}  // namespace omx

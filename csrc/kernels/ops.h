@@ -45,6 +45,15 @@ struct GemvParams {
   // split-K partial slabs for small-M GEMMs: fp32 [splits][B][N], capacity gws_elems (0 -> no split)
   float* gws;
   long long gws_elems;
+  // MoE prefill grouped GEMM (gemm.hip GROUPED): rows are the B*k (token, expert) pairs sorted by
+  // expert (moe_sort); x / y rows are in sorted order except that moe_scatter writes output row
+  // pair = moe_rows[pos] to token pair / n_sel with routing weight expert_w[pair]
+  const int* moe_rows;         // [B*k] sorted position -> pair index (token * k + j)
+  const int* moe_tiles;        // [max_tiles][3] {expert, first sorted row, rows}
+  const int* moe_ntiles;       // device count of valid tiles
+  int moe_max_tiles;
+  int moe_gather;              // x row of sorted position pos = moe_rows[pos] / n_sel (else pos)
+  int moe_scatter;             // output row of pos = token (EPI_ADD, weighted, atomic) (else pos)
 };
 
 // y = epi(W x): the quantised GEMV for small B (decode), the MFMA dequant GEMM for B >= GEMM_MIN_B
@@ -112,6 +121,10 @@ void argmax(const float* logits, int B, int V, int ld, int* out, hipStream_t s);
 
 void moe_route(const float* logits, int B, int X, int k, int* ids, float* w, hipStream_t s);
 void gather_rows(const float* x, int ld, const int* idx, int rows, int n, float* out, hipStream_t s);
+void moe_sort(const int* eids, int n_pairs, int X, int* rows, int* tiles, int* n_tiles, int tile_m, hipStream_t s);
+// grouped dequant GEMM over expert-homogeneous row tiles (P.moe_* set; P.B = number of pairs)
+void moe_gemm(const GemvParams& P, hipStream_t s);
+constexpr int MOE_TILE_M = 128;
 
 // small elementwise helpers
 void add_inplace(float* y, const float* x, long long n, hipStream_t s);

@@ -129,6 +129,40 @@ void Executor::ffn_block(int i, const StepInputs& in, hipStream_t s) {
     R.ldy = X;
     gemv(R, s);
     moe_route(ws.rlogits, B, X, k, ws.eids, ws.ew, s);
+    if (B >= GEMM_MIN_B && ws.x16 && ws.moe_rows) {
+      // prefill: grouped MFMA GEMM over expert-homogeneous tiles of the sorted (token, expert)
+      // pairs -- each expert's weights stream once per 128 routed rows, not once per pair
+      const int pairs = B * k;
+      moe_sort(ws.eids, pairs, X, ws.moe_rows, ws.moe_tiles, ws.moe_ntiles, MOE_TILE_M, s);
+      auto grouped = [&](GemvParams& P) {
+        P.n_sel = k;
+        P.moe_rows = ws.moe_rows;
+        P.moe_tiles = ws.moe_tiles;
+        P.moe_ntiles = ws.moe_ntiles;
+        P.moe_max_tiles = (pairs + MOE_TILE_M - 1) / MOE_TILE_M + X;
+      };
+      GemvParams G = base_params(L.gu_exps, pairs, ws.resid, E, ws);
+      G.norm = NORM_RMS;
+      G.norm_w = L.ffn_norm;
+      G.eps = cfg.eps;
+      G.epi = EPI_GLU;
+      G.y = ws.hbuf;  // [pair (sorted)][F]
+      G.ldy = F;
+      grouped(G);
+      G.moe_gather = 1;
+      moe_gemm(G, s);
+      if (cfg.tp > 1) hipMemsetAsync(ws.ypart, 0, sizeof(float) * (size_t)B * E, s);
+      GemvParams Dn = base_params(L.down_exps, pairs, ws.hbuf, F, ws);
+      Dn.epi = EPI_ADD;  // routing-weighted, atomically accumulated per token
+      Dn.y = dst;
+      Dn.ldy = E;
+      Dn.expert_ids = ws.eids;
+      Dn.expert_w = ws.ew;
+      grouped(Dn);
+      Dn.moe_scatter = 1;
+      moe_gemm(Dn, s);
+      return;
+    }
     GemvParams G = base_params(L.gu_exps, B, ws.resid, E, ws);
     G.norm = NORM_RMS;
     G.norm_w = L.ffn_norm;

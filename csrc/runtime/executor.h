@@ -56,6 +56,9 @@ struct Workspace {
   int* attn_cnt = nullptr;   // [maxB][Hkv] split arrival tickets (zero-initialised)
   void* x16 = nullptr;       // [maxB][max K] fp16 activations for the prefill MFMA GEMM
   float* gws = nullptr;      // split-K partial slabs for small-M prefill GEMMs
+  int* moe_rows = nullptr;   // [maxB*k] MoE prefill: pairs sorted by expert
+  int* moe_tiles = nullptr;  // [(maxB*k/128 + X + 1)*3] expert row tiles
+  int* moe_ntiles = nullptr; // [1]
   long long gws_elems = 0;
   int max_B = 0;
   int n_splits = 1;

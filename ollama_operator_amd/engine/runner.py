@@ -58,6 +58,8 @@ class NativeExec:
         e.set_workspace(dict(resid=p(r.resid), qbuf=p(r.qbuf), abuf=p(r.abuf), hbuf=p(r.hbuf), ypart=p(r.ypart),
                              lbuf=p(r.lbuf), rlogits=p(r.rlogits), eids=p(r.eids), ew=p(r.ew),
                              attn_ws=p(r.attn_ws), attn_cnt=p(r.attn_cnt), x16=p(r.x16), gws=p(r.gws),
+                             moe_rows=p(r.moe_rows) if cfg.n_expert else 0, moe_tiles=p(r.moe_tiles),
+                             moe_ntiles=p(r.moe_ntiles),
                              gws_elems=r.gws.numel(), max_B=r.max_batch,
                              n_splits=1))
         self.inputs = dict(tokens=p(r.d_tokens), pos=p(r.d_pos), slot=p(r.d_slot), q_len=p(r.d_qlen),
@@ -124,7 +126,12 @@ class Runner:
         self.eids = torch.zeros(max_batch, ksel, **i32)
         self.ew = torch.zeros(max_batch, ksel, **f32)
         # fp16 activations for the prefill MFMA GEMM (any GEMM input: E, H*D, F, k*F wide)
-        self.x16 = torch.zeros(max_batch * max(E, Eq, ksel * Fl), device=dev, dtype=torch.float16)
+        self.x16 = torch.zeros(max_batch * max(E, Eq, ksel * Fl, ksel * E), device=dev, dtype=torch.float16)
+        # MoE prefill grouping (csrc/kernels/moe.hip moe_sort -> grouped MFMA GEMM)
+        n_pairs = max_batch * ksel
+        self.moe_rows = torch.zeros(n_pairs, **i32)
+        self.moe_tiles = torch.zeros(3 * (n_pairs // 128 + max(1, cfg.n_expert) + 1), **i32)
+        self.moe_ntiles = torch.zeros(1, **i32)
         # split-K partial slabs of small-M prefill GEMMs (the kernel picks splits that fit)
         self.gws = torch.zeros(GEMM_SPLIT_WS_FLOATS if str(dev).startswith("cuda") else 1, **f32)
         ws = max(self._ws_floats(B) for B in range(1, max_batch + 1))
