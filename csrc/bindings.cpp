@@ -145,7 +145,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("attention", [](uintptr_t q, int ldq, uintptr_t kc, uintptr_t vc, uintptr_t block_table, int max_blocks,
                         uintptr_t q_seq, uintptr_t q_len, int NQ, int H, int n_kv, int D, int bs, float scale,
                         int window, uintptr_t out, int ldo, uintptr_t ws, int n_splits, uintptr_t counters,
-                        uintptr_t stream) {
+                        uintptr_t stream, int prefill) {
     if (n_splits < 1 || n_splits > 64) throw std::runtime_error("n_splits must be in [1, 64]");
     if (n_splits > 1 && (!ws || !counters)) throw std::runtime_error("split attention needs ws and counters");
     check_attn(H, n_kv, D);
@@ -170,8 +170,12 @@ PYBIND11_MODULE(_C, m) {
     A.ws = Pp<float>(ws);
     A.n_splits = n_splits;
     A.counters = Pp<int>(counters);
+    A.prefill = prefill;
     attention_decode(A, S(stream));
-  });
+  }, py::arg("q"), py::arg("ldq"), py::arg("kc"), py::arg("vc"), py::arg("block_table"), py::arg("max_blocks"),
+     py::arg("q_seq"), py::arg("q_len"), py::arg("NQ"), py::arg("H"), py::arg("n_kv"), py::arg("D"), py::arg("bs"),
+     py::arg("scale"), py::arg("window"), py::arg("out"), py::arg("ldo"), py::arg("ws"), py::arg("n_splits"),
+     py::arg("counters"), py::arg("stream"), py::arg("prefill") = 0);
   m.def("attention_ws_floats", &attention_ws_floats);
   m.def("set_gemv_tuning", &set_gemv_tuning, py::arg("blocks_per_cu") = 0, py::arg("rows") = 0,
         py::arg("debug") = 0);
@@ -305,6 +309,7 @@ PYBIND11_MODULE(_C, m) {
         in.block_table = Pp<const int>(ptr("block_table"));
         in.max_blocks = d["max_blocks"].cast<int>();
         in.bs = d["bs"].cast<int>();
+        in.prefill = d.contains("prefill") ? d["prefill"].cast<int>() : 0;
         in.n_logits = d.contains("n_logits") ? d["n_logits"].cast<int>() : 0;
         in.logit_idx = Pp<const int>(ptr("logit_idx"));
         in.logits = Pp<float>(ptr("logits"));

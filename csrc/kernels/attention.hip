@@ -286,6 +286,179 @@ __global__ __launch_bounds__(ATT_NT) void attn_decode_kernel(AttnParams P) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Causal prefill attention on the matrix cores: one sequence, NQ >= 16
+// contiguous query positions (a prefill chunk), K/V already in the paged cache (the QKV epilogue
+// wrote them). Block = 4 waves x 32 queries of one head; key tiles of 32 staged in LDS and shared
+// by the waves. Per tile and wave:
+//   S^T = K . Q^T   (v_mfma_f32_32x32x16_f16; keys on the accumulator rows, one query per lane, so
+//                    the online softmax is lane-local + one exchange with lane ^ 32)
+//   O^T += V^T . P^T (P^T used straight from the accumulator registers as the B operand in the
+//                    permuted k order of cdna_hip_programming.md §3; V^T fragments come from
+//                    ds_read_b64_tr_b16 hardware-transposed reads of the row-major V tile, stored
+//                    with the XOR swizzle of §5.5 T10 (b) so both the row writes and the transposed
+//                    reads are bank-conflict-free)
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16a __attribute__((ext_vector_type(16)));
+constexpr int PF_BQ = 128, PF_BK = 32;
+
+__device__ __forceinline__ int vswz(int row, int ch) {  // T10 (b): byte offset of 16-B chunk ch
+  return 256 * row + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void attn_prefill_kernel(AttnParams P) {
+  constexpr int NKS = D / 16;             // k-steps of S^T over the head dim
+  constexpr int NDT = (D + 31) / 32;      // 32-row d tiles of O^T
+  constexpr int LDK = D + 8;              // K tile row stride (f16): 16-B rows offset by 4 banks
+  constexpr int KCH = D / 8;              // 16-B chunks per K/V row
+  __shared__ __attribute__((aligned(16))) f16 Ks[PF_BK * LDK];
+  __shared__ __attribute__((aligned(16))) char Vs[PF_BK * 256];  // [key][256 B] swizzled, zero-padded
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h2 = lane >> 5, qc = lane & 31;
+  const int head = blockIdx.y, G = P.H / P.n_kv, kvh = head / G;
+  const int q0 = blockIdx.x * PF_BQ;
+  const int NQ = P.NQ;
+  const int qi = min(q0 + wave * 32 + qc, NQ - 1);  // this lane's query (clamped; stores masked)
+  const int len_q = P.q_len[qi];                    // visible keys = pos + 1
+  const int kstart_q = P.window > 0 ? max(0, len_q - P.window) : 0;
+  const int seq = P.q_seq ? P.q_seq[0] : 0;
+  const int* bt = P.block_table + (long long)seq * P.max_blocks;
+  const f16* kc = (const f16*)P.kc;
+  const f16* vc = (const f16*)P.vc;
+  const int bs = P.bs;
+  // key range of the block: contiguous positions -> first query has the smallest window start,
+  // the last query the largest length
+  const int q_last = min(q0 + PF_BQ, NQ) - 1;
+  const int len_max = P.q_len[q_last];
+  const int k_lo = P.window > 0 ? max(0, P.q_len[q0] - P.window) / PF_BK * PF_BK : 0;
+
+  // Q^T fragments (B operand of S^T): lane = query, 8 consecutive d per k-step, scaled
+  f16x8 qf[NKS];
+  {
+    const float* qp = P.q + (long long)qi * P.ldq + head * D;
+#pragma unroll
+    for (int kk = 0; kk < NKS; ++kk) {
+      const f32x4 a = *(const f32x4*)(qp + 16 * kk + 8 * h2), b = *(const f32x4*)(qp + 16 * kk + 8 * h2 + 4);
+      qf[kk] = (f16x8){(f16)(a.x * P.scale), (f16)(a.y * P.scale), (f16)(a.z * P.scale), (f16)(a.w * P.scale),
+                       (f16)(b.x * P.scale), (f16)(b.y * P.scale), (f16)(b.z * P.scale), (f16)(b.w * P.scale)};
+    }
+  }
+  f32x16a o[NDT];
+#pragma unroll
+  for (int i = 0; i < NDT; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[i][r] = 0.f;
+  float m = -INFINITY, l = 0.f;
+
+  // zero the V padding columns once (d in [D, 128)): they feed the last O^T tile when D % 32 != 0
+  if (D < 128) {
+    for (int i = tid; i < PF_BK * 16; i += 256) {
+      const int row = i >> 4, ch = i & 15;
+      if (ch >= KCH) *(u32x4*)(Vs + vswz(row, ch)) = (u32x4){0u, 0u, 0u, 0u};
+    }
+  }
+  // staging: each thread moves chunks of the K and V tiles (global paged cache -> registers -> LDS)
+  constexpr int NCH = (PF_BK * KCH + 255) / 256;
+  u32x4 kr[NCH], vr[NCH];
+  auto issue = [&](int kt0) {
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int i = tid + 256 * c;
+      const int row = min(i / KCH, PF_BK - 1), ch = i % KCH;
+      const int t = min(kt0 + row, len_max - 1);
+      const long long base = (((long long)bt[t / bs] * P.n_kv + kvh) * bs + (t % bs)) * D + 8 * ch;
+      kr[c] = *(const u32x4*)(kc + base);
+      vr[c] = *(const u32x4*)(vc + base);
+    }
+  };
+  issue(k_lo);
+  for (int kt0 = k_lo; kt0 < len_max; kt0 += PF_BK) {
+    __syncthreads();  // previous tile's LDS reads done
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int i = tid + 256 * c;
+      if (i < PF_BK * KCH) {
+        const int row = i / KCH, ch = i % KCH;
+        *(u32x4*)(Ks + row * LDK + 8 * ch) = kr[c];
+        *(u32x4*)(Vs + vswz(row, ch)) = vr[c];
+      }
+    }
+    __syncthreads();
+    if (kt0 + PF_BK < len_max) issue(kt0 + PF_BK);  // next tile in flight during the MFMAs
+    // S^T = K . Q^T : rows = keys kt0 + (r&3) + 8(r>>2) + 4*h2, column = this lane's query
+    f32x16a sacc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sacc[r] = 0.f;
+#pragma unroll
+    for (int kk = 0; kk < NKS; ++kk) {
+      const f16x8 kf = *(const f16x8*)(Ks + qc * LDK + 16 * kk + 8 * h2);
+      sacc = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf, qf[kk], sacc, 0, 0, 0);
+    }
+    // causal / window / length mask + online softmax (per lane = per query; halves exchange)
+    float tmax = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int t = kt0 + (r & 3) + 8 * (r >> 2) + 4 * h2;
+      const bool ok = t < len_q && t >= kstart_q;
+      sacc[r] = ok ? sacc[r] : -INFINITY;
+      tmax = fmaxf(tmax, sacc[r]);
+    }
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+    const float mn = fmaxf(m, tmax);
+    const float corr = mn == -INFINITY ? 1.f : __expf(m - mn);
+    float ps = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      sacc[r] = mn == -INFINITY ? 0.f : __expf(sacc[r] - mn);
+      ps += sacc[r];
+    }
+    ps += __shfl_xor(ps, 32, 64);
+    l = l * corr + ps;
+    m = mn;
+#pragma unroll
+    for (int i = 0; i < NDT; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) o[i][r] *= corr;
+    // O^T += V^T . P^T : two k-steps of 16 keys; P^T fragment s = registers 8s..8s+7
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      f16x8 pf;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) pf[j] = (f16)sacc[8 * s2 + j];
+      const int g = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
+#pragma unroll
+      for (int i = 0; i < NDT; ++i) {
+        const int c0 = (32 * i + 16 * (g & 1)) / 8;  // first 16-B chunk of this group's 16 d columns
+        const int r0 = 16 * s2 + 4 * h2;             // element j < 4: keys r0 + 0..3; j >= 4: + 8
+        const int a0 = vswz(r0 + qq, c0 + (pp >> 1)) + 8 * (pp & 1);
+        const int a1 = vswz(r0 + 8 + qq, c0 + (pp >> 1)) + 8 * (pp & 1);
+        typedef __attribute__((address_space(3))) s16x4 lds_s4;
+        // whole-vector bit casts: element-wise extraction from the v4i16 result miscompiled
+        // (duplicated pairs), caught by scripts/dbg_prefill_attn.py + scripts/probes/tr16_probe.hip
+        const f16x4 lo = __builtin_bit_cast(f16x4, __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(Vs + a0)));
+        const f16x4 hi = __builtin_bit_cast(f16x4, __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(Vs + a1)));
+        const f16x8 vf = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        o[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf, pf, o[i], 0, 0, 0);
+      }
+    }
+  }
+  // O = O^T / l : lane = query, rows = d (r&3) + 8(r>>2) + 4*h2 of d tile i
+  const int qo = q0 + wave * 32 + qc;
+  if (qo < NQ) {
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    float* out = P.out + (long long)qo * P.ldo + head * D;
+#pragma unroll
+    for (int i = 0; i < NDT; ++i)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int d = 32 * i + 8 * k + 4 * h2;
+        if (d < D)
+          *(f32x4*)(out + d) = (f32x4){o[i][4 * k] * inv, o[i][4 * k + 1] * inv, o[i][4 * k + 2] * inv,
+                                       o[i][4 * k + 3] * inv};
+      }
+  }
+}
+
 template <int D>
 static void launch_d(const AttnParams& P, hipStream_t s) {
   const int G = P.H / P.n_kv;
@@ -301,6 +474,16 @@ static void launch_d(const AttnParams& P, hipStream_t s) {
 
 void attention_decode(const AttnParams& P, hipStream_t s) {
   if (P.NQ <= 0) return;
+  if (P.prefill && P.NQ >= 16 && P.D % 16 == 0) {  // one sequence, contiguous positions: MFMA flash
+    dim3 grid((P.NQ + PF_BQ - 1) / PF_BQ, P.H);
+    switch (P.D) {
+      case 64: hipLaunchKernelGGL(attn_prefill_kernel<64>, grid, dim3(256), 0, s, P); return;
+      case 80: hipLaunchKernelGGL(attn_prefill_kernel<80>, grid, dim3(256), 0, s, P); return;
+      case 96: hipLaunchKernelGGL(attn_prefill_kernel<96>, grid, dim3(256), 0, s, P); return;
+      case 128: hipLaunchKernelGGL(attn_prefill_kernel<128>, grid, dim3(256), 0, s, P); return;
+      default: break;
+    }
+  }
   switch (P.D) {
     case 64: launch_d<64>(P, s); break;
     case 80: launch_d<80>(P, s); break;

@@ -93,6 +93,7 @@ struct AttnParams {
   float* ws;                   // split workspace: [NQ][H][S][D + 2] fp32
   int n_splits;                // <= 64
   int* counters;               // [NQ][n_kv] arrival tickets, zero before first use (self re-arming)
+  int prefill;                 // all NQ queries: one sequence, contiguous positions (MFMA flash path)
 };
 void attention_decode(const AttnParams& P, hipStream_t s);
 size_t attention_ws_floats(int NQ, int H, int D, int n_splits);

@@ -89,6 +89,7 @@ void Executor::attn_block(int i, const StepInputs& in, hipStream_t s) {
   A.ws = ws.attn_ws;
   A.n_splits = ws.n_splits;
   A.counters = ws.attn_cnt;
+  A.prefill = in.prefill;
   attention_decode(A, s);
   // --- output projection (+ residual, or partial sum under TP)
   GemvParams O = base_params(L.wo, B, ws.abuf, Eq, ws);

@@ -74,6 +74,7 @@ struct StepInputs {
   const int* block_table = nullptr;
   int max_blocks = 0;
   int bs = 16;
+  int prefill = 0;                // one sequence, contiguous positions (MFMA flash attention)
   int n_logits = 0;               // rows that need logits
   const int* logit_idx = nullptr; // [n_logits] (null = first n_logits rows)
   float* logits = nullptr;        // [n_logits][V]

@@ -67,9 +67,11 @@ class NativeExec:
                            bs=r.block_size, logits=p(r.logits))
         self.logit_idx_ptr = p(r.d_logit_idx)
 
-    def run(self, stage: str, layer: int, B: int, n_logits: int = 0, use_idx: bool = False):
+    def run(self, stage: str, layer: int, B: int, n_logits: int = 0, use_idx: bool = False,
+            prefill: bool = False):
         d = dict(self.inputs)
         d["B"] = B
+        d["prefill"] = int(prefill)
         d["n_logits"] = n_logits
         d["logit_idx"] = self.logit_idx_ptr if use_idx else 0
         self.exe.set_splits(self.r.n_splits(B))
@@ -188,14 +190,15 @@ class Runner:
             dist.all_reduce(self.ypart[:B], group=self.tp_group)
         self.resid[:B] += self.ypart[:B]
 
-    def forward(self, B: int, n_logits: int, use_idx: bool = False):
+    def forward(self, B: int, n_logits: int, use_idx: bool = False, prefill: bool = False):
+        """prefill=True: the B rows are one sequence's contiguous positions (MFMA flash attention)."""
         if self.tp_size == 1:
-            self.exe.run("forward", 0, B, n_logits, use_idx)
+            self.exe.run("forward", 0, B, n_logits, use_idx, prefill)
             return
         import torch.distributed as dist
         self.exe.run("embed", 0, B)
         for i in range(self.cfg.n_layer):
-            self.exe.run("attn", i, B)
+            self.exe.run("attn", i, B, prefill=prefill)
             self._all_reduce_add(B)
             self.exe.run("ffn", i, B)
             self._all_reduce_add(B)
@@ -253,7 +256,7 @@ class Runner:
                             np.full(B, B - 1, np.int32)]).astype(np.int32)
             self._upload(arr, np.asarray(chunk, np.int32))
             with trace_range(f"prefill B={B}"):
-                self.forward(B, 1 if (last and want_logits) else 0, use_idx=True)
+                self.forward(B, 1 if (last and want_logits) else 0, use_idx=True, prefill=True)
         s.tokens.extend(tokens)
 
     def embed(self, tokens: list[int]) -> np.ndarray:

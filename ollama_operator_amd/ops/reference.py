@@ -169,7 +169,8 @@ class TorchExecutor:
             lg = lg + w.lm_bias
         r.logits[:n_logits, :lg.shape[1]] = lg
 
-    def run(self, stage: str, layer: int, B: int, n_logits: int = 0, use_idx: bool = False):
+    def run(self, stage: str, layer: int, B: int, n_logits: int = 0, use_idx: bool = False,
+            prefill: bool = False):
         if stage == "embed":
             self.embed(B)
         elif stage == "attn":

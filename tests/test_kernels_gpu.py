@@ -171,6 +171,43 @@ def test_attention_paged(D, G, splits):
         assert rel(out[i], ref) < 2e-3
 
 
+@pytest.mark.parametrize("D", [64, 80, 128])
+@pytest.mark.parametrize("G", [1, 4])
+@pytest.mark.parametrize("start,NQ,window", [(0, 16, 0), (37, 100, 0), (0, 300, 0), (5, 130, 64)])
+def test_attention_prefill_mfma(D, G, start, NQ, window):
+    """MFMA flash prefill (attn_prefill_kernel): one sequence, queries at contiguous positions
+    start..start+NQ-1 (a prompt chunk after `start` cached tokens), causal (+ sliding window)."""
+    Hkv, bs = 2, 16
+    H = Hkv * G
+    total = start + NQ
+    max_blocks = (total + bs - 1) // bs
+    nblk = max_blocks + 8
+    torch.manual_seed(1)
+    kc = torch.randn(nblk, Hkv, bs, D, device="cuda").half()
+    vc = torch.randn(nblk, Hkv, bs, D, device="cuda").half()
+    bt = torch.randperm(nblk, device="cuda")[:max_blocks].view(1, max_blocks).int()
+    q = torch.randn(NQ, H * D, device="cuda")
+    qlen = torch.arange(start + 1, start + NQ + 1, device="cuda", dtype=torch.int32)
+    qseq = torch.zeros(NQ, device="cuda", dtype=torch.int32)
+    out = torch.zeros(NQ, H * D, device="cuda")
+    scale = 1 / math.sqrt(D)
+    C().attention(q.data_ptr(), H * D, kc.data_ptr(), vc.data_ptr(), bt.data_ptr(), max_blocks, qseq.data_ptr(),
+                  qlen.data_ptr(), NQ, H, Hkv, D, bs, scale, window, out.data_ptr(), H * D, 0, 1, 0, S(),
+                  prefill=1)
+    torch.cuda.synchronize()
+    t = torch.arange(total, device="cuda")
+    kk = kc[bt[0][t // bs].long(), :, t % bs].float().repeat_interleave(G, 1)  # [T][H][D]
+    vv = vc[bt[0][t // bs].long(), :, t % bs].float().repeat_interleave(G, 1)
+    s = torch.einsum("qhd,thd->hqt", q.view(NQ, H, D), kk) * scale
+    pos = torch.arange(start, start + NQ, device="cuda")[:, None]
+    mask = t[None, :] <= pos
+    if window:
+        mask &= t[None, :] >= (pos + 1 - window)
+    s = s.masked_fill(~mask[None], float("-inf"))
+    ref = torch.einsum("hqt,thd->qhd", torch.softmax(s, -1), vv).reshape(NQ, -1)
+    assert rel(out, ref) < 3e-3
+
+
 @pytest.mark.parametrize("qt", QTYPES)
 def test_embed_and_dequant_f16(qt):
     V, E = 64, 512
