@@ -178,7 +178,7 @@ PYBIND11_MODULE(_C, m) {
      py::arg("counters"), py::arg("stream"), py::arg("prefill") = 0);
   m.def("attention_ws_floats", &attention_ws_floats);
   m.def("set_gemv_tuning", &set_gemv_tuning, py::arg("blocks_per_cu") = 0, py::arg("rows") = 0,
-        py::arg("debug") = 0);
+        py::arg("debug") = 0, py::arg("ks") = -1);
   m.def("embed_rows", [](py::object w, uintptr_t rows, int n, uintptr_t out, int ldo, uintptr_t stream) {
     embed_rows(qmat(w), Pp<const int>(rows), n, Pp<float>(out), ldo, S(stream));
   });

@@ -40,8 +40,9 @@ constexpr int GEMV_NT = 64 * GEMV_NW;
 constexpr int XPAD = 17;      // LDS x slots per super-block: 16 groups + 1 pad
 
 GemvTuning g_tune;
-void set_gemv_tuning(int blocks_per_cu, int rows, int debug) {
+void set_gemv_tuning(int blocks_per_cu, int rows, int debug, int ks) {
   g_tune.debug = debug > 0 ? debug : 0;
+  if (ks >= 0 && ks <= 4) g_tune.ks = ks;
   if (blocks_per_cu > 0) g_tune.blocks_per_cu = blocks_per_cu;
   if (rows == 1 || rows == 2) g_tune.rows = rows;
 }
@@ -84,35 +85,57 @@ struct WTile {
   unsigned d[Q6 ? R : 1][Q6 ? NSB : 1];                // Q6_K super-block scale (fp16)
 };
 
+// the machine scheduler otherwise permutes independent loads; vmcnt retires in issue order, so a
+// permutation makes the first consumer wait for (nearly) the whole tile
+#define OMX_LOAD_ORDER() __builtin_amdgcn_sched_barrier(0)
+// pieces are consumed in load order: VALU may not cross (hoisting a later piece's unpack would put
+// its vmcnt wait first); LDS reads (activation fragments) and SALU may
+#define OMX_PIECE_ORDER() __builtin_amdgcn_sched_barrier(0x0104)
+
 template <int QT, int NSB, int R>
 __device__ __forceinline__ void load_wtile(const QMat& w, long long row_base, int row0, int N, int SB, int sb0,
-                                           int s, WTile<QT, NSB, R>& T) {
+                                           int s, WTile<QT, NSB, R>& T, int se = -1) {
+  if (se < 0) se = SB;  // lanes own super-blocks [sb0, se): an in-block K split ends a group's range early
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     const long long row = row_base + min(row0 + r, N - 1);
 #pragma unroll
     for (int i = 0; i < NSB; ++i) {
-      const long long sb = min(sb0 + s + 16 * i, SB - 1);  // clamped: padding lanes re-read, never use
+      const long long sb = min(sb0 + s + 16 * i, se - 1);  // clamped: padding lanes re-read, never use
+      // issue order = consumption order: vmcnt retires loads in order, so the super-block scales go
+      // first and each piece's operands together; otherwise the first dot product waits for the
+      // wave's last load and no compute overlaps the stream
       if constexpr (QT == QT_Q8_0) {
         const uint8_t* q = w.s0 + row * SB * 256 + 32 * sb;
+        T.m[r][i] = *(const u32x4*)(w.s1 + row * SB * 16 + 16 * sb);
+        OMX_LOAD_ORDER();
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
           T.a[r][i][t] = __builtin_nontemporal_load((const u32x4*)(q + 32LL * t * SB));
           T.b[r][i][t] = __builtin_nontemporal_load((const u32x4*)(q + 32LL * t * SB + 16));
+          OMX_LOAD_ORDER();
         }
-        T.m[r][i] = *(const u32x4*)(w.s1 + row * SB * 16 + 16 * sb);
+      } else if constexpr (QT == QT_Q6_K) {
+        const uint8_t* q = w.s0 + row * SB * 128 + 16 * sb;
+        const uint8_t* hq = w.s1 + row * SB * 64 + 8 * sb;
+        T.m[r][i] = *(const u32x4*)(w.s2 + row * SB * 16 + 16 * sb);
+        OMX_LOAD_ORDER();
+        T.d[r][i] = *(const uint16_t*)(w.s3 + row * SB * 2 + 2 * sb);
+        OMX_LOAD_ORDER();
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          T.a[r][i][t] = __builtin_nontemporal_load((const u32x4*)(q + 16LL * t * SB));
+          T.h[r][i][t] = __builtin_nontemporal_load((const u32x2*)(hq + 8LL * t * SB));
+          OMX_LOAD_ORDER();
+        }
       } else {
         const uint8_t* q = w.s0 + row * SB * 128 + 16 * sb;
+        T.m[r][i] = *(const u32x4*)(w.s1 + row * SB * 16 + 16 * sb);
+        OMX_LOAD_ORDER();
 #pragma unroll
-        for (int t = 0; t < 8; ++t) T.a[r][i][t] = __builtin_nontemporal_load((const u32x4*)(q + 16LL * t * SB));
-        if constexpr (QT == QT_Q6_K) {
-          const uint8_t* hq = w.s1 + row * SB * 64 + 8 * sb;
-#pragma unroll
-          for (int t = 0; t < 8; ++t) T.h[r][i][t] = __builtin_nontemporal_load((const u32x2*)(hq + 8LL * t * SB));
-          T.m[r][i] = *(const u32x4*)(w.s2 + row * SB * 16 + 16 * sb);
-          T.d[r][i] = *(const uint16_t*)(w.s3 + row * SB * 2 + 2 * sb);
-        } else {
-          T.m[r][i] = *(const u32x4*)(w.s1 + row * SB * 16 + 16 * sb);
+        for (int t = 0; t < 8; ++t) {
+          T.a[r][i][t] = __builtin_nontemporal_load((const u32x4*)(q + 16LL * t * SB));
+          OMX_LOAD_ORDER();
         }
       }
     }
@@ -140,11 +163,12 @@ __device__ __forceinline__ void load_x(const i32x4* xq, const f32x2* xf, int XS,
 
 template <int QT, int NSB, int R, int BT>
 __device__ __forceinline__ void compute_wtile(const WTile<QT, NSB, R>& T, int SB, int sb0, int s, const i32x4* xq,
-                                              const f32x2* xf, int XS, float (&acc)[R][BT]) {
+                                              const f32x2* xf, int XS, float (&acc)[R][BT], int se = -1) {
+  if (se < 0) se = SB;
 #pragma unroll
   for (int i = 0; i < NSB; ++i) {
     const int sb = sb0 + s + 16 * i;
-    if (sb >= SB) continue;
+    if (sb >= se) continue;
     const int xs0 = sb * XPAD;
     if constexpr (QT == QT_Q4_K) {
       // w = d*sc*n - dmin*m per 32-weight sub-block; lo nibbles: sub-block 2c, hi: 2c+1 (signed n-8)
@@ -189,6 +213,7 @@ __device__ __forceinline__ void compute_wtile(const WTile<QT, NSB, R>& T, int SB
                            gh[r] * x.fh[b].y;
             }
           }
+          OMX_PIECE_ORDER();
         }
       }
     } else if constexpr (QT == QT_Q6_K) {
@@ -222,6 +247,7 @@ __device__ __forceinline__ void compute_wtile(const WTile<QT, NSB, R>& T, int SB
             acc[r][b] += fl * (x.fl[b].x * il - 32.f * x.fl[b].y) + fh * (x.fh[b].x * ih - 32.f * x.fh[b].y);
           }
         }
+        OMX_PIECE_ORDER();
       }
     } else {
       // Q4_0: w = d*(n - 8), lo nibble unsigned, hi nibble signed; Q8_0: w = d*q
@@ -246,6 +272,7 @@ __device__ __forceinline__ void compute_wtile(const WTile<QT, NSB, R>& T, int SB
             }
           }
         }
+        OMX_PIECE_ORDER();
       }
     }
   }
@@ -456,19 +483,28 @@ __global__ __launch_bounds__(GEMV_NT) void qgemv_kernel(GemvParams P) {
 // norm weights) into registers, THEN issues the loads of all J weight tiles of its block, computes
 // the norm + int8 quantisation from registers while the weights stream, and consumes the tiles in
 // order with counted vmcnt waits (fully unrolled), so HBM sees the whole matrix requested up front.
-template <int QT, int NSB, int R, int J>
-__global__ __launch_bounds__(GEMV_NT) void qgemv_flight_kernel(GemvParams P) {
-  constexpr int ROWS_B = GEMV_NW * 4 * R;
+// NRM: 0 = no norm (only x is loaded), 1 = RMSNorm (x, w), 2 = LayerNorm (x, w, b). Stand-in loads
+// for absent norm operands would spend the wave's 63-deep vmcnt budget (NSB = 3: 69 loads per lane).
+// KS > 1 (matrices with few row tiles, e.g. the K = 11008 down projection: 256 tiles = one 4-wave
+// block per CU): the block has KS groups of GEMV_NW waves on the same rows, group kg owning the
+// super-block range [kg*CH, (kg+1)*CH); partial sums meet in LDS before the epilogue. More waves per
+// CU = more weight bytes in flight.
+template <int QT, int NSB, int R, int J, int NRM, int DBG = 0, int KS = 1>
+__global__ __launch_bounds__(GEMV_NT * KS) void qgemv_flight_kernel(GemvParams P) {
+  constexpr int ROWS_B = GEMV_NW * 4 * R, NT = GEMV_NT * KS;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const QMat& w = P.w;
   const int K = w.K, N = w.N, SB = n_sb(K);
   const int XS = SB * XPAD;
-  i32x4* lq = (i32x4*)smem;
-  f32x2* lf = (f32x2*)(smem + (size_t)XS * 16);
-  float* red = (float*)(lf + XS);
+  i32x4* lq = (i32x4*)smem;                           // [XS + 1]: slot XS is a dummy
+  f32x2* lf = (f32x2*)(smem + (size_t)(XS + 1) * 16);  // [XS + 1]
+  float* red = (float*)(lf + XS + 1);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = lane >> 4, s = lane & 15;
+  const int kg = KS > 1 ? wave / GEMV_NW : 0, gtid = tid - kg * GEMV_NT;
+  const int CH = KS > 1 ? (SB + KS - 1) / KS : SB;
+  const int sb0 = kg * CH, se = min(SB, sb0 + CH);
   const int n_tiles = (N + ROWS_B - 1) / ROWS_B;
-  const int rbase = wave * (4 * R) + g * R;
+  const int rbase = (wave - kg * GEMV_NW) * (4 * R) + g * R;
 
   long long row_base = 0;
   const float* x = P.x;
@@ -478,43 +514,43 @@ __global__ __launch_bounds__(GEMV_NT) void qgemv_flight_kernel(GemvParams P) {
     if (P.x_per_sel) x = P.x + (long long)blockIdx.z * P.x_sel_stride;
   }
 
-  // 1. this thread's activation groups g = tid + 256 i (i < NSB) and norm weights -> registers
-  const bool nrm = P.norm != NORM_NONE, lnb = P.norm == NORM_LAYER && P.norm_b;
+  // 1. this thread's activation groups g = tid + NT i (i < NSB) and norm weights -> registers
+  constexpr bool nrm = NRM != 0, lnb = NRM == 2;
   f32x4 xv[NSB][4], nw[NSB][4], nb[NSB][4];
-  // unconditional loads from clamped / stand-in addresses (a conditional load would make the compiler
-  // drain it before the weight loads are issued); out-of-range values are masked at use
-  const float* nwp = nrm ? P.norm_w : x;
-  const float* nbp = lnb ? P.norm_b : x;
+  // unconditional loads from clamped addresses (a conditional load would make the compiler drain it
+  // before the weight loads are issued); out-of-range values are masked at use
 #pragma unroll
   for (int i = 0; i < NSB; ++i) {
-    const int gi = min(tid + GEMV_NT * i, K / 16 - 1);
+    const int gi = min(tid + NT * i, K / 16 - 1);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       xv[i][j] = *(const f32x4*)(x + 16 * gi + 4 * j);
-      nw[i][j] = *(const f32x4*)(nwp + 16 * gi + 4 * j);
-      nb[i][j] = *(const f32x4*)(nbp + 16 * gi + 4 * j);
+      if constexpr (nrm) nw[i][j] = *(const f32x4*)(P.norm_w + 16 * gi + 4 * j);
+      if constexpr (lnb) nb[i][j] = *(const f32x4*)(P.norm_b + 16 * gi + 4 * j);
     }
   }
+  __builtin_amdgcn_sched_barrier(0);  // activations ahead of the weights
   // 2. every weight tile of this block in flight (surplus slots re-read the last tile, unused)
   WTile<QT, NSB, R> T[J];
 #pragma unroll
   for (int j = 0; j < J; ++j) {
     const int t = min((int)blockIdx.x + j * (int)gridDim.x, n_tiles - 1);
-    load_wtile<QT, NSB, R>(w, row_base, t * ROWS_B + rbase, N, SB, 0, s, T[j]);
+    load_wtile<QT, NSB, R>(w, row_base, t * ROWS_B + rbase, N, SB, sb0, s, T[j], se);
   }
+  __builtin_amdgcn_sched_barrier(0);  // every load issued before the prologue's first wait
   // 3. norm statistics + quantisation from registers while the weights stream
 #pragma unroll
   for (int i = 0; i < NSB; ++i) {
-    const bool ok = 16 * (tid + GEMV_NT * i) < K;
+    const bool ok = 16 * (tid + NT * i) < K;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       if (!ok) xv[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-      if (!nrm) nw[i][j] = (f32x4){1.f, 1.f, 1.f, 1.f};
-      if (!lnb) nb[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      if constexpr (!nrm) nw[i][j] = (f32x4){1.f, 1.f, 1.f, 1.f};
+      if constexpr (!lnb) nb[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
     }
   }
   float mean = 0.f, rstd = 1.f;
-  if (nrm) {
+  if (nrm && !(DBG & 2)) {
     float sm = 0.f, ss = 0.f;
 #pragma unroll
     for (int i = 0; i < NSB; ++i)
@@ -524,9 +560,9 @@ __global__ __launch_bounds__(GEMV_NT) void qgemv_flight_kernel(GemvParams P) {
         sm += v.x + v.y + v.z + v.w;
         ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
       }
-    ss = block_sum<GEMV_NT>(ss, red);
-    if (P.norm == NORM_LAYER) {
-      sm = block_sum<GEMV_NT>(sm, red);
+    ss = block_sum<NT>(ss, red);
+    if (NRM == 2 || P.norm == NORM_LAYER) {
+      sm = block_sum<NT>(sm, red);
       mean = sm / K;
       rstd = rsqrtf(fmaxf(ss / K - mean * mean, 0.f) + P.eps);
     } else {
@@ -535,9 +571,11 @@ __global__ __launch_bounds__(GEMV_NT) void qgemv_flight_kernel(GemvParams P) {
   }
 #pragma unroll
   for (int i = 0; i < NSB; ++i) {
-    const int gi = tid + GEMV_NT * i;
-    if (gi >= SB * 16) continue;
-    const int slot = (gi >> 4) * XPAD + (gi & 15);
+    if constexpr (DBG & 2) continue;
+    const int gi = tid + NT * i;
+    // branch-free: surplus threads store to the dummy slot (a guarded block lets the compiler sink
+    // the activation loads behind the weight loads, then drain them all with vmcnt(0))
+    const int slot = gi < SB * 16 ? (gi >> 4) * XPAD + (gi & 15) : XS;
     float v[16];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -571,6 +609,36 @@ __global__ __launch_bounds__(GEMV_NT) void qgemv_flight_kernel(GemvParams P) {
     lf[slot] = (f32x2){d, d * (float)qsum};
   }
   __syncthreads();
+  if constexpr (KS > 1) {  // one tile per block: groups 1.. hand their partial sums to group 0
+    static_assert(J == 1, "in-block K split is for single-tile blocks");
+    float acc[R][1];
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r][0] = 0.f;
+    if constexpr (DBG & 1) {
+      unsigned v = 0;
+#pragma unroll
+      for (int i = 0; i < NSB; ++i)
+#pragma unroll
+        for (int tt = 0; tt < 8; ++tt) v ^= T[0].a[0][i][tt].x ^ T[0].a[0][i][tt].w ^ T[0].m[0][i].y;
+      acc[0][0] = (float)(v & 1);
+    } else {
+      compute_wtile<QT, NSB, R, 1>(T[0], SB, sb0, s, lq, lf, XS, acc, se);
+    }
+    float* part = red + NT / 64;  // [KS-1][R][GEMV_NT]
+    if (kg > 0) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) part[((kg - 1) * R + r) * GEMV_NT + gtid] = acc[r][0];
+    }
+    __syncthreads();
+    if (kg == 0 && (int)blockIdx.x < n_tiles) {
+#pragma unroll
+      for (int k = 1; k < KS; ++k)
+#pragma unroll
+        for (int r = 0; r < R; ++r) acc[r][0] += part[((k - 1) * R + r) * GEMV_NT + gtid];
+      finish_rows<R, 1>(P, acc, (int)blockIdx.x * ROWS_B + rbase, N, 0, s);
+    }
+    return;
+  }
   // 4. consume the tiles in issue order
 #pragma unroll
   for (int j = 0; j < J; ++j) {
@@ -579,7 +647,19 @@ __global__ __launch_bounds__(GEMV_NT) void qgemv_flight_kernel(GemvParams P) {
     float acc[R][1];
 #pragma unroll
     for (int r = 0; r < R; ++r) acc[r][0] = 0.f;
-    compute_wtile<QT, NSB, R, 1>(T[j], SB, 0, s, lq, lf, XS, acc);
+    if constexpr (DBG & 1) {  // memory path only: consume every loaded word, no dot products
+      unsigned v = 0;
+#pragma unroll
+      for (int i = 0; i < NSB; ++i)
+#pragma unroll
+        for (int tt = 0; tt < 8; ++tt) {
+          v ^= T[j].a[0][i][tt].x ^ T[j].a[0][i][tt].w ^ T[j].m[0][i].y;
+          if constexpr (QT == QT_Q6_K) v ^= T[j].h[0][i][tt].x;
+        }
+      acc[0][0] = (float)(v & 1);
+    } else {
+      compute_wtile<QT, NSB, R, 1>(T[j], SB, 0, s, lq, lf, XS, acc);
+    }
     finish_rows<R, 1>(P, acc, t * ROWS_B + rbase, N, 0, s);
   }
 }
@@ -592,7 +672,11 @@ constexpr int flight_jmax() {
   return regs * 3 <= 150 ? 3 : regs * 2 <= 150 ? 2 : 1;
 }
 
-static size_t lds_bytes(int K, int BT) { return (size_t)BT * ((K + 255) / 256) * XPAD * 24 + 4 * GEMV_NW; }
+static size_t lds_bytes(int K, int BT) { return (size_t)BT * ((K + 255) / 256) * XPAD * 24 + 24 + 4 * GEMV_NW; }
+// flight kernel with an in-block K split: activation slots + reduction slots + partial sums
+static size_t lds_bytes_ks(int K, int KS, int R) {
+  return (size_t)((K + 255) / 256) * XPAD * 24 + 24 + 4 * GEMV_NW * KS + (size_t)4 * (KS - 1) * R * GEMV_NT;
+}
 
 template <int QT, int NSB, int R, int BT, int DBG = 0>
 static void launch_t(const GemvParams& P, hipStream_t s) {
@@ -607,13 +691,73 @@ static void launch_t(const GemvParams& P, hipStream_t s) {
   hipLaunchKernelGGL((qgemv_kernel<QT, NSB, R, BT, DBG>), dim3(gx, by, bz), dim3(GEMV_NT), lds_bytes(P.w.K, BT), s, P);
 }
 
+template <int QT, int NSB, int R, int J, int NRM>
+static void launch_flight_n(const GemvParams& P, int gx, hipStream_t s) {
+  const int bz = P.expert_ids ? P.n_sel : 1;
+  const size_t lds = lds_bytes(P.w.K, 1);
+  if constexpr (R == 1 && (QT == QT_Q4_K || QT == QT_Q6_K) && (NSB == 1 || NSB == 3) && NRM < 2) {
+    switch (g_tune.debug) {  // microbenchmark-only variants (scripts/bench_gemv.py OMX_BENCH_DEBUG)
+      case 1: hipLaunchKernelGGL((qgemv_flight_kernel<QT, NSB, R, J, NRM, 1>), dim3(gx, 1, bz), dim3(GEMV_NT), lds, s, P); return;
+      case 2: hipLaunchKernelGGL((qgemv_flight_kernel<QT, NSB, R, J, NRM, 2>), dim3(gx, 1, bz), dim3(GEMV_NT), lds, s, P); return;
+      case 3: hipLaunchKernelGGL((qgemv_flight_kernel<QT, NSB, R, J, NRM, 3>), dim3(gx, 1, bz), dim3(GEMV_NT), lds, s, P); return;
+      default: break;
+    }
+  }
+  hipLaunchKernelGGL((qgemv_flight_kernel<QT, NSB, R, J, NRM>), dim3(gx, 1, bz), dim3(GEMV_NT), lds, s, P);
+}
+
+template <int QT, int NSB, int KS, int NRM>
+static void launch_flight_ks_n(const GemvParams& P, int gx, hipStream_t s) {
+  const int bz = P.expert_ids ? P.n_sel : 1;
+  const size_t lds = lds_bytes_ks(P.w.K, KS, 1);
+  if constexpr ((QT == QT_Q4_K || QT == QT_Q6_K) && NRM == 0) {
+    switch (g_tune.debug) {  // microbenchmark-only variants, as launch_flight_n
+      case 1: hipLaunchKernelGGL((qgemv_flight_kernel<QT, NSB, 1, 1, NRM, 1, KS>), dim3(gx, 1, bz), dim3(GEMV_NT * KS), lds, s, P); return;
+      case 2: hipLaunchKernelGGL((qgemv_flight_kernel<QT, NSB, 1, 1, NRM, 2, KS>), dim3(gx, 1, bz), dim3(GEMV_NT * KS), lds, s, P); return;
+      case 3: hipLaunchKernelGGL((qgemv_flight_kernel<QT, NSB, 1, 1, NRM, 3, KS>), dim3(gx, 1, bz), dim3(GEMV_NT * KS), lds, s, P); return;
+      default: break;
+    }
+  }
+  hipLaunchKernelGGL((qgemv_flight_kernel<QT, NSB, 1, 1, NRM, 0, KS>), dim3(gx, 1, bz), dim3(GEMV_NT * KS), lds, s, P);
+}
+
+template <int QT, int NSB, int KS>
+static void launch_flight_ks(const GemvParams& P, int gx, hipStream_t s) {
+  if (P.norm == NORM_NONE) launch_flight_ks_n<QT, NSB, KS, 0>(P, gx, s);
+  else if (P.norm == NORM_LAYER && P.norm_b) launch_flight_ks_n<QT, NSB, KS, 2>(P, gx, s);
+  else launch_flight_ks_n<QT, NSB, KS, 1>(P, gx, s);
+}
+
 template <int QT, int NSB, int R, int J>
 static void launch_flight_j(const GemvParams& P, int gx, hipStream_t s) {
-  const int bz = P.expert_ids ? P.n_sel : 1;
-  hipLaunchKernelGGL((qgemv_flight_kernel<QT, NSB, R, J>), dim3(gx, 1, bz), dim3(GEMV_NT), lds_bytes(P.w.K, 1), s, P);
+  if (P.norm == NORM_NONE) launch_flight_n<QT, NSB, R, J, 0>(P, gx, s);
+  else if (P.norm == NORM_LAYER && P.norm_b) launch_flight_n<QT, NSB, R, J, 2>(P, gx, s);
+  else launch_flight_n<QT, NSB, R, J, 1>(P, gx, s);
 }
 
 // grid: at least one block per CU while the matrix has the tiles, then up to J tiles per block
+// in-block K split for single-row-tile matrices: KS groups of 4 waves, each NSB' = ceil(need / KS)
+static int flight_ks(int need, int tiles, int bz) {
+  if (g_tune.ks > 0) return g_tune.ks;
+  if (tiles * bz > 256 * 2) return 1;  // enough blocks to fill the CUs with waves already
+  return need >= 3 ? 3 : 2;
+}
+
+template <int QT>
+static bool launch_flight_split(const GemvParams& P, int need, hipStream_t s) {
+  const int tiles = (P.w.N + 4 * GEMV_NW - 1) / (4 * GEMV_NW);
+  const int bz = P.expert_ids ? P.n_sel : 1;
+  const int ks = flight_ks(need, tiles, bz);
+  if (ks <= 1) return false;
+  const int nsb = (need + ks - 1) / ks;  // 16 * nsb >= ceil(SB / ks)
+  if (ks == 2 && nsb == 1) launch_flight_ks<QT, 1, 2>(P, tiles, s);
+  else if (ks == 2 && nsb == 2) launch_flight_ks<QT, 2, 2>(P, tiles, s);
+  else if (ks == 3 && nsb == 1) launch_flight_ks<QT, 1, 3>(P, tiles, s);
+  else if (ks == 4 && nsb == 1) launch_flight_ks<QT, 1, 4>(P, tiles, s);
+  else return false;
+  return true;
+}
+
 template <int QT, int NSB, int R>
 static void launch_flight(const GemvParams& P, hipStream_t s) {
   constexpr int JM = flight_jmax<QT, NSB, R>();
@@ -649,19 +793,11 @@ static void launch_nsb(const GemvParams& P, hipStream_t s) {
 
 template <int QT>
 static void launch_q(const GemvParams& P, hipStream_t s) {
-  if constexpr (QT == QT_Q4_K) {
-    if (g_tune.debug && P.B == 1 && (P.w.K + 255) / 256 <= 16) {
-      switch (g_tune.debug) {
-        case 1: launch_t<QT, 1, 1, 1, 1>(P, s); return;
-        case 2: launch_t<QT, 1, 1, 1, 2>(P, s); return;
-        default: launch_t<QT, 1, 1, 1, 3>(P, s); return;
-      }
-    }
-  }
   if (P.B == 1 || P.expert_ids != nullptr) {  // decode (and MoE: experts differ per batch row)
     const int need = ((P.w.K + 255) / 256 + 15) / 16;
     if (P.B == 1 && need <= 4) {  // whole K in one chunk: all-in-flight kernel
       if (g_tune.rows == 2 && need == 1) { launch_flight<QT, 1, 2>(P, s); return; }
+      if (launch_flight_split<QT>(P, need, s)) return;
       switch (need) {
         case 1: launch_flight<QT, 1, 1>(P, s); return;
         case 2: launch_flight<QT, 2, 1>(P, s); return;

@@ -68,9 +68,10 @@ struct GemvTuning {
   int blocks_per_cu = 4;  // persistent-grid cap = 256 CUs x this (scripts/bench_gemv.py sweep)
   int rows = 1;           // rows per 16-lane row group in B == 1 launches (1 or 2)
   int debug = 0;          // microbenchmark-only kernel variants (gemv.hip DBG)
+  int ks = 0;             // in-block K split of the flight kernel: 0 = auto, 1 = off, 2..4 = forced
 };
 extern GemvTuning g_tune;
-void set_gemv_tuning(int blocks_per_cu, int rows, int debug);
+void set_gemv_tuning(int blocks_per_cu, int rows, int debug, int ks = -1);
 
 // Dequantize rows of a repacked matrix (embedding gather / fp16 copies)
 void embed_rows(const QMat& w, const int* rows, int n, float* out, int ldo, hipStream_t s);

@@ -171,6 +171,7 @@ class Runner:
             self._pinned = [torch.zeros(5, max_batch, dtype=torch.int32).pin_memory() for _ in range(4)]
             self._pin_i = 0
             self._tok_host = torch.zeros(max_batch, dtype=torch.int32).pin_memory()
+            self._tok_ring = torch.zeros(4, dtype=torch.int32).pin_memory()  # sampled tokens, per step
         self.load_s = time.perf_counter() - t0
 
     # ------------------------------------------------------------------ sizing helpers
@@ -354,11 +355,11 @@ class Runner:
             self._graph(1)
         torch.cuda.synchronize()
 
-    def decode_step(self, sid: int) -> None:
+    def decode_step(self, sid: int, pos: int | None = None) -> None:
         """One token for sequence `sid` whose input token (not yet in `tokens`) is already in
-        d_tokens[0] on device; it sits at position len(tokens)."""
+        d_tokens[0] on device; it sits at position `pos` (default len(tokens))."""
         s = self.kv.seqs[sid]
-        pos = s.length
+        pos = s.length if pos is None else pos
         if pos + 1 > len(s.blocks) * self.block_size:
             self.kv.reserve(sid, min(self.ctx, pos + 4 * self.block_size))
             self._sync_block_table(sid)
@@ -369,6 +370,51 @@ class Runner:
                 self._graph(1).replay()
             else:
                 self._decode_body(1)
+
+    def _generate_pipelined(self, sid: int, st, first: int, max_tokens: int, stop, times, t1) -> Iterator[int]:
+        """Two decode steps in flight: step i consumes token i+1 straight from device memory (written
+        by step i-1's sampler), so the host never has to see a token before issuing the step after
+        it. When token n is handed out, steps producing tokens n+1 and n+2 are already queued; the
+        host's detokenise / stop checks / Python overhead hide behind ~2 steps of GPU work instead of
+        leaving the GPU idle between steps (was ~130 us per step, profiles/r1_attn). A step issued
+        past a stop is wasted work whose KV position is never recorded in `tokens`."""
+        base = st.length  # position of `first`
+        ring = self._tok_ring
+        R = ring.numel()
+        evs: list = [None] * R
+        issued = 0
+
+        def issue():
+            nonlocal issued
+            self.decode_step(sid, base + issued)
+            slot = issued % R
+            ring[slot:slot + 1].copy_(self.s_out[:1], non_blocking=True)
+            e = torch.cuda.Event()
+            e.record()
+            evs[slot] = e
+            issued += 1
+
+        n = 0
+        tok = first
+        try:
+            while True:
+                n += 1  # handing out token n (1-based; token 1 came from the prompt)
+                done = n >= max_tokens or (stop is not None and stop(tok))
+                if not done:
+                    target = min(n + 1, max_tokens - 1)  # steps 0..n: tokens up to n+2
+                    while issued < target:
+                        issue()
+                    st.tokens.append(tok)  # step n-1 (issued) writes its KV
+                yield tok
+                if done:
+                    break
+                slot = (n - 1) % R  # step n-1 produced token n+1
+                evs[slot].synchronize()
+                tok = int(ring[slot])
+        finally:
+            if times is not None:
+                times.gen_tokens = n
+                times.gen_s = time.perf_counter() - t1
 
     def generate(self, sid: int, prompt: list[int], options: SamplingOptions | None = None,
                  max_tokens: int = 128, stop: Callable[[int], bool] | None = None,
@@ -396,9 +442,12 @@ class Runner:
             times.prompt_tokens = len(prompt) - keep
             times.prompt_s = time.perf_counter() - t0
         t1 = time.perf_counter()
+        max_tokens = min(max_tokens, self.ctx - st.length)
+        if self.is_gpu and self.tp_ctrl is None:
+            yield from self._generate_pipelined(sid, st, first, max_tokens, stop, times, t1)
+            return
         n = 0
         tok = first
-        max_tokens = min(max_tokens, self.ctx - st.length)
         ctrl = self.tp_ctrl
         follower = ctrl is not None and not ctrl.leader
         try:

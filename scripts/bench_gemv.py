@@ -1,6 +1,7 @@
 """Decode-GEMV microbenchmark on the Llama-2-7B Q4_K_M shapes: achieved HBM GB/s per launch shape.
 Run on the GPU box:  python scripts/bench_gemv.py  (prints one line per shape x tuning)."""
 import itertools
+import time
 import os
 import sys
 
@@ -47,17 +48,29 @@ def main():
     res = []
     keep = os.environ.get("OMX_BENCH_SHAPES", "").split(",") if os.environ.get("OMX_BENCH_SHAPES") else None
     mats = {name: make(qt, N, K) for name, qt, N, K, _ in SHAPES if keep is None or name in keep}
-    knobs = [(b, r, 0) for b in (1, 2, 4) for r in (1, 2)]
+    knobs = [(b, r, 0, 0) for b in (1, 2, 4) for r in (1, 2)]
     if os.environ.get("OMX_BENCH_DEBUG"):  # memory-path experiments on the Q4_K K=4096 kernel
-        knobs = [(b, 1, d) for b in (2, 4) for d in (0, 1, 2, 3)]
+        knobs = [(b, 1, d, 1) for b in (2, 4) for d in (0, 1, 2, 3)]
+    if os.environ.get("OMX_BENCH_KS"):  # in-block K split of the flight kernel (1 = off), full and memory-only
+        knobs = [(4, 1, d, k) for k in (1, 2, 3, 4) for d in (0, 3)]
+        if os.environ["OMX_BENCH_KS"] != "1":  # e.g. OMX_BENCH_KS=3: all debug variants at that split
+            knobs = [(4, 1, d, int(os.environ["OMX_BENCH_KS"])) for d in (0, 1, 2, 3)]
     if os.environ.get("OMX_BENCH_KNOBS"):  # e.g. "3,2,1" (profiling one configuration)
         knobs = [tuple(int(v) for v in os.environ["OMX_BENCH_KNOBS"].split(","))]
     shapes = SHAPES
     if os.environ.get("OMX_BENCH_SHAPES"):
         keep = os.environ["OMX_BENCH_SHAPES"].split(",")
         shapes = [s for s in SHAPES if s[0] in keep]
-    for (name, qt, N, K, epi), (bpc, rpw, r1) in itertools.product(shapes, knobs):
-        C.set_gemv_tuning(bpc, rpw, r1)
+    knobs = [k + (0,) * (4 - len(k)) for k in knobs]
+    # clock warm-up: the first shape measured on an idle GPU otherwise reads up to 2x slow
+    big = torch.empty(256 << 20, dtype=torch.uint8, device="cuda")
+    t0 = time.time()
+    while time.time() - t0 < 1.5:
+        big.add_(1)
+    torch.cuda.synchronize()
+    del big
+    for (name, qt, N, K, epi), (bpc, rpw, r1, ks) in itertools.product(shapes, knobs):
+        C.set_gemv_tuning(bpc, rpw, r1, ks)
         tups, ts, nbytes = mats[name]
         x = torch.randn(1, K, device="cuda")
         nw = torch.ones(K, device="cuda")
@@ -76,12 +89,12 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) * 1e3 / n
-        res.append((name, f"blocks/CU={bpc} rows={rpw} dbg={r1}", us, nbytes / us / 1e3))
+        res.append((name, f"blocks/CU={bpc} rows={rpw} dbg={r1} ks={ks}", us, nbytes / us / 1e3))
         print(f"{name:10s} {res[-1][1]} {us:8.2f} us  {nbytes/us/1e3:7.1f} GB/s", flush=True)
-    C.set_gemv_tuning(4, 1, 0)
+    C.set_gemv_tuning(4, 1, 0, 0)
     print("best per shape:")
     for name in mats:
-        b = min((r for r in res if r[0] == name), key=lambda r: r[2])
+        b = min((r for r in res if r[0] == name), key=lambda r: ("dbg=0" not in r[1], r[2]))
         print(f"  {name:10s} {b[1]} {b[2]:.2f} us {b[3]:.0f} GB/s")
 
 

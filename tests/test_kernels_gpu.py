@@ -101,6 +101,28 @@ def test_gemv_glu():
     assert rel(y, ref) < 1.5e-2
 
 
+@pytest.mark.parametrize("ks", [1, 2, 3, 4])
+@pytest.mark.parametrize("qt,K", [(GGMLType.Q4_K, 11008), (GGMLType.Q6_K, 11008), (GGMLType.Q4_K, 4096),
+                                  (GGMLType.Q8_0, 2560), (GGMLType.Q6_K, 1024)])
+def test_gemv_flight_k_split(qt, K, ks):
+    """The decode kernel's in-block K split (KS groups of 4 waves on the same rows, partial sums
+    meeting in LDS) against fp32 torch, with the RMSNorm prologue and the pairwise GLU epilogue."""
+    F = 200  # 400 rows: the last 16-row tile is partial
+    m = QM(qt, 2 * F, K, seed=K + ks)
+    x = torch.randn(1, K, device="cuda")
+    nw = torch.rand(K, device="cuda") + 0.5
+    y = torch.zeros(1, F, device="cuda")
+    C().set_gemv_tuning(0, 0, 0, ks)
+    try:
+        gemv(m, x, norm=1, nw=nw, epi=2, y=y)
+    finally:
+        C().set_gemv_tuning(0, 0, 0, 0)
+    xn = x * torch.rsqrt(x.pow(2).mean(-1, keepdim=True) + 1e-5) * nw
+    gu = xn @ m.w.T
+    ref = torch.nn.functional.silu(gu[:, 0::2]) * gu[:, 1::2]
+    assert rel(y, ref) < 1.5e-2
+
+
 @pytest.mark.parametrize("D,n_rot", [(128, 128), (80, 32), (64, 64)])
 def test_gemv_qkv_rope_kv_scatter(D, n_rot):
     H, Hkv, K, B, bs = 4, 2, 512, 3, 16
