@@ -215,6 +215,8 @@ PYBIND11_MODULE(_C, m) {
     P.step = Pp<int>(d["step"].cast<uintptr_t>());
     P.out = Pp<int>(d["out"].cast<uintptr_t>());
     P.out_logprob = Pp<float>(d.contains("out_logprob") ? d["out_logprob"].cast<uintptr_t>() : 0);
+    P.ws = Pp<float>(d.contains("ws") ? d["ws"].cast<uintptr_t>() : 0);
+    P.counters = Pp<int>(d.contains("counters") ? d["counters"].cast<uintptr_t>() : 0);
     sample(P, S(stream));
   });
 

@@ -739,7 +739,9 @@ static void launch_flight_j(const GemvParams& P, int gx, hipStream_t s) {
 // in-block K split for single-row-tile matrices: KS groups of 4 waves, each NSB' = ceil(need / KS)
 static int flight_ks(int need, int tiles, int bz) {
   if (g_tune.ks > 0) return g_tune.ks;
-  if (tiles * bz > 256 * 2) return 1;  // enough blocks to fill the CUs with waves already
+  // K <= 4096 (need 1): a split leaves half of every row group's lanes idle and doubles the VALU
+  // work (measured: O 4.4 -> 5.0 us, V Q6_K 5.0 -> 7.8 us); enough tiles fill the CUs anyway
+  if (need < 2 || tiles * bz > 256 * 2) return 1;
   return need >= 3 ? 3 : 2;
 }
 

@@ -117,7 +117,12 @@ struct SampleParams {
   int* step;                   // [B] RNG counter, incremented per sample
   int* out;                    // [B] sampled token
   float* out_logprob;          // [B] or null
+  // multi-block path (null = single-block kernel): candidate lists [B][ceil(V/1024)][2][64] and
+  // per-row tickets [B] (zero-initialised; re-armed by the kernel)
+  float* ws = nullptr;
+  int* counters = nullptr;
 };
+constexpr int SAMPLE_WS_FLOATS_PER_ROW(int V) { return ((V + 1023) / 1024) * 2 * 64; }
 void sample(const SampleParams& P, hipStream_t s);
 void argmax(const float* logits, int B, int V, int ld, int* out, hipStream_t s);
 

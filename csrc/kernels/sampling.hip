@@ -7,6 +7,7 @@
 // radix select over order-preserving float keys is the fallback when too many logits tie.
 #include "common.h"
 #include "ops.h"
+#include "wave_shuffle.h"
 
 namespace omx {
 
@@ -52,28 +53,16 @@ __device__ void block_argmax(const float* lg, int V, float* sv, int* si, float& 
   bi = si[0];
 }
 
-__global__ __launch_bounds__(SAMPLE_NT) void sample_kernel(SampleParams P) {
-  __shared__ float cval[SAMPLE_CAP];
-  __shared__ int cidx[SAMPLE_CAP];
-  __shared__ unsigned hist[256];
-  __shared__ float redv[SAMPLE_NT / 64];
-  __shared__ int redi[SAMPLE_NT / 64];
-  __shared__ unsigned s_prefix, s_mask, s_remaining;
-  __shared__ int s_count, s_bstar;
-  __shared__ unsigned bins[SAMPLE_BINS];
-  __shared__ unsigned wsum[SAMPLE_NT / 64];
-  const int b = blockIdx.x;
-  float* lg = (float*)P.logits + (long long)b * P.ld;
-  const int V = P.V;
-
-  // ---- penalties over the recent-token window (each distinct token once, with its count)
+// repeat / presence / frequency penalties over the recent-token window, in place (each distinct
+// token once, with its count); block-wide
+__device__ void apply_penalties_inplace(const SampleParams& P, int b, float* lg, int V) {
   const int seen = P.hist_count[b];
   int win = min(seen, P.repeat_last_n[b]);
   win = min(win, P.hist_cap);
   const float rp = P.repeat_penalty[b], pp = P.presence_penalty[b], fp = P.frequency_penalty[b];
   if (win > 0 && (rp != 1.f || pp != 0.f || fp != 0.f)) {
     const int* h = P.history + (long long)b * P.hist_cap;
-    for (int i = threadIdx.x; i < win; i += SAMPLE_NT) {
+    for (int i = threadIdx.x; i < win; i += blockDim.x) {
       const int tok = h[(seen - 1 - i) % P.hist_cap];
       bool first = true;
       int cnt = 1;
@@ -94,10 +83,25 @@ __global__ __launch_bounds__(SAMPLE_NT) void sample_kernel(SampleParams P) {
     }
     __syncthreads();
   }
+}
+
+// single-block selection over the whole (penalised) row: greedy, or top-k (any k <= SAMPLE_CAP)
+// -> top-p -> min-p -> temperature -> draw. Needs blockDim.x == SAMPLE_NT.
+__device__ void legacy_select(const SampleParams& P, int b, float* lg, int V, int& chosen, float& chosen_lp) {
+
+  __shared__ float cval[SAMPLE_CAP];
+  __shared__ int cidx[SAMPLE_CAP];
+  __shared__ unsigned hist[256];
+  __shared__ float redv[SAMPLE_NT / 64];
+  __shared__ int redi[SAMPLE_NT / 64];
+  __shared__ unsigned s_prefix, s_mask, s_remaining;
+  __shared__ int s_count, s_bstar;
+  __shared__ unsigned bins[SAMPLE_BINS];
+  __shared__ unsigned wsum[SAMPLE_NT / 64];
 
   const float temp = P.temperature[b];
-  int chosen = 0;
-  float chosen_lp = 0.f;
+  chosen = 0;
+  chosen_lp = 0.f;
   if (temp <= 0.f) {
     float best;
     block_argmax(lg, V, redv, redi, best, chosen);
@@ -181,13 +185,36 @@ __global__ __launch_bounds__(SAMPLE_NT) void sample_kernel(SampleParams P) {
     const unsigned thr = s_prefix;
     if (threadIdx.x == 0) s_count = 0;
     __syncthreads();
-    for (int i = threadIdx.x; i < V; i += SAMPLE_NT) {
+    for (int i = threadIdx.x; i < V; i += SAMPLE_NT) {  // strictly above the k-th key: < k of them
       const float v = lg[i];
-      if (fkey(v) >= thr) {
+      if (fkey(v) > thr) {
         const int slot = atomicAdd(&s_count, 1);
-        if (slot < SAMPLE_CAP) { cval[slot] = v; cidx[slot] = i; }
+        cval[slot] = v;
+        cidx[slot] = i;
       }
     }
+    __syncthreads();
+    // ties with the k-th key fill the rest lowest index first (the host's stable order; atomic
+    // arrival order would make the kept set depend on scheduling when > SAMPLE_CAP logits tie)
+    int have = s_count;
+    const int ln = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (int base = 0; base < V && have < k; base += SAMPLE_NT) {
+      const int i = base + threadIdx.x;
+      const bool tie = i < V && fkey(lg[i]) == thr;
+      const unsigned long long m = __ballot(tie);
+      if (ln == 0) wsum[wv] = (unsigned)__popcll(m);
+      __syncthreads();
+      unsigned pre = 0, tot = 0;
+      for (int w = 0; w < SAMPLE_NT / 64; ++w) {
+        if (w < wv) pre += wsum[w];
+        tot += wsum[w];
+      }
+      const int pos = have + (int)pre + __popcll(m & ((1ull << ln) - 1));
+      if (tie && pos < k) { cval[pos] = lg[i]; cidx[pos] = i; }
+      have = min(k, have + (int)tot);
+      __syncthreads();  // wsum reuse
+    }
+    if (threadIdx.x == 0) s_count = have;
     __syncthreads();
     }
     const int cnt = min(s_count, SAMPLE_CAP);
@@ -253,17 +280,231 @@ __global__ __launch_bounds__(SAMPLE_NT) void sample_kernel(SampleParams P) {
     chosen = redi[0];
     chosen_lp = redv[0];
   }
-  if (threadIdx.x == 0) {
-    P.out[b] = chosen;
-    if (P.out_logprob) P.out_logprob[b] = chosen_lp;
-    P.history[(long long)b * P.hist_cap + (seen % P.hist_cap)] = chosen;
-    P.hist_count[b] = seen + 1;
-    P.step[b] += 1;
+}
+
+__device__ __forceinline__ void finish_sample(const SampleParams& P, int b, int chosen, float chosen_lp) {
+  const int seen = P.hist_count[b];
+  P.out[b] = chosen;
+  if (P.out_logprob) P.out_logprob[b] = chosen_lp;
+  P.history[(long long)b * P.hist_cap + (seen % P.hist_cap)] = chosen;
+  P.hist_count[b] = seen + 1;
+  P.step[b] += 1;
+}
+
+__global__ __launch_bounds__(SAMPLE_NT) void sample_kernel(SampleParams P) {
+  const int b = blockIdx.x;
+  float* lg = (float*)P.logits + (long long)b * P.ld;
+  apply_penalties_inplace(P, b, lg, P.V);
+  int chosen;
+  float chosen_lp;
+  legacy_select(P, b, lg, P.V, chosen, chosen_lp);
+  if (threadIdx.x == 0) finish_sample(P, b, chosen, chosen_lp);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Multi-block fast path (top_k in 1..64, or greedy): one 1024-thread block per 1024-logit slice,
+// one logit per lane. Each wave sorts its 64 logits (64-lane bitonic network on DPP / permlane
+// exchanges, order = value desc, index asc -- the host reference's stable argsort); the block's 16
+// sorted lists merge through LDS in a tree into its exact top-64; the list goes out with sc1
+// (agent-scope) stores and the block drawing the last agent-scope ticket merges every block's list
+// and samples with wave scans (MI355X_MICROARCH.md "Valid forms" row 1, as attention's split
+// combine). A row whose top_k is outside 1..64 is handed to legacy_select in that last block, on
+// the untouched logits.
+constexpr int FAST_K = 64;
+constexpr int FAST_SLICE = SAMPLE_NT;
+
+__device__ __forceinline__ bool cand_better(float av, int ai, float bv, int bi) {
+  return av > bv || (av == bv && ai < bi);
+}
+
+// compare-exchange with lane ^ J; the lower lane of the pair ends with the better when lo_better
+template <int J>
+__device__ __forceinline__ void cand_cx(float& v, int& i, bool lo_better) {
+  const int lane = threadIdx.x & 63;
+  const float ov = xor_shfl<J>(v);
+  const int oi = xor_shfl<J>(i);
+  const bool want_better = ((lane & J) == 0) == lo_better;
+  if (want_better == cand_better(ov, oi, v, i)) { v = ov; i = oi; }
+}
+
+// half-cleaners J, J/2, .., 1
+template <int J>
+__device__ __forceinline__ void cand_clean(float& v, int& i, bool lo_better) {
+  cand_cx<J>(v, i, lo_better);
+  if constexpr (J > 1) cand_clean<J / 2>(v, i, lo_better);
+}
+
+template <int SIZE>
+__device__ __forceinline__ void cand_sort_stage(float& v, int& i, bool desc) {
+  const int lane = threadIdx.x & 63;
+  cand_clean<SIZE / 2>(v, i, ((lane & SIZE) == 0) == desc);
+  if constexpr (SIZE < 64) cand_sort_stage<SIZE * 2>(v, i, desc);
+}
+
+// sort one candidate per lane across the wave: descending (lane 0 best) or ascending
+__device__ __forceinline__ void wave_bitonic_sort(float& v, int& i, bool desc) { cand_sort_stage<2>(v, i, desc); }
+
+// R (desc) := top-64 of R u C, where C is sorted ascending
+__device__ __forceinline__ void wave_merge_asc(float& rv, int& ri, float cv, int ci) {
+  if (cand_better(cv, ci, rv, ri)) { rv = cv; ri = ci; }  // bitonic: the 64 best of the union
+  cand_clean<32>(rv, ri, true);
+}
+
+// R (desc) := top-64 of R u L, where L is sorted descending (lane l reads L[63 - l])
+__device__ __forceinline__ void wave_merge_desc(float& rv, int& ri, const float* lv, const int* li) {
+  const int lane = threadIdx.x & 63;
+  wave_merge_asc(rv, ri, lv[63 - lane], li[63 - lane]);
+}
+
+__global__ __launch_bounds__(SAMPLE_NT) void sample_fast_kernel(SampleParams P) {
+  __shared__ int pen_cnt[FAST_SLICE];
+  __shared__ float lv[SAMPLE_NT / 64][FAST_K];
+  __shared__ int li[SAMPLE_NT / 64][FAST_K];
+  __shared__ int s_last;
+  const int b = blockIdx.y, G = gridDim.x, blk = blockIdx.x;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const float* lg = P.logits + (long long)b * P.ld;
+  const int V = P.V, base = blk * FAST_SLICE + wave * 64;
+  const float temp = P.temperature[b];
+  const int kk = P.top_k[b];
+  const bool fast = temp <= 0.f || (kk >= 1 && kk <= FAST_K);
+
+  if (fast) {
+    const int ix = base + lane;
+    float v = ix < V ? lg[ix] : -INFINITY;
+    // penalties for the tokens of this slice (counts via LDS, applied in registers)
+    const int seen = P.hist_count[b];
+    const int win = min(min(seen, P.repeat_last_n[b]), P.hist_cap);
+    const float rp = P.repeat_penalty[b], pp = P.presence_penalty[b], fp = P.frequency_penalty[b];
+    if (win > 0 && (rp != 1.f || pp != 0.f || fp != 0.f)) {
+      pen_cnt[tid] = 0;
+      __syncthreads();
+      const int* h = P.history + (long long)b * P.hist_cap;
+      for (int i = tid; i < win; i += SAMPLE_NT) {
+        const int tok = h[(seen - 1 - i) % P.hist_cap] - blk * FAST_SLICE;
+        if (tok >= 0 && tok < FAST_SLICE) atomicAdd(&pen_cnt[tok], 1);
+      }
+      __syncthreads();
+      const int cnt = pen_cnt[tid];
+      if (cnt > 0 && ix < V) {
+        if (rp != 1.f) v = v > 0.f ? v / rp : v * rp;
+        v -= (float)cnt * fp + pp;
+      }
+    }
+    float rv = v;
+    int ri = ix < V ? ix : 0x7FFFFFFF;
+    wave_bitonic_sort(rv, ri, true);
+    // block tree merge of the 16 wave lists
+    lv[wave][lane] = rv;
+    li[wave][lane] = ri;
+    for (int st = 1; st < SAMPLE_NT / 64; st <<= 1) {
+      __syncthreads();
+      if ((wave & (2 * st - 1)) == 0) {
+        wave_merge_desc(rv, ri, lv[wave + st], li[wave + st]);
+        lv[wave][lane] = rv;
+        li[wave][lane] = ri;
+      }
+    }
+    if (wave == 0) {  // sc1 stores of the block list; drained before the ticket
+      float* wsv = P.ws + ((long long)b * G + blk) * 2 * FAST_K;
+      __hip_atomic_store(wsv + lane, rv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store((int*)wsv + FAST_K + lane, ri, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    int* cnt = P.counters + b;
+    const int old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = old == G - 1;
+    if (last) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+    s_last = last;
+  }
+  __syncthreads();
+  if (!s_last) return;
+
+  if (!fast) {  // top_k outside 1..64: the whole row in this block, as sample_kernel
+    float* lgw = (float*)P.logits + (long long)b * P.ld;
+    apply_penalties_inplace(P, b, lgw, V);
+    int chosen;
+    float chosen_lp;
+    legacy_select(P, b, lgw, V, chosen, chosen_lp);
+    if (tid == 0) finish_sample(P, b, chosen, chosen_lp);
+    return;
+  }
+  // ---- merge every block's list (sc1 loads), tree over the waves
+  auto ldf = [](const float* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+  auto ldi = [](const int* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+  float rv = -INFINITY;
+  int ri = 0x7FFFFFFF;
+  for (int l = wave; l < G; l += SAMPLE_NT / 64) {
+    const float* wsv = P.ws + ((long long)b * G + l) * 2 * FAST_K;
+    const float cv = ldf(wsv + 63 - lane);
+    const int ci = ldi((const int*)wsv + FAST_K + 63 - lane);
+    wave_merge_asc(rv, ri, cv, ci);
+  }
+  __syncthreads();  // lv / li reuse
+  lv[wave][lane] = rv;
+  li[wave][lane] = ri;
+  for (int st = 1; st < SAMPLE_NT / 64; st <<= 1) {
+    __syncthreads();
+    if ((wave & (2 * st - 1)) == 0) {
+      wave_merge_desc(rv, ri, lv[wave + st], li[wave + st]);
+      lv[wave][lane] = rv;
+      li[wave][lane] = ri;
+    }
+  }
+  if (wave != 0) return;
+  // ---- wave 0: candidates sorted (lane = rank); top-p -> min-p -> temperature -> draw
+  int chosen = __shfl(ri, 0, 64);
+  float chosen_lp = 0.f;
+  if (temp > 0.f) {
+    const int n = min(kk, V);
+    const float top = __shfl(rv, 0, 64);
+    const bool in = lane < n;
+    const float e1 = in ? __expf(rv - top) : 0.f;
+    const float z = wave_sum(e1);
+    int keep = n;
+    const float topp = P.top_p[b], minp = P.min_p[b];
+    if (topp < 1.f) {
+      float c = e1 / z;  // inclusive prefix sum over ranks
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const float t = __shfl_up(c, o, 64);
+        if (lane >= o) c += t;
+      }
+      const unsigned long long hit = __ballot(in && c >= topp);
+      if (hit) keep = __ffsll((long long)hit);  // first rank reaching top_p, inclusive
+    }
+    if (minp > 0.f) {
+      const unsigned long long fail = __ballot(lane >= 1 && lane < keep && e1 < minp);
+      if (fail) keep = __ffsll((long long)fail) - 1;
+    }
+    const float wt = lane < keep ? __expf((rv - top) / temp) : 0.f;
+    const float zt = wave_sum(wt);
+    float c = wt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const float t = __shfl_up(c, o, 64);
+      if (lane >= o) c += t;
+    }
+    const unsigned long long r = splitmix64(P.seed[b] ^ (0xD1B54A32D192ED03ull * (unsigned long long)(P.step[b] + 1)));
+    const float u = (float)(r >> 40) * (1.0f / 16777216.0f) * zt;
+    const unsigned long long hit = __ballot(lane < keep && u < c);
+    const int pick = hit ? __ffsll((long long)hit) - 1 : keep - 1;
+    chosen = __shfl(ri, pick, 64);
+    chosen_lp = (__shfl(rv, pick, 64) - top) / temp - __logf(zt);
+  }
+  if (lane == 0) finish_sample(P, b, chosen, chosen_lp);
 }
 
 void sample(const SampleParams& P, hipStream_t s) {
   if (P.B <= 0) return;
+  if (P.ws && P.counters) {  // multi-block path (rows with top_k outside 1..64 fall back inside it)
+    const int G = (P.V + FAST_SLICE - 1) / FAST_SLICE;
+    hipLaunchKernelGGL(sample_fast_kernel, dim3(G, P.B), dim3(SAMPLE_NT), 0, s, P);
+    return;
+  }
   hipLaunchKernelGGL(sample_kernel, dim3(P.B), dim3(SAMPLE_NT), 0, s, P);
 }
 

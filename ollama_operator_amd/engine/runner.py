@@ -159,6 +159,10 @@ class Runner:
         self.s_hist = torch.zeros(max_batch, HIST_CAP, **i32)
         self.s_hcount = torch.zeros(max_batch, **i32)
         self.s_out = torch.zeros(max_batch, **i32)
+        # multi-block sampler: per-row candidate lists (ceil(V/1024) blocks x 64 x {value, index})
+        # and hand-off tickets (zeroed once; the kernel re-arms them)
+        self.s_ws = torch.zeros(max_batch, -(-cfg.n_vocab // 1024) * 128, **f32)
+        self.s_tickets = torch.zeros(max_batch, **i32)
         self.kv = PagedKV(n_blocks, block_size, max_seqs, self.max_blocks)
         self.exe = NativeExec(self) if self.is_gpu else TorchExecutor(self)
         if use_graphs is None:  # TP steps run Python-level collectives between executor stages
@@ -309,7 +313,8 @@ class Runner:
                                  repeat_penalty=p(self.s_rpen), presence_penalty=p(self.s_ppen),
                                  frequency_penalty=p(self.s_fpen), history=p(self.s_hist),
                                  hist_count=p(self.s_hcount), hist_cap=HIST_CAP, repeat_last_n=p(self.s_lastn),
-                                 seed=p(self.s_seed), step=p(self.s_step), out=p(self.s_out)), stream_handle())
+                                 seed=p(self.s_seed), step=p(self.s_step), out=p(self.s_out),
+                                 ws=p(self.s_ws), counters=p(self.s_tickets)), stream_handle())
         else:
             for b in range(B):
                 o, hist, seed, step = self._host_sampler[b]

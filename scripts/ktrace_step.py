@@ -18,7 +18,7 @@ def short(name: str) -> str:
 def main():
     rows = list(csv.DictReader(open(sys.argv[1])))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    idx = [i for i, r in enumerate(rows) if "sample_kernel" in r["Kernel_Name"]]
+    idx = [i for i, r in enumerate(rows) if re.search(r"sample(_fast)?_kernel", r["Kernel_Name"])]
     # steady-state decode steps: between consecutive sampler launches, skip the first few
     steps = list(zip(idx[4:-1], idx[5:]))[-16:]
     busy = collections.Counter()

@@ -251,10 +251,51 @@ def _sample_args(B, V, logits, **kw):
              seed=torch.tensor([kw.get("seed", 7)] * B, dtype=torch.int64), step=torch.zeros(B, dtype=torch.int32),
              history=torch.zeros(B, 64, dtype=torch.int32), hist_count=torch.zeros(B, dtype=torch.int32),
              out=torch.zeros(B, dtype=torch.int32))
+    if kw.get("fast"):
+        d["ws"] = torch.full((B, -(-V // 1024) * 128), float("nan"))
+        d["counters"] = torch.zeros(B, dtype=torch.int32)
     d = {k: v.cuda() for k, v in d.items()}
     ptrs = {k: v.data_ptr() for k, v in d.items()}
     ptrs.update(logits=logits.data_ptr(), B=B, V=V, ld=V, hist_cap=64)
     return d, ptrs
+
+
+@pytest.mark.parametrize("V", [32000, 50257, 1000])
+@pytest.mark.parametrize("top_k,top_p,min_p", [(40, 0.9, 0.0), (1, 1.0, 0.0), (64, 0.95, 0.05), (7, 1.0, 0.0),
+                                               (65, 0.9, 0.0), (0, 0.9, 0.0)])
+def test_sampling_multiblock_matches_host(V, top_k, top_p, min_p):
+    """The multi-block sampler (per-wave bitonic top-64, LDS tree, ticket hand-off; top_k outside
+    1..64 falls back to the single-block selection in the last block) against the host reference,
+    token for token: penalties with repeated history tokens, ties broken by the lower index, and
+    three consecutive calls on the same tickets."""
+    from ollama_operator_amd.engine.sampling import SamplingOptions, sample_host
+    B = 3
+    torch.manual_seed(V + top_k)
+    base = torch.randn(B, V, device="cuda") * 2
+    base[1] = torch.round(base[1] * 2) / 2  # heavy ties
+    hist = [[5, 17, 5, 900, 17, 5], [], [3, 3, 3, 999]]
+    o = SamplingOptions(temperature=0.7, top_k=top_k, top_p=top_p, min_p=min_p, repeat_penalty=1.3,
+                        presence_penalty=0.2, frequency_penalty=0.1, repeat_last_n=64)
+    for temperature in (0.7, 0.0):
+        lg = base.clone()
+        d, p = _sample_args(B, V, lg, fast=True, temperature=temperature, top_k=top_k, top_p=top_p, min_p=min_p,
+                            repeat_penalty=1.3, seed=11)
+        d["presence_penalty"].fill_(0.2)
+        d["frequency_penalty"].fill_(0.1)
+        for b in range(B):
+            d["history"][b, :len(hist[b])] = torch.tensor(hist[b], dtype=torch.int32) if hist[b] else 0
+            d["hist_count"][b] = len(hist[b])
+        o.temperature = temperature
+        hs = [list(h) for h in hist]
+        for step in range(3):
+            lg.copy_(base)
+            C().sample(p, S())
+            torch.cuda.synchronize()
+            for b in range(B):
+                want = sample_host(base[b].cpu().numpy(), hs[b], o, 11, step)
+                assert int(d["out"][b]) == want, (b, step, temperature)
+                hs[b].append(want)
+        assert int(d["counters"].abs().sum()) == 0  # tickets re-armed
 
 
 def test_sampling_greedy_and_seeded():
