@@ -115,6 +115,7 @@ PYBIND11_MODULE(_C, m) {
     P.row_offset = row_offset;
     P.n_sel = 1;
     if (qkv.contains("xws")) P.xws = Pp<void>(qkv["xws"].cast<uintptr_t>());  // enables the GEMM path
+    if (qkv.contains("dbg_ts")) P.dbg_ts = Pp<unsigned long long>(qkv["dbg_ts"].cast<uintptr_t>());
     if (qkv.contains("gws")) {  // split-K slabs for small-M GEMMs
       P.gws = Pp<float>(qkv["gws"].cast<uintptr_t>());
       P.gws_elems = qkv["gws_elems"].cast<long long>();
@@ -177,6 +178,8 @@ PYBIND11_MODULE(_C, m) {
      py::arg("scale"), py::arg("window"), py::arg("out"), py::arg("ldo"), py::arg("ws"), py::arg("n_splits"),
      py::arg("counters"), py::arg("stream"), py::arg("prefill") = 0);
   m.def("attention_ws_floats", &attention_ws_floats);
+  m.def("set_attn_tuning", &set_attn_tuning, py::arg("kps"));
+  m.def("gemv_merge_supported", &gemv_merge_supported);
   m.def("set_gemv_tuning", &set_gemv_tuning, py::arg("blocks_per_cu") = 0, py::arg("rows") = 0,
         py::arg("debug") = 0, py::arg("ks") = -1);
   m.def("embed_rows", [](py::object w, uintptr_t rows, int n, uintptr_t out, int ldo, uintptr_t stream) {
@@ -298,7 +301,10 @@ PYBIND11_MODULE(_C, m) {
         w.max_B = d["max_B"].cast<int>();
         w.n_splits = d["n_splits"].cast<int>();
       })
-      .def("set_splits", [](Executor& e, int n) { e.ws.n_splits = n; })
+      .def("set_splits", [](Executor& e, int n, int defer) {
+        e.ws.n_splits = n;
+        e.ws.defer = defer;
+      }, py::arg("n"), py::arg("defer") = 0)
       .def("run", [](Executor& e, const std::string& what, int layer, py::dict d, uintptr_t stream) {
         StepInputs in;
         auto ptr = [&](const char* k) -> uintptr_t { return d.contains(k) ? d[k].cast<uintptr_t>() : 0; };

@@ -25,7 +25,10 @@ namespace omx {
 constexpr int ATT_NW = 8;               // waves per block
 constexpr int ATT_NT = 64 * ATT_NW;
 constexpr int ATT_NG = 4 * ATT_NW;      // key groups (16 lanes each) per block
-constexpr int ATT_KPS = 256;            // target keys per split
+int g_attn_kps = 256;                   // target keys per split (runtime knob, set_attn_tuning)
+void set_attn_tuning(int kps) {
+  if (kps >= 16) g_attn_kps = kps;
+}
 constexpr int ATT_BTW = 1024;           // block-table entries staged in LDS per window
 
 template <int CTRL>
@@ -85,7 +88,9 @@ __global__ __launch_bounds__(ATT_NT) void attn_decode_kernel(AttnParams P) {
   const int len = P.q_len[qi];
   const int kstart = P.window > 0 ? max(0, len - P.window) : 0;
   const int nk = len - kstart;
-  const int S = max(1, min((int)gridDim.z, (nk + ATT_KPS - 1) / ATT_KPS));
+  // deferred merge: exactly gridDim.z splits (empty ones publish m = -inf, l = 0) and the consumer
+  // (the O-projection GEMV prologue) merges them; otherwise the split count follows the length
+  const int S = P.defer ? (int)gridDim.z : max(1, min((int)gridDim.z, (nk + P.kps - 1) / P.kps));
   if (split >= S) return;  // block-uniform: surplus splits of a short query leave immediately
   const int chunk = (nk + S - 1) / S;
   const int t0 = kstart + split * chunk;
@@ -228,7 +233,11 @@ __global__ __launch_bounds__(ATT_NT) void attn_decode_kernel(AttnParams P) {
       }
     }
     const int h = kvh * G + g;
-    if (S == 1) {
+    if (P.defer) {  // partial slabs [NQ][S][H*D] + [NQ][S][H]{m, l}; the kernel boundary publishes them
+      const long long row = (long long)qi * S + split;
+      P.ws[row * P.H * D + h * D + d] = A;
+      if (d == 0) *(f32x2*)(P.ws + (long long)P.NQ * S * P.H * D + (row * P.H + h) * 2) = (f32x2){M, L};
+    } else if (S == 1) {
       P.out[(long long)qi * P.ldo + h * D + d] = L > 0.f ? A / L : 0.f;
     } else {  // write-through (sc1) stores: the hand-off below then needs no release fence
       float* ws = P.ws + (((long long)qi * P.H + h) * gridDim.z + split) * (D + 2);
@@ -239,7 +248,7 @@ __global__ __launch_bounds__(ATT_NT) void attn_decode_kernel(AttnParams P) {
       }
     }
   }
-  if (S == 1) return;
+  if (S == 1 || P.defer) return;
   // ---- in-launch split combine (cdna_hip_programming.md §6 Guideline 16 / MI355X_MICROARCH.md
   // "Valid forms" row 1): partials were stored sc1; every wave drains them (vmcnt(0)), the block
   // barriers, one lane takes an agent-scope ticket. The block drawing the last of S tickets reads
@@ -472,8 +481,10 @@ static void launch_d(const AttnParams& P, hipStream_t s) {
   }
 }
 
-void attention_decode(const AttnParams& P, hipStream_t s) {
-  if (P.NQ <= 0) return;
+void attention_decode(const AttnParams& P0, hipStream_t s) {
+  if (P0.NQ <= 0) return;
+  AttnParams P = P0;
+  if (P.kps <= 0) P.kps = g_attn_kps;
   if (P.prefill && P.NQ >= 16 && P.D % 16 == 0) {  // one sequence, contiguous positions: MFMA flash
     dim3 grid((P.NQ + PF_BQ - 1) / PF_BQ, P.H);
     switch (P.D) {

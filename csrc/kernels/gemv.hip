@@ -33,7 +33,6 @@
 
 namespace omx {
 
-typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int GEMV_NW = 4;  // waves per block (8-wave blocks measured slower: profiles/r1_pmc)
 constexpr int GEMV_NT = 64 * GEMV_NW;
@@ -489,11 +488,19 @@ __global__ __launch_bounds__(GEMV_NT) void qgemv_kernel(GemvParams P) {
 // block per CU): the block has KS groups of GEMV_NW waves on the same rows, group kg owning the
 // super-block range [kg*CH, (kg+1)*CH); partial sums meet in LDS before the epilogue. More waves per
 // CU = more weight bytes in flight.
-template <int QT, int NSB, int R, int J, int NRM, int DBG = 0, int KS = 1>
-__global__ __launch_bounds__(GEMV_NT * KS) void qgemv_flight_kernel(GemvParams P) {
+// MRG > 0 (B == 1 decode, O projection): x holds MRG unmerged flash-decode partial slabs
+// (attention.hip `defer`); the prologue merges them per head in registers -- the merge rides on the
+// activation round trip this kernel pays anyway, instead of an in-launch ticket + re-read (~2.5 us).
+template <int QT, int NSB, int R, int J, int NRM, int DBG = 0, int KS = 1, int MRG = 0>
+__device__ __forceinline__ void flight_body(const GemvParams& P, const int bx, const int gxn) {
   constexpr int ROWS_B = GEMV_NW * 4 * R, NT = GEMV_NT * KS;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const QMat& w = P.w;
+  auto stamp = [&](int k) {
+    if (P.dbg_ts && threadIdx.x == 0)
+      P.dbg_ts[4 * ((long long)blockIdx.z * gxn + bx) + k] = __builtin_amdgcn_s_memrealtime();
+  };
+  stamp(0);
   const int K = w.K, N = w.N, SB = n_sb(K);
   const int XS = SB * XPAD;
   i32x4* lq = (i32x4*)smem;                           // [XS + 1]: slot XS is a dummy
@@ -517,27 +524,60 @@ __global__ __launch_bounds__(GEMV_NT * KS) void qgemv_flight_kernel(GemvParams P
   // 1. this thread's activation groups g = tid + NT i (i < NSB) and norm weights -> registers
   constexpr bool nrm = NRM != 0, lnb = NRM == 2;
   f32x4 xv[NSB][4], nw[NSB][4], nb[NSB][4];
+  constexpr int MS = MRG > 0 ? MRG : 1;
+  f32x4 av[MS][NSB][4];
+  f32x2 ml[MS][NSB];
   // unconditional loads from clamped addresses (a conditional load would make the compiler drain it
   // before the weight loads are issued); out-of-range values are masked at use
 #pragma unroll
   for (int i = 0; i < NSB; ++i) {
     const int gi = min(tid + NT * i, K / 16 - 1);
+    if constexpr (MRG > 0) {
+      const int h = 16 * gi / P.merge_D, nh = K / P.merge_D;
+#pragma unroll
+      for (int sp = 0; sp < MRG; ++sp) {
+        ml[sp][i] = *(const f32x2*)(P.merge_ml + 2 * (sp * nh + h));
+#pragma unroll
+        for (int j = 0; j < 4; ++j) av[sp][i][j] = *(const f32x4*)(x + (long long)sp * K + 16 * gi + 4 * j);
+      }
+    }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      xv[i][j] = *(const f32x4*)(x + 16 * gi + 4 * j);
+      if constexpr (MRG == 0) xv[i][j] = *(const f32x4*)(x + 16 * gi + 4 * j);
       if constexpr (nrm) nw[i][j] = *(const f32x4*)(P.norm_w + 16 * gi + 4 * j);
       if constexpr (lnb) nb[i][j] = *(const f32x4*)(P.norm_b + 16 * gi + 4 * j);
     }
   }
   __builtin_amdgcn_sched_barrier(0);  // activations ahead of the weights
+  if constexpr ((DBG & 4) != 0) __builtin_amdgcn_s_barrier();  // every wave's x requests queued first
   // 2. every weight tile of this block in flight (surplus slots re-read the last tile, unused)
   WTile<QT, NSB, R> T[J];
 #pragma unroll
   for (int j = 0; j < J; ++j) {
-    const int t = min((int)blockIdx.x + j * (int)gridDim.x, n_tiles - 1);
+    const int t = min(bx + j * gxn, n_tiles - 1);
     load_wtile<QT, NSB, R>(w, row_base, t * ROWS_B + rbase, N, SB, sb0, s, T[j], se);
   }
   __builtin_amdgcn_sched_barrier(0);  // every load issued before the prologue's first wait
+  if constexpr (MRG > 0) {  // flash-decode merge: splits without keys carry m = -inf, l = 0
+#pragma unroll
+    for (int i = 0; i < NSB; ++i) {
+      float M = -INFINITY;
+#pragma unroll
+      for (int sp = 0; sp < MRG; ++sp) M = fmaxf(M, ml[sp][i].x);
+      float L = 0.f;
+      f32x4 a[4] = {};
+#pragma unroll
+      for (int sp = 0; sp < MRG; ++sp) {
+        const float c = ml[sp][i].x == -INFINITY ? 0.f : __expf(ml[sp][i].x - M);
+        L += c * ml[sp][i].y;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) a[j] += c * av[sp][i][j];
+      }
+      const float inv = L > 0.f ? 1.f / L : 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) xv[i][j] = a[j] * inv;
+    }
+  }
   // 3. norm statistics + quantisation from registers while the weights stream
 #pragma unroll
   for (int i = 0; i < NSB; ++i) {
@@ -609,6 +649,7 @@ __global__ __launch_bounds__(GEMV_NT * KS) void qgemv_flight_kernel(GemvParams P
     lf[slot] = (f32x2){d, d * (float)qsum};
   }
   __syncthreads();
+  stamp(1);
   if constexpr (KS > 1) {  // one tile per block: groups 1.. hand their partial sums to group 0
     static_assert(J == 1, "in-block K split is for single-tile blocks");
     float acc[R][1];
@@ -624,25 +665,27 @@ __global__ __launch_bounds__(GEMV_NT * KS) void qgemv_flight_kernel(GemvParams P
     } else {
       compute_wtile<QT, NSB, R, 1>(T[0], SB, sb0, s, lq, lf, XS, acc, se);
     }
+    stamp(2);
     float* part = red + NT / 64;  // [KS-1][R][GEMV_NT]
     if (kg > 0) {
 #pragma unroll
       for (int r = 0; r < R; ++r) part[((kg - 1) * R + r) * GEMV_NT + gtid] = acc[r][0];
     }
     __syncthreads();
-    if (kg == 0 && (int)blockIdx.x < n_tiles) {
+    if (kg == 0 && bx < n_tiles) {
 #pragma unroll
       for (int k = 1; k < KS; ++k)
 #pragma unroll
         for (int r = 0; r < R; ++r) acc[r][0] += part[((k - 1) * R + r) * GEMV_NT + gtid];
-      finish_rows<R, 1>(P, acc, (int)blockIdx.x * ROWS_B + rbase, N, 0, s);
+      finish_rows<R, 1>(P, acc, bx * ROWS_B + rbase, N, 0, s);
     }
+    stamp(3);
     return;
   }
   // 4. consume the tiles in issue order
 #pragma unroll
   for (int j = 0; j < J; ++j) {
-    const int t = (int)blockIdx.x + j * (int)gridDim.x;
+    const int t = bx + j * gxn;
     if (t >= n_tiles) break;  // block-uniform
     float acc[R][1];
 #pragma unroll
@@ -660,8 +703,24 @@ __global__ __launch_bounds__(GEMV_NT * KS) void qgemv_flight_kernel(GemvParams P
     } else {
       compute_wtile<QT, NSB, R, 1>(T[j], SB, 0, s, lq, lf, XS, acc);
     }
+    if (j == 0) stamp(2);
     finish_rows<R, 1>(P, acc, t * ROWS_B + rbase, N, 0, s);
   }
+  stamp(3);
+}
+
+template <int QT, int NSB, int R, int J, int NRM, int DBG = 0, int KS = 1, int MRG = 0>
+__global__ __launch_bounds__(GEMV_NT * KS) void qgemv_flight_kernel(GemvParams P) {
+  flight_body<QT, NSB, R, J, NRM, DBG, KS, MRG>(P, blockIdx.x, gridDim.x);
+}
+
+// two matrices that read the same normalised x in ONE launch (Q4_K_M QKV: q,k rows Q4_K + v rows
+// Q6_K): blocks [0, gxa) run A, the rest B -- one launch ramp / drain instead of two (v alone was
+// 6.3 us for 13.8 MB, rocprofv3 profiles/r1_defer)
+template <int QA, int QB, int NSB, int NRM>
+__global__ __launch_bounds__(GEMV_NT) void qgemv_flight_dual_kernel(GemvParams PA, GemvParams PB, int gxa) {
+  if ((int)blockIdx.x < gxa) flight_body<QA, NSB, 1, 1, NRM>(PA, blockIdx.x, gxa);
+  else flight_body<QB, NSB, 1, 1, NRM>(PB, (int)blockIdx.x - gxa, (int)gridDim.x - gxa);
 }
 
 // register tiles a block keeps in flight: ~150 VGPRs of weight tiles per lane
@@ -695,11 +754,21 @@ template <int QT, int NSB, int R, int J, int NRM>
 static void launch_flight_n(const GemvParams& P, int gx, hipStream_t s) {
   const int bz = P.expert_ids ? P.n_sel : 1;
   const size_t lds = lds_bytes(P.w.K, 1);
+  if constexpr (NSB == 1 && R == 1 && NRM == 0) {
+    switch (P.merge_S) {  // deferred flash-decode merge in the prologue (O projection)
+      case 0: break;
+      case 2: hipLaunchKernelGGL((qgemv_flight_kernel<QT, NSB, R, J, NRM, 0, 1, 2>), dim3(gx, 1, bz), dim3(GEMV_NT), lds, s, P); return;
+      case 4: hipLaunchKernelGGL((qgemv_flight_kernel<QT, NSB, R, J, NRM, 0, 1, 4>), dim3(gx, 1, bz), dim3(GEMV_NT), lds, s, P); return;
+      case 8: hipLaunchKernelGGL((qgemv_flight_kernel<QT, NSB, R, J, NRM, 0, 1, 8>), dim3(gx, 1, bz), dim3(GEMV_NT), lds, s, P); return;
+      default: return;  // rejected by gemv() before launch
+    }
+  }
   if constexpr (R == 1 && (QT == QT_Q4_K || QT == QT_Q6_K) && (NSB == 1 || NSB == 3) && NRM < 2) {
     switch (g_tune.debug) {  // microbenchmark-only variants (scripts/bench_gemv.py OMX_BENCH_DEBUG)
       case 1: hipLaunchKernelGGL((qgemv_flight_kernel<QT, NSB, R, J, NRM, 1>), dim3(gx, 1, bz), dim3(GEMV_NT), lds, s, P); return;
       case 2: hipLaunchKernelGGL((qgemv_flight_kernel<QT, NSB, R, J, NRM, 2>), dim3(gx, 1, bz), dim3(GEMV_NT), lds, s, P); return;
       case 3: hipLaunchKernelGGL((qgemv_flight_kernel<QT, NSB, R, J, NRM, 3>), dim3(gx, 1, bz), dim3(GEMV_NT), lds, s, P); return;
+      case 4: hipLaunchKernelGGL((qgemv_flight_kernel<QT, NSB, R, J, NRM, 4>), dim3(gx, 1, bz), dim3(GEMV_NT), lds, s, P); return;
       default: break;
     }
   }
@@ -715,6 +784,7 @@ static void launch_flight_ks_n(const GemvParams& P, int gx, hipStream_t s) {
       case 1: hipLaunchKernelGGL((qgemv_flight_kernel<QT, NSB, 1, 1, NRM, 1, KS>), dim3(gx, 1, bz), dim3(GEMV_NT * KS), lds, s, P); return;
       case 2: hipLaunchKernelGGL((qgemv_flight_kernel<QT, NSB, 1, 1, NRM, 2, KS>), dim3(gx, 1, bz), dim3(GEMV_NT * KS), lds, s, P); return;
       case 3: hipLaunchKernelGGL((qgemv_flight_kernel<QT, NSB, 1, 1, NRM, 3, KS>), dim3(gx, 1, bz), dim3(GEMV_NT * KS), lds, s, P); return;
+      case 4: hipLaunchKernelGGL((qgemv_flight_kernel<QT, NSB, 1, 1, NRM, 4, KS>), dim3(gx, 1, bz), dim3(GEMV_NT * KS), lds, s, P); return;
       default: break;
     }
   }
@@ -795,6 +865,10 @@ static void launch_nsb(const GemvParams& P, hipStream_t s) {
 
 template <int QT>
 static void launch_q(const GemvParams& P, hipStream_t s) {
+  if (P.merge_S > 0) {  // only the single-chunk B == 1 flight kernel merges (merge_supported())
+    launch_flight<QT, 1, 1>(P, s);
+    return;
+  }
   if (P.B == 1 || P.expert_ids != nullptr) {  // decode (and MoE: experts differ per batch row)
     const int need = ((P.w.K + 255) / 256 + 15) / 16;
     if (P.B == 1 && need <= 4) {  // whole K in one chunk: all-in-flight kernel
@@ -818,7 +892,60 @@ static void launch_q(const GemvParams& P, hipStream_t s) {
   else launch_nsb<QT, 1, 1>(P, s);
 }
 
+template <int QA, int QB, int NSB>
+static void launch_dual_n(const GemvParams& A, const GemvParams& Bp, hipStream_t s) {
+  const int ta = (A.w.N + 4 * GEMV_NW - 1) / (4 * GEMV_NW), tb = (Bp.w.N + 4 * GEMV_NW - 1) / (4 * GEMV_NW);
+  hipLaunchKernelGGL((qgemv_flight_dual_kernel<QA, QB, NSB, 1>), dim3(ta + tb), dim3(GEMV_NT), lds_bytes(A.w.K, 1),
+                     s, A, Bp, ta);
+}
+
+template <int QA, int QB>
+static void launch_dual_q(const GemvParams& A, const GemvParams& Bp, int need, hipStream_t s) {
+  if (need == 1) launch_dual_n<QA, QB, 1>(A, Bp, s);
+  else launch_dual_n<QA, QB, 2>(A, Bp, s);
+}
+
+template <int QA>
+static bool launch_dual_a(const GemvParams& A, const GemvParams& Bp, int need, hipStream_t s) {
+  switch (Bp.w.qtype) {
+    case QT_Q4_K: if (QA != QT_Q4_K) { launch_dual_q<QA, QT_Q4_K>(A, Bp, need, s); return true; } break;
+    case QT_Q6_K: if (QA != QT_Q6_K) { launch_dual_q<QA, QT_Q6_K>(A, Bp, need, s); return true; } break;
+    case QT_Q4_0: if (QA != QT_Q4_0) { launch_dual_q<QA, QT_Q4_0>(A, Bp, need, s); return true; } break;
+    case QT_Q8_0: if (QA != QT_Q8_0) { launch_dual_q<QA, QT_Q8_0>(A, Bp, need, s); return true; } break;
+    default: break;
+  }
+  return false;
+}
+
+void gemv2(const GemvParams& A, const GemvParams& Bp, hipStream_t s) {
+  const int need = ((A.w.K + 255) / 256 + 15) / 16;
+  const bool ok = A.B == 1 && Bp.B == 1 && A.w.K == Bp.w.K && need <= 2 && A.norm == NORM_RMS &&
+                  Bp.norm == NORM_RMS && !A.expert_ids && !Bp.expert_ids && !A.merge_S && !Bp.merge_S &&
+                  A.x == Bp.x && g_tune.debug == 0;
+  if (ok) {
+    bool done = false;
+    switch (A.w.qtype) {
+      case QT_Q4_K: done = launch_dual_a<QT_Q4_K>(A, Bp, need, s); break;
+      case QT_Q6_K: done = launch_dual_a<QT_Q6_K>(A, Bp, need, s); break;
+      case QT_Q4_0: done = launch_dual_a<QT_Q4_0>(A, Bp, need, s); break;
+      case QT_Q8_0: done = launch_dual_a<QT_Q8_0>(A, Bp, need, s); break;
+      default: break;
+    }
+    if (done) return;
+  }
+  gemv(A, s);
+  gemv(Bp, s);
+}
+
+bool gemv_merge_supported(int B, int K, int D, int S) {
+  return B == 1 && K <= 4096 && D % 16 == 0 && K % D == 0 && (S == 2 || S == 4 || S == 8);
+}
+
 void gemv(const GemvParams& P, hipStream_t s) {
+  if (P.merge_S > 0) {
+    // flight grid for K <= 4096 is one chunk, R = 1, no K split: the merge variant covers exactly it
+    if (!gemv_merge_supported(P.B, P.w.K, P.merge_D, P.merge_S) || P.norm != NORM_NONE || P.expert_ids) return;
+  }
   if (gemm_eligible(P)) {
     gemm(P, s);
     return;

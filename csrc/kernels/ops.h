@@ -54,11 +54,22 @@ struct GemvParams {
   int moe_max_tiles;
   int moe_gather;              // x row of sorted position pos = moe_rows[pos] / n_sel (else pos)
   int moe_scatter;             // output row of pos = token (EPI_ADD, weighted, atomic) (else pos)
+  // deferred attention merge (B == 1 decode): x = acc slabs [merge_S][K], merge_ml = [merge_S][K/D]{m, l};
+  // the activation prologue computes x[k] = sum_s e^(m_s - M) acc_s[k] / sum_s e^(m_s - M) l_s
+  int merge_S;                 // 0 = x is the activation itself
+  const float* merge_ml;
+  int merge_D;                 // head dim (elements per {m, l} pair)
+  // timeline probe (scripts/gemv_timeline.py): per block 4 x s_memrealtime (100 MHz) at entry,
+  // prologue done, first tile computed, exit; null in production
+  unsigned long long* dbg_ts;
 };
 
 // y = epi(W x): the quantised GEMV for small B (decode), the MFMA dequant GEMM for B >= GEMM_MIN_B
 // when an fp16 activation workspace is given (prefill); same epilogues either way.
 void gemv(const GemvParams& P, hipStream_t s);
+bool gemv_merge_supported(int B, int K, int D, int S);
+// two GEMVs over the same x (same K, RMS norm prologue) in one launch when B == 1, else two launches
+void gemv2(const GemvParams& A, const GemvParams& B, hipStream_t s);
 constexpr int GEMM_MIN_B = 16;
 bool gemm_eligible(const GemvParams& P);
 void gemm(const GemvParams& P, hipStream_t s);
@@ -95,9 +106,14 @@ struct AttnParams {
   int n_splits;                // <= 64
   int* counters;               // [NQ][n_kv] arrival tickets, zero before first use (self re-arming)
   int prefill;                 // all NQ queries: one sequence, contiguous positions (MFMA flash path)
+  int kps;                     // target keys per split (0 -> g_attn_kps)
+  int defer;                   // write exactly n_splits unmerged partials (attention_ws_floats layout
+                               // [NQ][S][H*D] then [NQ][S][H][2] {m, l}); the consumer merges them
 };
 void attention_decode(const AttnParams& P, hipStream_t s);
 size_t attention_ws_floats(int NQ, int H, int D, int n_splits);
+extern int g_attn_kps;  // decode keys per flash-decode split (scripts/bench_attn.py sweep)
+void set_attn_tuning(int kps);
 
 struct SampleParams {
   const float* logits;         // [B][V] (modified in place by penalties)

@@ -48,12 +48,13 @@ void Executor::attn_block(int i, const StepInputs& in, hipStream_t s) {
   P.n_rot = cfg.n_rot;
   P.n_kv = cfg.Hkv;
   P.bs = in.bs;
-  gemv(P, s);
-  if (!L.qkv_fused) {
+  if (!L.qkv_fused) {  // q,k and v rows of different quant types: one dual launch at B == 1
     GemvParams V = P;
     V.w = L.wv;
     V.row_offset = Eq + Ekv;
-    gemv(V, s);
+    gemv2(P, V, s);
+  } else {
+    gemv(P, s);
   }
   if (phi) {  // parallel block: FFN up reads the same normed input, before O touches resid
     GemvParams U = base_params(L.wgu, B, ws.resid, E, ws);
@@ -90,9 +91,19 @@ void Executor::attn_block(int i, const StepInputs& in, hipStream_t s) {
   A.n_splits = ws.n_splits;
   A.counters = ws.attn_cnt;
   A.prefill = in.prefill;
+  // deferred split merge (B == 1): the O projection's prologue merges the partial slabs
+  const bool defer = ws.defer && B == 1 && ws.n_splits > 1;
+  if (defer && !gemv_merge_supported(B, Eq, cfg.D, ws.n_splits))
+    throw std::runtime_error("deferred attention merge: unsupported (K, D, splits)");
+  A.defer = defer;
   attention_decode(A, s);
   // --- output projection (+ residual, or partial sum under TP)
-  GemvParams O = base_params(L.wo, B, ws.abuf, Eq, ws);
+  GemvParams O = base_params(L.wo, B, defer ? ws.attn_ws : ws.abuf, Eq, ws);
+  if (defer) {
+    O.merge_S = ws.n_splits;
+    O.merge_ml = ws.attn_ws + (size_t)ws.n_splits * Eq;
+    O.merge_D = cfg.D;
+  }
   O.bias = L.bo;
   if (cfg.tp > 1) {
     O.epi = EPI_STORE;

@@ -62,6 +62,7 @@ struct Workspace {
   long long gws_elems = 0;
   int max_B = 0;
   int n_splits = 1;
+  int defer = 0;             // B == 1: attention leaves n_splits partials, the O GEMV merges them
 };
 
 struct StepInputs {

@@ -74,7 +74,8 @@ class NativeExec:
         d["prefill"] = int(prefill)
         d["n_logits"] = n_logits
         d["logit_idx"] = self.logit_idx_ptr if use_idx else 0
-        self.exe.set_splits(self.r.n_splits(B))
+        S, defer = self.r.split_plan(B)
+        self.exe.set_splits(S, defer)
         self.exe.run(stage, layer, d, stream_handle())
 
 
@@ -164,6 +165,12 @@ class Runner:
         self.s_ws = torch.zeros(max_batch, -(-cfg.n_vocab // 1024) * 128, **f32)
         self.s_tickets = torch.zeros(max_batch, **i32)
         self.kv = PagedKV(n_blocks, block_size, max_seqs, self.max_blocks)
+        # deferred flash-decode merge (B == 1): attention leaves S <= 8 partial slabs, the O GEMV
+        # merges them in its activation prologue (no in-launch ticket + re-read)
+        self.defer_kps = int(os.environ.get("OMX_DEFER_KPS", "128"))
+        self._defer_ok = (self.is_gpu and os.environ.get("OMX_DEFER_MERGE", "1") != "0" and
+                          native().gemv_merge_supported(1, Eq, loc["D"], 8) and self.n_splits(1) >= 8)
+        self._decode_S = 0
         self.exe = NativeExec(self) if self.is_gpu else TorchExecutor(self)
         if use_graphs is None:  # TP steps run Python-level collectives between executor stages
             use_graphs = self.is_gpu and tp_size == 1 and os.environ.get("OMX_NO_GRAPH", "0") != "1"
@@ -182,6 +189,25 @@ class Runner:
     def n_splits(self, B: int) -> int:
         hkv = self.w.local["Hkv"]
         return max(1, min(32, 512 // max(1, B * hkv)))
+
+    def split_plan(self, B: int) -> tuple[int, int]:
+        """(splits, deferred) for the next launch sequence. B == 1 decode uses the length bucket set
+        by `decode_step` (`_decode_S`): S partial slabs merged in the O GEMV prologue; everything
+        else keeps the on-device split rule with the in-launch merge."""
+        S = self._decode_S if B == 1 else 0
+        if S:
+            return S, int(S > 1)
+        return self.n_splits(B), 0
+
+    def decode_splits(self, length: int) -> int:
+        """Flash-decode split bucket for a B == 1 step over `length` visible keys: 1 / 2 / 4 / 8
+        deferred splits of >= DEFER_KPS keys, 0 (= on-device rule, in-launch merge) beyond."""
+        if not self._defer_ok:
+            return 0
+        S = 1
+        while S < 8 and length > S * self.defer_kps:
+            S *= 2
+        return S if length <= S * self.defer_kps else 0
 
     def _ws_floats(self, B: int) -> int:
         loc = self.w.local
@@ -330,7 +356,8 @@ class Runner:
         self.d_tokens[:B].copy_(self.s_out[:B])
 
     def _graph(self, B: int):
-        g = self.graphs.get(B)
+        key = (B, self._decode_S)
+        g = self.graphs.get(key)
         if g is None:
             s = torch.cuda.Stream()
             s.wait_stream(torch.cuda.current_stream())
@@ -341,7 +368,7 @@ class Runner:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 self._decode_body(B)
-            self.graphs[B] = g
+            self.graphs[key] = g
         return g
 
     def warmup(self) -> None:
@@ -357,7 +384,11 @@ class Runner:
         finally:
             self.free_sequence(sid)
         if self.use_graphs:
-            self._graph(1)
+            buckets = sorted({self.decode_splits(n) for n in range(1, self.ctx + 1)})
+            for S in buckets:  # one decode graph per split bucket reachable at this context size
+                self._decode_S = S
+                self._graph(1)
+            self._decode_S = 0
         torch.cuda.synchronize()
 
     def decode_step(self, sid: int, pos: int | None = None) -> None:
@@ -370,11 +401,15 @@ class Runner:
             self._sync_block_table(sid)
         arr = np.array([[pos], [self.kv.slot(sid, pos)], [pos + 1], [s.row], [0]], np.int32)
         self._upload(arr, None)
-        with trace_range("decode"):
-            if self.use_graphs:
-                self._graph(1).replay()
-            else:
-                self._decode_body(1)
+        self._decode_S = self.decode_splits(pos + 1)
+        try:
+            with trace_range("decode"):
+                if self.use_graphs:
+                    self._graph(1).replay()
+                else:
+                    self._decode_body(1)
+        finally:
+            self._decode_S = 0
 
     def _generate_pipelined(self, sid: int, st, first: int, max_tokens: int, stop, times, t1) -> Iterator[int]:
         """Two decode steps in flight: step i consumes token i+1 straight from device memory (written

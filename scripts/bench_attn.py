@@ -27,6 +27,56 @@ def timeit(fn, n=200):
     return e0.elapsed_time(e1) * 1e3 / n
 
 
+def timeit_graph(fn, n=50, reps=20):
+    """Device time per call: n calls captured in one hipGraph, replayed (no host launch cost)."""
+    st = torch.cuda.Stream()
+    st.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(st):
+        for _ in range(3):
+            fn(st.cuda_stream)
+    torch.cuda.current_stream().wait_stream(st)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        s = torch.cuda.current_stream().cuda_stream
+        for _ in range(n):
+            fn(s)
+    g.replay()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        g.replay()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) * 1e3 / (n * reps)
+
+
+def attn_kps_sweep(C):
+    """Graph-timed decode attention vs keys-per-split (the on-device split rule) at serving lengths."""
+    bs = 16
+    for H, Hkv, D in ((32, 32, 128), (32, 8, 128)):
+        for L in (128, 464, 1024, 2048, 4096):
+            nblk = (L + bs - 1) // bs
+            kc = torch.randn(nblk, Hkv, bs, D, device="cuda").half()
+            vc = torch.randn(nblk, Hkv, bs, D, device="cuda").half()
+            bt = torch.arange(nblk, device="cuda", dtype=torch.int32)
+            qlen = torch.tensor([L], device="cuda", dtype=torch.int32)
+            q = torch.randn(1, H * D, device="cuda")
+            out = torch.empty(1, H * D, device="cuda")
+            S = max(1, min(32, 512 // Hkv))
+            ws = torch.empty(max(1, C.attention_ws_floats(1, H, D, S)), device="cuda")
+            cnt = torch.zeros(Hkv, device="cuda", dtype=torch.int32)
+            row = []
+            for kps in (32, 64, 128, 256):
+                C.set_attn_tuning(kps)
+                fn = lambda st: C.attention(q.data_ptr(), H * D, kc.data_ptr(), vc.data_ptr(), bt.data_ptr(), nblk,  # noqa
+                                            0, qlen.data_ptr(), 1, H, Hkv, D, bs, D ** -0.5, 0, out.data_ptr(), H * D,
+                                            ws.data_ptr(), S, cnt.data_ptr(), st)
+                row.append(f"kps={kps}:{timeit_graph(fn):6.2f}")
+            print(f"attn(graph) H={H} Hkv={Hkv} L={L:5d} S<={S}  " + "  ".join(row) + "  (us)", flush=True)
+    C.set_attn_tuning(256)
+
+
 def attn_sweep(C, s):
     bs = 16
     for H, Hkv, D in ((32, 32, 128), (32, 8, 128)):
@@ -71,6 +121,9 @@ def gemv_fixed(C, s):
 def main():
     C = native()
     s = torch.cuda.current_stream().cuda_stream
+    if os.environ.get("OMX_BENCH_KPS"):
+        attn_kps_sweep(C)
+        return
     gemv_fixed(C, s)
     attn_sweep(C, s)
 

@@ -33,6 +33,8 @@ def make(qt, N, K):
     raw = random_blocks(qt, N, K, rng)
     st = repack(raw, qt, N, K)
     copies = max(2, (768 << 20) // raw.nbytes)
+    if os.environ.get("OMX_BENCH_HOT"):  # one copy re-read: MALL/L2-served (prefetch upper bound)
+        copies = 1
     tups, keep = [], []
     for _ in range(copies):
         ts = [torch.from_numpy(np.ascontiguousarray(st[n])).cuda() for n in STREAMS[qt]]

@@ -72,3 +72,41 @@ def test_prefill_gemm_path_vs_torch(tiny_models, name):
     g.prefill(sg, [5])  # then a decode-shaped step on the KV the GEMM path wrote
     c.prefill(sc, [5])
     assert rel(g.logits[0, :V].cpu(), c.logits[0, :V]) < 3e-2
+
+
+@pytest.mark.parametrize("name", ["tiny-llama", "tiny-phi2"])
+def test_deferred_split_merge_decode(tmp_path, monkeypatch, name):
+    """B == 1 decode at lengths in every split bucket: the deferred merge (attention leaves S partial
+    slabs, the O GEMV prologue merges them) must match the in-launch merge and the torch twin."""
+    from ollama_operator_amd.gguf.constants import FileType
+    from ollama_operator_amd.models.config import preset
+    from ollama_operator_amd.models.random_init import write_random_gguf
+    path = str(tmp_path / "long.gguf")
+    write_random_gguf(path, preset(name, ctx_len=2048), FileType.MOSTLY_Q4_K_M, seed=5, quantize_from_float=True)
+    g = Runner(path, device="cuda", max_batch=64, max_seqs=1, ctx=1100)
+    monkeypatch.setenv("OMX_DEFER_MERGE", "0")
+    g0 = Runner(path, device="cuda", max_batch=64, max_seqs=1, ctx=1100, weights=g.w)
+    assert g._defer_ok and not g0._defer_ok
+    c = Runner(path, device="cpu", max_batch=64, max_seqs=1, ctx=1100)
+    rng = np.random.default_rng(3)
+    V = g.cfg.n_vocab
+    seen = set()
+    for L in (100, 200, 400, 900, 1050):
+        toks = [1] + [int(x) for x in rng.integers(3, 500, L - 1)]
+        seen.add(g.decode_splits(L + 1))
+        outs = []
+        for r in (g, g0, c):
+            sid = r.new_sequence()
+            r.prefill(sid, toks)
+            if r.is_gpu:
+                r.d_tokens[0] = 77
+                r.decode_step(sid, L)
+                torch.cuda.synchronize()
+                outs.append(r.logits[0, :V].float().cpu().clone())
+            else:
+                r.prefill(sid, [77])
+                outs.append(r.logits[0, :V].clone())
+            r.free_sequence(sid)
+        assert rel(outs[0], outs[1]) < 2e-3, L
+        assert rel(outs[0], outs[2]) < 3e-2, L
+    assert seen == {1, 2, 4, 8, 0}
