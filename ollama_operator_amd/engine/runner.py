@@ -11,7 +11,6 @@ step behind, so the GPU never waits on Python.
 """
 from __future__ import annotations
 
-import math
 import os
 import time
 from dataclasses import dataclass
@@ -20,7 +19,7 @@ from typing import Callable, Iterator
 import numpy as np
 import torch
 
-from ..ops import has_native, native, stream_handle
+from ..ops import native, stream_handle
 from ..ops.reference import TorchExecutor
 from ..utils.trace import trace_range
 from .kv_cache import PagedKV

@@ -207,7 +207,23 @@ def write(outdir: str) -> list[str]:
     return written
 
 
-if __name__ == "__main__":
-    out = sys.argv[1] if len(sys.argv) > 1 else os.path.join(os.path.dirname(__file__), "..", "..", "deploy")
-    for p in write(out):
+def main(argv: list[str] | None = None) -> None:
+    """python -m ollama_operator_amd.operator.manifests [outdir] [--image IMG] [--server-image IMG]
+    (reference Makefile:117-121 build-installer: kustomize edit set image + kustomize build)."""
+    import argparse
+    global OPERATOR_IMAGE, SERVER_IMAGE
+    ap = argparse.ArgumentParser()
+    ap.add_argument("outdir", nargs="?", default=os.path.join(os.path.dirname(__file__), "..", "..", "deploy"))
+    ap.add_argument("--image", default=None, help="operator image for the manager Deployment")
+    ap.add_argument("--server-image", default=None, help="default model-server image (OMX_SERVER_IMAGE)")
+    a = ap.parse_args(argv)
+    if a.image:
+        OPERATOR_IMAGE = a.image
+    if a.server_image:
+        SERVER_IMAGE = a.server_image
+    for p in write(a.outdir):
         print(p)
+
+
+if __name__ == "__main__":
+    main()

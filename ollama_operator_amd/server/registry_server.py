@@ -11,7 +11,7 @@ import os
 import uuid
 
 from fastapi import FastAPI, Request, Response
-from fastapi.responses import FileResponse, JSONResponse, StreamingResponse
+from fastapi.responses import JSONResponse, StreamingResponse
 
 from .store import MT_MANIFEST, ModelName, ModelStore, StoreError
 
