@@ -42,6 +42,62 @@ def ensure_model(path: str, preset_name: str, ftype_name: str) -> str:
     return path
 
 
+def bench_batched(runner, a, rank, world, sync):
+    """Aggregate decode tokens/s with B = a.batch_extra sequences per GPU sharing every step (the
+    server's continuous batching, engine/scheduler.py): B prompts prefilled, then exactly a.steps batched
+    steps (each samples B tokens on device, Ollama-default options per row), two steps in flight."""
+    import torch
+    import torch.distributed as dist
+    from ollama_operator_amd.engine.sampling import SamplingOptions
+    B = a.batch_extra
+    runner.capture_batch_graphs(B)
+    g = torch.Generator().manual_seed(4321 + rank)
+    sids, poss, firsts, prompts = [], [], [], []
+    for b in range(B):
+        p = [1] + torch.randint(3, runner.cfg.n_vocab, (a.prompt - 1,), generator=g).tolist()
+        sid = runner.new_sequence()
+        runner.prefill(sid, p)
+        runner._set_sampler(0, SamplingOptions(seed=7 + b), p, 7 + b, 0)
+        runner._sample(1)
+        firsts.append(int(runner.s_out[0].item()))
+        sids.append(sid)
+        poss.append(len(p))
+        prompts.append(p)
+    for b in range(B):
+        runner._set_sampler(b, SamplingOptions(seed=7 + b), prompts[b] + [firsts[b]], 7 + b, 1)
+    runner.set_tokens(firsts)
+    ring = [torch.zeros(B, dtype=torch.int32).pin_memory() for _ in range(4)]
+    evs = []
+
+    def step(i):
+        runner.decode_batch(sids, poss)
+        for b in range(B):
+            poss[b] += 1
+        ring[i % 4].copy_(runner.s_out[:B], non_blocking=True)
+        e = torch.cuda.Event()
+        e.record()
+        evs.append(e)
+        if len(evs) > 2:  # two steps in flight, the host reads tokens one step behind
+            evs.pop(0).synchronize()
+
+    for i in range(a.warmup):
+        step(i)
+    sync()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        step(i)
+    sync()
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], device="cuda")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = float(t)
+    for sid in sids:
+        runner.free_sequence(sid)
+    return {"sequences_per_gpu": B, "tokens_per_s": round(world * B * a.steps / dt, 2),
+            "ms_per_step": round(dt / a.steps * 1e3, 4)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -51,6 +107,9 @@ def main():
     ap.add_argument("--model", default="llama2-7b")
     ap.add_argument("--ftype", default="Q4_K_M")
     ap.add_argument("--dir", default=os.environ.get("OMX_BENCH_DIR", "/tmp/omx_bench"))
+    ap.add_argument("--batch-extra", type=int, default=0,
+                    help="also measure continuous-batching throughput with this many concurrent sequences per "
+                         "GPU (Ollama OLLAMA_NUM_PARALLEL default 4; reported under extra, 0 = skip)")
     a = ap.parse_args()
 
     import torch
@@ -76,7 +135,7 @@ def main():
 
     ctx = a.prompt + a.warmup + a.steps + 64
     t_load = time.perf_counter()
-    runner = Runner(path, device=f"cuda:{local}", max_batch=512, max_seqs=1, ctx=ctx)
+    runner = Runner(path, device=f"cuda:{local}", max_batch=512, max_seqs=max(1, a.batch_extra), ctx=ctx)
     runner.warmup()  # load-time decode-graph capture, as the server does at model load
     torch.cuda.synchronize()
     load_s = time.perf_counter() - t_load
@@ -110,6 +169,11 @@ def main():
     dt = float(t)
     ms = dt / a.steps * 1e3
     value = world * a.steps / dt
+    gen.close()
+    runner.free_sequence(sid)
+    batched = None
+    if a.batch_extra > 1:
+        batched = bench_batched(runner, a, rank, world, sync)
     if rank == 0:
         print(json.dumps({
             "metric": "output tokens/sec Llama-2-7B Q4_K_M",
@@ -128,7 +192,8 @@ def main():
                        "parallelism": f"dp{world}", "prompt_tokens": a.prompt, "decode_batch_per_gpu": 1,
                        "sampling": "temperature 0.8, top_k 40, top_p 0.9, repeat_penalty 1.1 (on device)"},
             "extra": {"ttft_ms": round(ttft * 1e3, 2), "load_s": round(load_s, 2),
-                      "weights_gb": round(runner.w.nbytes / 1e9, 3)},
+                      "weights_gb": round(runner.w.nbytes / 1e9, 3),
+                      "continuous_batching": batched},
         }), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -106,6 +106,7 @@ class Runner:
         cfg = self.cfg = self.w.cfg
         loc = self.w.local
         self.max_batch = max_batch
+        self.max_seqs = max_seqs
         self.block_size = block_size
         self.ctx = min(ctx or cfg.ctx_len, cfg.ctx_len)
         self.max_blocks = (self.ctx + block_size - 1) // block_size
@@ -311,7 +312,7 @@ class Runner:
             self.free_sequence(sid)
 
     # ------------------------------------------------------------------ sampling
-    def _set_sampler(self, row: int, o: SamplingOptions, history: list[int], seed: int):
+    def _set_sampler(self, row: int, o: SamplingOptions, history: list[int], seed: int, step: int = 0):
         self.s_temp[row] = o.temperature
         self.s_topk[row] = o.top_k
         self.s_topp[row] = o.top_p
@@ -321,13 +322,13 @@ class Runner:
         self.s_fpen[row] = o.frequency_penalty
         self.s_lastn[row] = o.repeat_last_n
         self.s_seed[row] = seed - (1 << 64) if seed >= (1 << 63) else seed
-        self.s_step[row] = 0
+        self.s_step[row] = step  # RNG counter: draws already made for this request
         h = history[-HIST_CAP:]
         self.s_hist[row].zero_()
         if h:
             self.s_hist[row, :len(h)] = torch.tensor(h, dtype=torch.int32)
         self.s_hcount[row] = len(h)
-        self._host_sampler[row] = (o, list(history), seed, 0)
+        self._host_sampler[row] = (o, list(history), seed, step)
 
     def _sample(self, B: int):
         lg = self.full_logits
@@ -394,21 +395,41 @@ class Runner:
         """One token for sequence `sid` whose input token (not yet in `tokens`) is already in
         d_tokens[0] on device; it sits at position `pos` (default len(tokens))."""
         s = self.kv.seqs[sid]
-        pos = s.length if pos is None else pos
-        if pos + 1 > len(s.blocks) * self.block_size:
-            self.kv.reserve(sid, min(self.ctx, pos + 4 * self.block_size))
-            self._sync_block_table(sid)
-        arr = np.array([[pos], [self.kv.slot(sid, pos)], [pos + 1], [s.row], [0]], np.int32)
+        self.decode_batch([sid], [s.length if pos is None else pos])
+
+    def decode_batch(self, sids: list[int], poss: list[int]) -> None:
+        """One decode step for B = len(sids) sequences (continuous batching: engine/scheduler.py).
+        Row b's input token is d_tokens[b] on device and sits at position poss[b]; the step samples
+        row b with sampler row b and feeds the sampled tokens back into d_tokens[:B]."""
+        B = len(sids)
+        arr = np.empty((5, B), np.int32)
+        for b, (sid, pos) in enumerate(zip(sids, poss)):
+            s = self.kv.seqs[sid]
+            if pos + 1 > len(s.blocks) * self.block_size:
+                self.kv.reserve(sid, min(self.ctx, pos + 4 * self.block_size))
+                self._sync_block_table(sid)
+            arr[:, b] = (pos, self.kv.slot(sid, pos), pos + 1, s.row, b)
         self._upload(arr, None)
-        self._decode_S = self.decode_splits(pos + 1)
+        self._decode_S = self.decode_splits(poss[0] + 1) if B == 1 else 0
         try:
-            with trace_range("decode"):
+            with trace_range(f"decode B={B}"):
                 if self.use_graphs:
-                    self._graph(1).replay()
+                    self._graph(B).replay()
                 else:
-                    self._decode_body(1)
+                    self._decode_body(B)
         finally:
             self._decode_S = 0
+
+    def set_tokens(self, tokens: list[int]) -> None:
+        """Host -> d_tokens[:len(tokens)] (batch recomposition: rows' next inputs)."""
+        self._upload(np.zeros((5, 0), np.int32), np.asarray(tokens, np.int32))
+
+    def capture_batch_graphs(self, max_B: int) -> None:
+        """Load-time capture of the B = 2..max_B decode graphs (continuous batching)."""
+        if self.use_graphs:
+            for B in range(2, max_B + 1):
+                self._graph(B)
+            torch.cuda.synchronize()
 
     def _generate_pipelined(self, sid: int, st, first: int, max_tokens: int, stop, times, t1) -> Iterator[int]:
         """Two decode steps in flight: step i consumes token i+1 straight from device memory (written

@@ -1,0 +1,282 @@
+"""Continuous batching: several requests to one loaded model decode together, one batched step per token.
+
+Ollama serves `OLLAMA_NUM_PARALLEL` requests per model at once (its runner keeps that many "slots",
+each with its own KV cache and prefix reuse). The reference operator inherits that from the external
+`ollama/ollama` image (reference pkg/model/pod.go:10-12); here it is native: one scheduler thread per
+loaded model owns the `Runner` and
+
+* admits queued requests into free rows (up to `max_parallel`), reusing the idle sequence whose KV holds
+  the longest common prefix with the new prompt (multi-turn chats skip the shared history);
+* prefills the new prompt, samples its first token with the request's own sampler state;
+* runs batched decode steps for every active row (`Runner.decode_batch`: B rows through the batched
+  GEMV + paged GQA attention + per-row on-device sampling, one hipGraph per B), keeping two steps in
+  flight while the batch composition is stable -- the sampled tokens feed back on device, exactly as
+  the batch-1 pipelined path does -- and draining only when a request joins, finishes or is cancelled;
+* restores every row's sampler state (penalty history, seeded RNG counter) when rows are recomposed, so a
+  request's random draws do not depend on who else is in the batch.
+
+The same code drives the torch twin on CPU (tests), where steps are simply synchronous.
+"""
+from __future__ import annotations
+
+import collections
+import queue
+import threading
+import time
+from dataclasses import dataclass, field
+from typing import Callable, Iterator
+
+import torch
+
+from .runner import Runner, StepTimes
+from .sampling import SamplingOptions
+
+_DONE = object()
+
+
+@dataclass
+class _Req:
+    prompt: list[int]
+    opts: SamplingOptions
+    seed: int
+    max_tokens: int
+    times: StepTimes | None
+    out: "queue.Queue" = field(default_factory=queue.Queue)
+    cancelled: threading.Event = field(default_factory=threading.Event)
+    sid: int | None = None
+    history: list[int] = field(default_factory=list)  # prompt + sampled tokens (penalties)
+    n_sampled: int = 0          # RNG draws made (first token included)
+    pos: int = 0                # next position to issue (input token's position)
+    issued: int = 0             # decode steps issued (each yields one token)
+    delivered: int = 0          # tokens handed to the consumer
+    last_input: int = 0         # input token of the oldest unconsumed step
+    t_gen0: float = 0.0
+
+    def finished(self) -> bool:
+        return self.delivered >= self.max_tokens or self.cancelled.is_set()
+
+
+class BatchScheduler:
+    """Per-model continuous-batching loop (see module docstring)."""
+
+    def __init__(self, runner: Runner, max_parallel: int = 4, depth: int = 2):
+        if runner.tp_size > 1:
+            raise ValueError("continuous batching runs on single-rank runners (TP serving is serialised)")
+        self.r = runner
+        self.max_parallel = max(1, min(max_parallel, runner.max_batch, runner.max_seqs - 1))
+        self.depth = depth if runner.is_gpu else 1  # steps in flight
+        self.cv = threading.Condition()
+        self.pending: collections.deque[_Req] = collections.deque()
+        self.jobs: collections.deque = collections.deque()  # exclusive runner work (embeddings)
+        self.active: list[_Req] = []
+        self.idle: list[int] = []  # sequences kept for prefix reuse, most recent last
+        self.closed = False
+        self.steps = 0
+        self.max_batch_seen = 0
+        self._ring = None
+        self._thread = threading.Thread(target=self._loop, name="omx-batch", daemon=True)
+        self._thread.start()
+
+    # ------------------------------------------------------------------ public API
+    def submit(self, prompt: list[int], options: SamplingOptions | None = None, max_tokens: int = 128,
+               times: StepTimes | None = None) -> Iterator[int]:
+        """Queue a generation; yields its tokens as the batched steps produce them. Closing the
+        iterator early (stop string, client gone) cancels the request and frees its row."""
+        o = options or SamplingOptions()
+        req = _Req(prompt=list(prompt), opts=o, seed=o.resolved_seed(), max_tokens=max(0, max_tokens), times=times)
+        with self.cv:
+            if self.closed:
+                raise RuntimeError("scheduler closed")
+            self.pending.append(req)
+            self.cv.notify()
+        n, t1 = 0, None
+        try:
+            while True:
+                item = req.out.get()
+                if item is _DONE:
+                    return
+                if isinstance(item, BaseException):
+                    raise item
+                if t1 is None:  # eval timing as Runner.generate: from the first token on
+                    t1 = time.perf_counter()
+                n += 1
+                yield item
+        finally:
+            req.cancelled.set()
+            if times is not None:
+                times.gen_tokens = n
+                times.gen_s = time.perf_counter() - t1 if t1 is not None else 0.0
+            with self.cv:
+                self.cv.notify()
+
+    def run_exclusive(self, fn: Callable[[Runner], object]):
+        """Run fn(runner) on the scheduler thread between steps (embeddings share the runner)."""
+        box: queue.Queue = queue.Queue()
+        with self.cv:
+            self.jobs.append((fn, box))
+            self.cv.notify()
+        ok, val = box.get()
+        if not ok:
+            raise val
+        return val
+
+    @property
+    def busy(self) -> bool:
+        return bool(self.active or self.pending or self.jobs)
+
+    def close(self) -> None:
+        with self.cv:
+            self.closed = True
+            self.cv.notify()
+        self._thread.join(timeout=30)
+
+    # ------------------------------------------------------------------ scheduler thread
+    def _loop(self) -> None:
+        try:
+            while True:
+                with self.cv:
+                    while not (self.closed or self.pending or self.jobs or self.active):
+                        self.cv.wait()
+                    if self.closed:
+                        break
+                    jobs = list(self.jobs)
+                    self.jobs.clear()
+                for fn, box in jobs:
+                    try:
+                        box.put((True, fn(self.r)))
+                    except BaseException as e:  # noqa: BLE001 -- handed to the caller
+                        box.put((False, e))
+                self._admit()
+                if self.active:
+                    self._run_stable()
+        except BaseException as e:  # noqa: BLE001 -- fail every waiter loudly instead of hanging them
+            for req in list(self.active) + list(self.pending):
+                req.out.put(e)
+            raise
+        finally:
+            for req in list(self.active) + list(self.pending):
+                req.out.put(_DONE)
+
+    def _take_sequence(self, prompt: list[int]) -> tuple[int, int]:
+        """(sid, reusable prefix length): the idle sequence sharing the longest prefix, else a fresh one
+        (evicting the least recently used idle sequence when every KV row is taken)."""
+        kv = self.r.kv
+        best, keep = None, -1
+        for sid in self.idle:
+            n = kv.common_prefix(kv.seqs[sid].tokens, prompt)
+            if n > keep:
+                best, keep = sid, n
+        if best is not None and keep > 0:
+            self.idle.remove(best)
+            return best, keep
+        if not kv.rows_free and self.idle:
+            kv.free_seq(self.idle.pop(0))
+        return self.r.new_sequence(), 0
+
+    def _admit(self) -> None:
+        r = self.r
+        while True:
+            with self.cv:
+                if not self.pending or len(self.active) >= self.max_parallel:
+                    return
+                req = self.pending.popleft()
+            if req.cancelled.is_set() or req.max_tokens <= 0:
+                req.out.put(_DONE)
+                continue
+            try:
+                sid, keep = self._take_sequence(req.prompt)
+                keep = min(keep, len(req.prompt) - 1)
+                r.kv.truncate(sid, keep)
+                req.sid = sid
+                t0 = time.perf_counter()
+                r.prefill(sid, req.prompt[keep:])
+                r._set_sampler(0, req.opts, req.prompt, req.seed, 0)
+                r._sample(1)
+                first = int(r.s_out[0].item())
+            except BaseException as e:  # noqa: BLE001 -- this request fails, the batch goes on
+                if req.sid is not None and req.sid in r.kv.seqs:
+                    r.free_sequence(req.sid)
+                req.out.put(e)
+                continue
+            req.n_sampled = 1
+            req.history = list(req.prompt) + [first]
+            req.pos = r.kv.seqs[sid].length
+            req.max_tokens = min(req.max_tokens, r.ctx - req.pos)
+            req.last_input = first
+            req.t_gen0 = time.perf_counter()
+            if req.times is not None:
+                req.times.prompt_tokens = len(req.prompt) - keep
+                req.times.prompt_s = req.t_gen0 - t0
+            self._deliver(req, first)
+            if req.finished():
+                self._retire(req)
+            else:
+                self.active.append(req)
+
+    def _deliver(self, req: _Req, tok: int) -> None:
+        req.delivered += 1
+        req.out.put(tok)
+
+    def _retire(self, req: _Req) -> None:
+        req.out.put(_DONE)
+        if req.sid is not None:
+            self.idle.append(req.sid)
+            while len(self.idle) > self.max_parallel:  # bounded prefix cache
+                self.r.free_sequence(self.idle.pop(0))
+
+    def _recompose(self) -> None:
+        """Rows changed: upload every row's next input token and sampler state (history, RNG step)."""
+        r = self.r
+        for b, req in enumerate(self.active):
+            r._set_sampler(b, req.opts, req.history, req.seed, req.n_sampled)
+        r.set_tokens([req.last_input for req in self.active])
+
+    def _run_stable(self) -> None:
+        """Decode steps for the current rows, `depth` in flight, until a row finishes or a request
+        waits for admission; then drain so the next composition starts from known tokens."""
+        r = self.r
+        rows = list(self.active)
+        B = len(rows)
+        self.max_batch_seen = max(self.max_batch_seen, B)
+        self._recompose()
+        if self._ring is None and r.is_gpu:
+            self._ring = [torch.zeros(r.max_batch, dtype=torch.int32).pin_memory() for _ in range(4)]
+        inflight: collections.deque = collections.deque()
+        stop_issue = False
+        while True:
+            # issue while every row still needs a token beyond those in flight
+            while (not stop_issue and len(inflight) < self.depth and
+                   all(q.issued < q.max_tokens - 1 for q in rows)):
+                r.decode_batch([q.sid for q in rows], [q.pos for q in rows])
+                for q in rows:
+                    q.pos += 1
+                    q.issued += 1
+                self.steps += 1
+                if r.is_gpu:
+                    buf = self._ring[self.steps % len(self._ring)]
+                    buf[:B].copy_(r.s_out[:B], non_blocking=True)
+                    ev = torch.cuda.Event()
+                    ev.record()
+                    inflight.append((buf, ev))
+                else:
+                    inflight.append((r.s_out[:B].clone(), None))
+            if not inflight:
+                break
+            buf, ev = inflight.popleft()
+            if ev is not None:
+                ev.synchronize()
+            toks = buf[:B].tolist()
+            for q, t in zip(rows, toks):
+                r.kv.seqs[q.sid].tokens.append(q.last_input)  # its KV was written by this step
+                q.last_input = t
+                q.history.append(t)
+                q.n_sampled += 1
+                if not q.cancelled.is_set():
+                    self._deliver(q, t)
+            if any(q.finished() for q in rows) or self.pending or self.jobs or self.closed:
+                stop_issue = True  # drain what is in flight, then recompose
+        # steps issued past a cancellation were wasted; their KV positions are not recorded
+        for q in rows:
+            if q.finished():
+                self.active.remove(q)
+                self._retire(q)

@@ -56,6 +56,7 @@ class LoadedModel:
     expires_at: float = 0.0
     lock: threading.Lock = field(default_factory=threading.Lock)
     sid: int | None = None
+    scheduler: Any = None  # engine.scheduler.BatchScheduler (OLLAMA_NUM_PARALLEL > 1, single rank)
 
 
 @dataclass
@@ -88,12 +89,15 @@ class ModelManager:
     def _evict_expired(self):
         now = time.time()
         for k, lm in list(self.loaded.items()):
-            if lm.expires_at <= now and not lm.lock.locked():
+            busy = lm.lock.locked() or (lm.scheduler is not None and lm.scheduler.busy)
+            if lm.expires_at <= now and not busy:
                 self._unload(k)
 
     def _unload(self, key: str):
         lm = self.loaded.pop(key, None)
         if lm is not None:
+            if lm.scheduler is not None:
+                lm.scheduler.close()
             if hasattr(lm.runner, "close"):  # TP: the worker ranks drop their shards too
                 lm.runner.close()
             del lm.runner
@@ -145,13 +149,24 @@ class ModelManager:
         ctx = min(num_ctx, ctx_cap) if ctx_cap else num_ctx
         # prefill chunk = MFMA GEMM M dimension (weights cross HBM once per chunk)
         chunk = int(os.environ.get("OMX_PREFILL_CHUNK", "512"))
+        scheduler = None
         if self.tp_world is not None:  # tensor parallel: every rank loads its shard (parallel/tp.py)
             from ..parallel.tp import load_tp_runner
             runner = load_tp_runner(self.tp_world, path, max_batch=chunk, max_seqs=2, ctx=ctx)
+            runner.warmup()
         else:
-            runner = Runner(path, device=self.device, max_batch=chunk, max_seqs=2, ctx=ctx)
-        runner.warmup()
-        return LoadedModel(name=name, digest=m.digest, path=path, runner=runner, tokenizer=tok,
+            # continuous batching (Ollama OLLAMA_NUM_PARALLEL): parallel rows + as many idle sequences
+            # kept for prefix reuse; KV is sized for all of them at full context (288 GB HBM)
+            # default 1 (serialised) until the batched GPU path has been run on MI355X hardware
+            # (tests/test_engine_gpu.py::test_batched_decode_matches_single / test_scheduler_concurrent_gpu)
+            par = max(1, int(os.environ.get("OLLAMA_NUM_PARALLEL", "1")))
+            runner = Runner(path, device=self.device, max_batch=chunk, max_seqs=max(2, 2 * par), ctx=ctx)
+            runner.warmup()
+            if par > 1:
+                from ..engine.scheduler import BatchScheduler
+                runner.capture_batch_graphs(par)
+                scheduler = BatchScheduler(runner, max_parallel=par)
+        return LoadedModel(name=name, digest=m.digest, path=path, runner=runner, tokenizer=tok, scheduler=scheduler,
                            template=self.store.text_layer(m, MT_TEMPLATE), system=self.store.text_layer(m, MT_SYSTEM),
                            params=self.store.params(m), num_ctx=runner.ctx, size=os.path.getsize(path),
                            load_duration_ns=int((time.perf_counter() - t0) * 1e9))
@@ -190,14 +205,20 @@ class ModelManager:
             res.total_duration = int((time.perf_counter() - t_start) * 1e9)
             yield "", res
             return
-        with lm.lock:
-            if lm.sid is None:
-                lm.sid = runner.new_sequence()
+        import contextlib
+        # batched models: the scheduler thread owns the runner (requests share decode steps);
+        # otherwise requests to one model are serialised and reuse one sequence's KV prefix
+        with (contextlib.nullcontext() if lm.scheduler is not None else lm.lock):
             times = StepTimes()
             dec = StreamDecoder(lm.tokenizer, first=not prompt_ids or prompt_ids[-1] == lm.tokenizer.bos_id)
             pending = ""
             out_text = []
-            gen = runner.generate(lm.sid, prompt_ids, so, max_tokens=max_new, times=times)
+            if lm.scheduler is not None:
+                gen = lm.scheduler.submit(prompt_ids, so, max_tokens=max_new, times=times)
+            else:
+                if lm.sid is None:
+                    lm.sid = runner.new_sequence()
+                gen = runner.generate(lm.sid, prompt_ids, so, max_tokens=max_new, times=times)
             n = 0
             reason = "length"
             try:
@@ -247,17 +268,20 @@ class ModelManager:
     def embed(self, lm: LoadedModel, texts: list[str], truncate: bool = True) -> tuple[list[list[float]], int]:
         total = 0
         out = []
-        with lm.lock:
-            for t in texts:
-                ids = lm.tokenizer.encode(t)
-                if len(ids) > lm.runner.ctx:
-                    if not truncate:
-                        raise StoreError("input length exceeds context length")
-                    ids = ids[:lm.runner.ctx]
-                total += len(ids)
-                v = lm.runner.embed(ids)
-                n = float(np.linalg.norm(v)) or 1.0
-                out.append([float(x) / n for x in v])
+        for t in texts:
+            ids = lm.tokenizer.encode(t)
+            if len(ids) > lm.runner.ctx:
+                if not truncate:
+                    raise StoreError("input length exceeds context length")
+                ids = ids[:lm.runner.ctx]
+            total += len(ids)
+            if lm.scheduler is not None:  # between batched decode steps, on the scheduler thread
+                v = lm.scheduler.run_exclusive(lambda r, ids=ids: r.embed(ids))
+            else:
+                with lm.lock:
+                    v = lm.runner.embed(ids)
+            n = float(np.linalg.norm(v)) or 1.0
+            out.append([float(x) / n for x in v])
         return out, total
 
 

@@ -188,6 +188,8 @@ def client(tmp_path_factory, tiny_models):
     st = ModelStore(root)
     st.create("tiny", gguf_path=tiny_models["tiny-llama"], template="[INST] {{ .Prompt }} [/INST]",
               params={"temperature": 0.0, "stop": ["[INST]"], "num_ctx": 128})
+    import os
+    os.environ.setdefault("OLLAMA_NUM_PARALLEL", "4")  # exercise continuous batching on the CPU twin
     app = create_app(st, ModelManager(st, device="cpu"))
     return TestClient(app)
 
@@ -302,3 +304,24 @@ def test_create_from_modelfile(client, tiny_models):
     r = client.post("/api/create", json={"model": "phi-custom2", "from": "phi-custom", "system": "other"})
     assert r.status_code == 200
     assert "other" in client.post("/api/show", json={"model": "phi-custom2"}).json()["modelfile"]
+
+
+def test_concurrent_generate_batched(client):
+    """OLLAMA_NUM_PARALLEL (default 4): concurrent requests share batched decode steps and return what
+    each returns alone (greedy)."""
+    import threading
+    prompts = ["alpha beta", "the quick brown fox", "one two three four five", "zz"]
+    body = lambda p: {"model": "tiny", "prompt": p, "stream": False,  # noqa: E731
+                      "options": {"num_predict": 10, "temperature": 0}}
+    alone = [client.post("/api/generate", json=body(p)).json()["response"] for p in prompts]
+    got = [None] * len(prompts)
+
+    def work(i):
+        got[i] = client.post("/api/generate", json=body(prompts[i])).json()["response"]
+
+    th = [threading.Thread(target=work, args=(i,)) for i in range(len(prompts))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(60)
+    assert got == alone
