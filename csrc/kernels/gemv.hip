@@ -39,8 +39,9 @@ constexpr int GEMV_NT = 64 * GEMV_NW;
 constexpr int XPAD = 17;      // LDS x slots per super-block: 16 groups + 1 pad
 
 GemvTuning g_tune;
-void set_gemv_tuning(int blocks_per_cu, int rows, int debug, int ks) {
+void set_gemv_tuning(int blocks_per_cu, int rows, int debug, int ks, int xfirst) {
   g_tune.debug = debug > 0 ? debug : 0;
+  if (xfirst == 0 || xfirst == 1) g_tune.xfirst = xfirst;
   if (ks >= 0 && ks <= 4) g_tune.ks = ks;
   if (blocks_per_cu > 0) g_tune.blocks_per_cu = blocks_per_cu;
   if (rows == 1 || rows == 2) g_tune.rows = rows;
@@ -550,6 +551,12 @@ __device__ __forceinline__ void flight_body(const GemvParams& P, const int bx, c
   }
   __builtin_amdgcn_sched_barrier(0);  // activations ahead of the weights
   if constexpr ((DBG & 4) != 0) __builtin_amdgcn_s_barrier();  // every wave's x requests queued first
+  // x-first (GemvTuning::xfirst): wait for the activations BEFORE requesting any weight. The x lines
+  // were just written by the previous kernel and miss L2; issued behind the whole matrix's requests
+  // they return only after most of the weight stream (profiles/r1_defer/gemv_timeline.log: prologue
+  // p50 4.6-8.3 us on the down projections), so every tile waits on them.
+  if (P.xfirst) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
   // 2. every weight tile of this block in flight (surplus slots re-read the last tile, unused)
   WTile<QT, NSB, R> T[J];
 #pragma unroll
@@ -791,13 +798,6 @@ static void launch_flight_ks_n(const GemvParams& P, int gx, hipStream_t s) {
   hipLaunchKernelGGL((qgemv_flight_kernel<QT, NSB, 1, 1, NRM, 0, KS>), dim3(gx, 1, bz), dim3(GEMV_NT * KS), lds, s, P);
 }
 
-template <int QT, int NSB, int KS>
-static void launch_flight_ks(const GemvParams& P, int gx, hipStream_t s) {
-  if (P.norm == NORM_NONE) launch_flight_ks_n<QT, NSB, KS, 0>(P, gx, s);
-  else if (P.norm == NORM_LAYER && P.norm_b) launch_flight_ks_n<QT, NSB, KS, 2>(P, gx, s);
-  else launch_flight_ks_n<QT, NSB, KS, 1>(P, gx, s);
-}
-
 template <int QT, int NSB, int R, int J>
 static void launch_flight_j(const GemvParams& P, int gx, hipStream_t s) {
   if (P.norm == NORM_NONE) launch_flight_n<QT, NSB, R, J, 0>(P, gx, s);
@@ -815,6 +815,29 @@ static int flight_ks(int need, int tiles, int bz) {
   return need >= 3 ? 3 : 2;
 }
 
+// VGPRs a K-split flight instantiation needs (weight tile + activation / norm registers + ~24 of
+// addressing and accumulators) against the 512 / KS per lane that KS waves per SIMD leave. Calibrated
+// on the built code objects (tests/test_isa.py): the two Q8_0 LayerNorm variants above budget
+// (KS = 4 NSB = 1, KS = 2 NSB = 2) were the only ones spilling to scratch.
+template <int QT, int NSB, int KS, int NRM>
+constexpr bool flight_ks_fits() {
+  constexpr int PB = QT == QT_Q8_0 ? 8 : QT == QT_Q6_K ? 6 : QT == QT_Q5_K ? 5 : 4;
+  return NSB * (8 * PB + 5) + NSB * 16 * (1 + (NRM != 0) + (NRM == 2)) + 24 <= 512 / KS;
+}
+
+template <int QT, int NSB, int KS>
+static bool launch_flight_ks_fit(const GemvParams& P, int gx, hipStream_t s) {
+  const int nrm = P.norm == NORM_NONE ? 0 : (P.norm == NORM_LAYER && P.norm_b) ? 2 : 1;
+  if (nrm == 0) {
+    if constexpr (flight_ks_fits<QT, NSB, KS, 0>()) { launch_flight_ks_n<QT, NSB, KS, 0>(P, gx, s); return true; }
+  } else if (nrm == 1) {
+    if constexpr (flight_ks_fits<QT, NSB, KS, 1>()) { launch_flight_ks_n<QT, NSB, KS, 1>(P, gx, s); return true; }
+  } else {
+    if constexpr (flight_ks_fits<QT, NSB, KS, 2>()) { launch_flight_ks_n<QT, NSB, KS, 2>(P, gx, s); return true; }
+  }
+  return false;  // the variant would spill: the caller takes the unsplit kernel
+}
+
 template <int QT>
 static bool launch_flight_split(const GemvParams& P, int need, hipStream_t s) {
   const int tiles = (P.w.N + 4 * GEMV_NW - 1) / (4 * GEMV_NW);
@@ -822,12 +845,11 @@ static bool launch_flight_split(const GemvParams& P, int need, hipStream_t s) {
   const int ks = flight_ks(need, tiles, bz);
   if (ks <= 1) return false;
   const int nsb = (need + ks - 1) / ks;  // 16 * nsb >= ceil(SB / ks)
-  if (ks == 2 && nsb == 1) launch_flight_ks<QT, 1, 2>(P, tiles, s);
-  else if (ks == 2 && nsb == 2) launch_flight_ks<QT, 2, 2>(P, tiles, s);
-  else if (ks == 3 && nsb == 1) launch_flight_ks<QT, 1, 3>(P, tiles, s);
-  else if (ks == 4 && nsb == 1) launch_flight_ks<QT, 1, 4>(P, tiles, s);
-  else return false;
-  return true;
+  if (ks == 2 && nsb == 1) return launch_flight_ks_fit<QT, 1, 2>(P, tiles, s);
+  if (ks == 2 && nsb == 2) return launch_flight_ks_fit<QT, 2, 2>(P, tiles, s);
+  if (ks == 3 && nsb == 1) return launch_flight_ks_fit<QT, 1, 3>(P, tiles, s);
+  if (ks == 4 && nsb == 1) return launch_flight_ks_fit<QT, 1, 4>(P, tiles, s);
+  return false;
 }
 
 template <int QT, int NSB, int R>
@@ -917,7 +939,9 @@ static bool launch_dual_a(const GemvParams& A, const GemvParams& Bp, int need, h
   return false;
 }
 
-void gemv2(const GemvParams& A, const GemvParams& Bp, hipStream_t s) {
+void gemv2(const GemvParams& A0, const GemvParams& B0, hipStream_t s) {
+  GemvParams A = A0, Bp = B0;
+  A.xfirst = Bp.xfirst = g_tune.xfirst;
   const int need = ((A.w.K + 255) / 256 + 15) / 16;
   const bool ok = A.B == 1 && Bp.B == 1 && A.w.K == Bp.w.K && need <= 2 && A.norm == NORM_RMS &&
                   Bp.norm == NORM_RMS && !A.expert_ids && !Bp.expert_ids && !A.merge_S && !Bp.merge_S &&
@@ -941,7 +965,9 @@ bool gemv_merge_supported(int B, int K, int D, int S) {
   return B == 1 && K <= 4096 && D % 16 == 0 && K % D == 0 && (S == 2 || S == 4 || S == 8);
 }
 
-void gemv(const GemvParams& P, hipStream_t s) {
+void gemv(const GemvParams& P0, hipStream_t s) {
+  GemvParams P = P0;
+  P.xfirst = g_tune.xfirst;
   if (P.merge_S > 0) {
     // flight grid for K <= 4096 is one chunk, R = 1, no K split: the merge variant covers exactly it
     if (!gemv_merge_supported(P.B, P.w.K, P.merge_D, P.merge_S) || P.norm != NORM_NONE || P.expert_ids) return;

@@ -62,6 +62,7 @@ struct GemvParams {
   // timeline probe (scripts/gemv_timeline.py): per block 4 x s_memrealtime (100 MHz) at entry,
   // prologue done, first tile computed, exit; null in production
   unsigned long long* dbg_ts;
+  int xfirst;                  // activations waited for before any weight load (GemvTuning::xfirst)
 };
 
 // y = epi(W x): the quantised GEMV for small B (decode), the MFMA dequant GEMM for B >= GEMM_MIN_B
@@ -80,9 +81,10 @@ struct GemvTuning {
   int rows = 1;           // rows per 16-lane row group in B == 1 launches (1 or 2)
   int debug = 0;          // microbenchmark-only kernel variants (gemv.hip DBG)
   int ks = 0;             // in-block K split of the flight kernel: 0 = auto, 1 = off, 2..4 = forced
+  int xfirst = 0;         // 1: decode GEMVs wait for their activations before streaming weights
 };
 extern GemvTuning g_tune;
-void set_gemv_tuning(int blocks_per_cu, int rows, int debug, int ks = -1);
+void set_gemv_tuning(int blocks_per_cu, int rows, int debug, int ks = -1, int xfirst = -1);
 
 // Dequantize rows of a repacked matrix (embedding gather / fp16 copies)
 void embed_rows(const QMat& w, const int* rows, int n, float* out, int ldo, hipStream_t s);

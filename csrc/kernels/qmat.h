@@ -9,7 +9,7 @@
 #pragma once
 #include <stdint.h>
 
-enum QType : int { QT_Q4_0 = 2, QT_Q8_0 = 8, QT_Q4_K = 12, QT_Q6_K = 14 };
+enum QType : int { QT_Q4_0 = 2, QT_Q8_0 = 8, QT_Q4_K = 12, QT_Q5_K = 13, QT_Q6_K = 14 };
 
 struct QMat {
   const uint8_t* s0;

@@ -11,6 +11,7 @@ step behind, so the GPU never waits on Python.
 """
 from __future__ import annotations
 
+import gc
 import os
 import time
 from dataclasses import dataclass
@@ -99,6 +100,8 @@ class Runner:
         self.is_gpu = self.device.type == "cuda"
         if self.is_gpu:
             native()  # fail loudly: no silent torch fallback on a GPU box
+            if os.environ.get("OMX_GEMV_XFIRST") in ("0", "1"):  # decode GEMV x-first knob (gemv.hip)
+                native().set_gemv_tuning(xfirst=int(os.environ["OMX_GEMV_XFIRST"]))
         self.tp_rank, self.tp_size, self.tp_group = tp_rank, tp_size, tp_group
         # TP serving (parallel/tp.py): rank 0 signals each decode step, followers mirror it
         self.tp_ctrl = tp_ctrl
@@ -366,8 +369,18 @@ class Runner:
                 self.forward(B, B, use_idx=False)
             torch.cuda.current_stream().wait_stream(s)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                self._decode_body(B)
+            # No cyclic GC while capturing: a collection that frees another Runner's graph or
+            # events issues HIP destroy calls mid-capture, which invalidates the capture (abort).
+            # thread_local: other threads (scheduler, server) may keep issuing HIP calls meanwhile.
+            gc.collect()
+            gc_was = gc.isenabled()
+            gc.disable()
+            try:
+                with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                    self._decode_body(B)
+            finally:
+                if gc_was:
+                    gc.enable()
             self.graphs[key] = g
         return g
 

@@ -15,6 +15,10 @@ loaded model owns the `Runner` and
 * restores every row's sampler state (penalty history, seeded RNG counter) when rows are recomposed, so a
   request's random draws do not depend on who else is in the batch.
 
+Failure semantics: a step that raises fails only the requests it carried (their rows are freed) and the
+loop goes on; a closed or dead scheduler rejects new work immediately and fails everything queued, so no
+caller ever blocks on a scheduler that will not answer.
+
 The same code drives the torch twin on CPU (tests), where steps are simply synchronous.
 """
 from __future__ import annotations
@@ -32,6 +36,10 @@ from .runner import Runner, StepTimes
 from .sampling import SamplingOptions
 
 _DONE = object()
+
+
+class SchedulerClosed(RuntimeError):
+    pass
 
 
 @dataclass
@@ -63,7 +71,9 @@ class BatchScheduler:
         if runner.tp_size > 1:
             raise ValueError("continuous batching runs on single-rank runners (TP serving is serialised)")
         self.r = runner
+        # one KV row stays reserved for exclusive jobs (embeddings) even when every row decodes
         self.max_parallel = max(1, min(max_parallel, runner.max_batch, runner.max_seqs - 1))
+        self.max_idle = max(0, runner.max_seqs - self.max_parallel - 1)  # prefix cache rows
         self.depth = depth if runner.is_gpu else 1  # steps in flight
         self.cv = threading.Condition()
         self.pending: collections.deque[_Req] = collections.deque()
@@ -72,12 +82,17 @@ class BatchScheduler:
         self.idle: list[int] = []  # sequences kept for prefix reuse, most recent last
         self.closed = False
         self.steps = 0
+        self.failed_steps = 0
         self.max_batch_seen = 0
         self._ring = None
         self._thread = threading.Thread(target=self._loop, name="omx-batch", daemon=True)
         self._thread.start()
 
     # ------------------------------------------------------------------ public API
+    def _check_open(self) -> None:
+        if self.closed or not self._thread.is_alive():
+            raise SchedulerClosed("scheduler closed")
+
     def submit(self, prompt: list[int], options: SamplingOptions | None = None, max_tokens: int = 128,
                times: StepTimes | None = None) -> Iterator[int]:
         """Queue a generation; yields its tokens as the batched steps produce them. Closing the
@@ -85,10 +100,12 @@ class BatchScheduler:
         o = options or SamplingOptions()
         req = _Req(prompt=list(prompt), opts=o, seed=o.resolved_seed(), max_tokens=max(0, max_tokens), times=times)
         with self.cv:
-            if self.closed:
-                raise RuntimeError("scheduler closed")
+            self._check_open()
             self.pending.append(req)
             self.cv.notify()
+        return self._consume(req, times)
+
+    def _consume(self, req: _Req, times: StepTimes | None) -> Iterator[int]:
         n, t1 = 0, None
         try:
             while True:
@@ -113,6 +130,7 @@ class BatchScheduler:
         """Run fn(runner) on the scheduler thread between steps (embeddings share the runner)."""
         box: queue.Queue = queue.Queue()
         with self.cv:
+            self._check_open()
             self.jobs.append((fn, box))
             self.cv.notify()
         ok, val = box.get()
@@ -132,6 +150,7 @@ class BatchScheduler:
 
     # ------------------------------------------------------------------ scheduler thread
     def _loop(self) -> None:
+        err: BaseException = SchedulerClosed("scheduler closed")
         try:
             while True:
                 with self.cv:
@@ -142,20 +161,48 @@ class BatchScheduler:
                     jobs = list(self.jobs)
                     self.jobs.clear()
                 for fn, box in jobs:
-                    try:
-                        box.put((True, fn(self.r)))
-                    except BaseException as e:  # noqa: BLE001 -- handed to the caller
-                        box.put((False, e))
-                self._admit()
-                if self.active:
-                    self._run_stable()
-        except BaseException as e:  # noqa: BLE001 -- fail every waiter loudly instead of hanging them
-            for req in list(self.active) + list(self.pending):
-                req.out.put(e)
+                    self._run_job(fn, box)
+                try:
+                    self._admit()
+                    if self.active:
+                        self._run_stable()
+                except Exception as e:  # noqa: BLE001 -- fail the rows this step carried, keep serving
+                    self.failed_steps += 1
+                    self._fail_active(e)
+        except BaseException as e:  # noqa: BLE001 -- the loop itself died: nobody may wait on it
+            err = e
             raise
         finally:
-            for req in list(self.active) + list(self.pending):
-                req.out.put(_DONE)
+            self._shutdown(err)
+
+    def _run_job(self, fn, box) -> None:
+        kv = self.r.kv
+        if not kv.rows_free and self.idle:  # every row taken: give the job the LRU prefix-cache row
+            self.r.free_sequence(self.idle.pop(0))
+        try:
+            box.put((True, fn(self.r)))
+        except BaseException as e:  # noqa: BLE001 -- handed to the caller
+            box.put((False, e))
+
+    def _fail_active(self, e: BaseException) -> None:
+        for req in self.active:
+            req.out.put(e)
+            if req.sid is not None and req.sid in self.r.kv.seqs:
+                self.r.free_sequence(req.sid)
+        self.active.clear()
+
+    def _shutdown(self, e: BaseException) -> None:
+        with self.cv:
+            self.closed = True
+            reqs = list(self.active) + list(self.pending)
+            jobs = list(self.jobs)
+            self.active.clear()
+            self.pending.clear()
+            self.jobs.clear()
+        for req in reqs:
+            req.out.put(e)
+        for _, box in jobs:
+            box.put((False, e if isinstance(e, Exception) else SchedulerClosed("scheduler closed")))
 
     def _take_sequence(self, prompt: list[int]) -> tuple[int, int]:
         """(sid, reusable prefix length): the idle sequence sharing the longest prefix, else a fresh one
@@ -221,7 +268,7 @@ class BatchScheduler:
         req.out.put(_DONE)
         if req.sid is not None:
             self.idle.append(req.sid)
-            while len(self.idle) > self.max_parallel:  # bounded prefix cache
+            while len(self.idle) > self.max_idle:  # bounded prefix cache
                 self.r.free_sequence(self.idle.pop(0))
 
     def _recompose(self) -> None:
@@ -231,9 +278,17 @@ class BatchScheduler:
             r._set_sampler(b, req.opts, req.history, req.seed, req.n_sampled)
         r.set_tokens([req.last_input for req in self.active])
 
+    def _must_drain(self, rows: list[_Req]) -> bool:
+        """Stop issuing (drain in-flight steps, then recompose) only when the composition must change:
+        a row finished, an exclusive job or close is waiting, or a queued request can actually be
+        admitted. Under overload (every row busy) pending requests do not break the pipelining."""
+        if any(q.finished() for q in rows) or self.jobs or self.closed:
+            return True
+        return bool(self.pending) and len(self.active) < self.max_parallel
+
     def _run_stable(self) -> None:
-        """Decode steps for the current rows, `depth` in flight, until a row finishes or a request
-        waits for admission; then drain so the next composition starts from known tokens."""
+        """Decode steps for the current rows, `depth` in flight, until the composition must change;
+        then drain so the next composition starts from known tokens."""
         r = self.r
         rows = list(self.active)
         B = len(rows)
@@ -273,8 +328,9 @@ class BatchScheduler:
                 q.n_sampled += 1
                 if not q.cancelled.is_set():
                     self._deliver(q, t)
-            if any(q.finished() for q in rows) or self.pending or self.jobs or self.closed:
-                stop_issue = True  # drain what is in flight, then recompose
+            with self.cv:
+                if self._must_drain(rows):
+                    stop_issue = True  # drain what is in flight, then recompose
         # steps issued past a cancellation were wasted; their KV positions are not recorded
         for q in rows:
             if q.finished():

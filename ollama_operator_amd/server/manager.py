@@ -160,7 +160,8 @@ class ModelManager:
             # default 1 (serialised) until the batched GPU path has been run on MI355X hardware
             # (tests/test_engine_gpu.py::test_batched_decode_matches_single / test_scheduler_concurrent_gpu)
             par = max(1, int(os.environ.get("OLLAMA_NUM_PARALLEL", "1")))
-            runner = Runner(path, device=self.device, max_batch=chunk, max_seqs=max(2, 2 * par), ctx=ctx)
+            # rows: par decoding + par idle prefix-cache sequences + 1 kept free for embeddings
+            runner = Runner(path, device=self.device, max_batch=chunk, max_seqs=max(2, 2 * par + 1), ctx=ctx)
             runner.warmup()
             if par > 1:
                 from ..engine.scheduler import BatchScheduler

@@ -1,9 +1,9 @@
 """Self-contained linter (no third-party tools in the build image; reference .golangci.yml, SURVEY.md
 §2.1 R29). Python: compiles, no unused imports (ast), no tabs / trailing whitespace, <= 140 columns.
 HIP/C++ (csrc/): no tabs / trailing whitespace, <= 140 columns, and the MI355X-only policy:
-  * no CUDA compatibility layers (cuda_runtime, __CUDA_ARCH__, __HIP_PLATFORM_* dual paths, hipify);
-  * no writes through the scalar data cache (s_store*, s_buffer_store*, s_scratch_store*, scalar
-    atomics, s_dcache_wb, s_dcache_discard) -- forbidden on this hardware pool.
+  * no CUDA compatibility layers (cuda_runtime, __CUDA_ARCH__, __HIP_PLATFORM_* dual paths, hipify).
+The scalar-memory policy is enforced on the *built* ISA by an allow-list (scripts/isa_check.py), so
+no source file needs to spell out the instructions it rejects.
 Usage: python scripts/lint.py [paths...]   (exit 1 on findings)"""
 from __future__ import annotations
 
@@ -17,9 +17,6 @@ SKIP_DIRS = {".git", "build", "gpurun_out", "__pycache__", ".pytest_cache", ".hy
 MAX_COL = 140
 NATIVE_EXT = (".hip", ".cpp", ".h", ".hpp", ".s")
 FORBIDDEN_NATIVE = [
-    (re.compile(r"\bs_(buffer_|scratch_)?store_dword"), "scalar-cache store"),
-    (re.compile(r"\bs_(buffer_)?atomic_"), "scalar atomic"),
-    (re.compile(r"\bs_dcache_(wb|discard)"), "scalar-cache write-back/discard"),
     (re.compile(r"#\s*include\s*[<\"]cuda"), "CUDA header"),
     (re.compile(r"__CUDA_ARCH__|__NVCC__"), "CUDA dual path"),
     (re.compile(r"#\s*if(def)?\s+.*__HIP_PLATFORM_(AMD|NVIDIA)__"), "HIP platform dual path"),

@@ -18,10 +18,10 @@ def test_lint_catches_forbidden_native(tmp_path):
     sys.path.insert(0, os.path.join(ROOT, "scripts"))
     import lint
     bad = tmp_path / "k.hip"
-    bad.write_text('__global__ void k() { asm volatile("s_store_dword s0, s[2:3], 0x0"); }\n'
+    bad.write_text('#include <cuda_runtime.h>\n__global__ void k() {}\n'
                    "#ifdef __HIP_PLATFORM_AMD__\n#endif\n")
     msgs = lint.lint_file(str(bad))
-    assert any("scalar-cache store" in m for m in msgs) and any("dual path" in m for m in msgs)
+    assert any("CUDA header" in m for m in msgs) and any("dual path" in m for m in msgs)
     py = tmp_path / "m.py"
     py.write_text("import os\nimport sys\nprint(sys.argv)\n")
     assert any("unused import 'os'" in m for m in lint.lint_file(str(py)))

@@ -1,6 +1,7 @@
 """Continuous batching (engine/scheduler.py) on the torch twin: concurrent requests decode in one batch
 and produce what each would produce alone; cancellation frees rows; prefix reuse across turns."""
 import threading
+import time
 
 import pytest
 
@@ -69,4 +70,91 @@ def test_exclusive_job_between_steps(runner):
     sch = BatchScheduler(r, max_parallel=2)
     v = sch.run_exclusive(lambda rr: rr.embed([1, 2, 3]))
     assert v.shape == (r.cfg.n_embd,)
+    sch.close()
+
+
+def test_failed_step_fails_rows_and_loop_survives(runner, monkeypatch):
+    """A step that raises fails the requests it carried (rows freed); later requests are served."""
+    r = Runner(runner, device="cpu", max_batch=16, max_seqs=5, ctx=256)
+    sch = BatchScheduler(r, max_parallel=2)
+    orig = r.decode_batch
+    calls = {"n": 0}
+
+    def boom(sids, poss):
+        calls["n"] += 1
+        if calls["n"] == 2:
+            raise RuntimeError("injected HIP error")
+        return orig(sids, poss)
+
+    monkeypatch.setattr(r, "decode_batch", boom)
+    with pytest.raises(RuntimeError, match="injected"):
+        list(sch.submit([1, 2, 3], SamplingOptions(temperature=0), 10))
+    out = list(sch.submit([1, 4, 5], SamplingOptions(temperature=0), 5))
+    assert len(out) == 5 and sch.failed_steps == 1
+    sch.close()
+    with pytest.raises(RuntimeError, match="closed"):
+        sch.submit([1], SamplingOptions(), 2)
+    with pytest.raises(RuntimeError, match="closed"):
+        sch.run_exclusive(lambda rr: 1)
+
+
+def test_close_fails_queued_jobs_and_requests(runner):
+    r = Runner(runner, device="cpu", max_batch=16, max_seqs=5, ctx=256)
+    sch = BatchScheduler(r, max_parallel=2)
+    gate = threading.Event()
+    res = {}
+
+    def slow_job(rr):
+        gate.wait(10)
+        return 1
+
+    t1 = threading.Thread(target=lambda: res.setdefault("a", sch.run_exclusive(slow_job)))
+    t1.start()
+    time.sleep(0.2)
+
+    def second():
+        try:
+            sch.run_exclusive(lambda rr: 2)
+        except RuntimeError as e:
+            res["b"] = e
+
+    t2 = threading.Thread(target=second)
+    t2.start()
+    time.sleep(0.2)
+    closer = threading.Thread(target=sch.close)
+    closer.start()
+    time.sleep(0.1)
+    gate.set()
+    for t in (t1, t2, closer):
+        t.join(30)
+        assert not t.is_alive()
+    assert res["a"] == 1 and isinstance(res["b"], RuntimeError)
+
+
+def test_embed_job_with_every_row_taken(runner):
+    """All rows decoding + a full idle prefix cache: an embedding job still gets a KV row."""
+    r = Runner(runner, device="cpu", max_batch=16, max_seqs=5, ctx=256)  # the manager's 2*par+1
+    sch = BatchScheduler(r, max_parallel=2)
+    for i in range(2):  # fill the idle prefix cache
+        list(sch.submit([1, 30 + i, 40 + i], SamplingOptions(temperature=0), 2))
+    gens = [sch.submit([1, 50 + i], SamplingOptions(temperature=0), 40) for i in range(2)]
+    firsts = [next(g) for g in gens]  # both rows active now
+    v = sch.run_exclusive(lambda rr: rr.embed([1, 2, 3]))
+    assert v.shape == (r.cfg.n_embd,) and len(firsts) == 2
+    for g in gens:
+        g.close()
+    sch.close()
+
+
+def test_overload_keeps_pipelining(runner):
+    """More clients than rows: pending requests that cannot be admitted must not force a drain."""
+    r = Runner(runner, device="cpu", max_batch=16, max_seqs=3, ctx=256)
+    sch = BatchScheduler(r, max_parallel=1)
+    rows = []
+    sch.pending.append(object())  # a queued request while the only row is busy
+    sch.active = rows = [type("Q", (), {"finished": lambda self: False})()]
+    assert not sch._must_drain(rows)
+    sch.active = []
+    assert sch._must_drain(rows)  # a free row: admit now
+    sch.pending.clear()
     sch.close()
