@@ -3,6 +3,16 @@ work queue with per-key de-duplication, delayed requeues and exponential error b
 Models AND the owned StatefulSets / Deployments (the reference watches only Models,
 model_controller.go:172-176); Lease-based leader election with ID `300b498d.ayaka.io`
 (cmd/main.go:108); /healthz + /readyz (:8081) and Prometheus /metrics (:8080) endpoints.
+
+`--metrics-secure` (reference cmd/main.go:66-67,100-104) serves /metrics over TLS and authorises
+every scrape the way the reference's kube-rbac-proxy sidecar does
+(config/default/manager_auth_proxy_patch.yaml:11-39): the bearer token goes through a TokenReview,
+the user through a SubjectAccessReview for `get` on the `/metrics` non-resource URL (granted by the
+`metrics-reader` ClusterRole). HTTP/2 is never offered (`--enable-http2` is accepted for flag
+compatibility; the reference disables it by default for the same CVEs, cmd/main.go:78-92).
+SIGTERM/SIGINT stop the manager gracefully (reference `ctrl.SetupSignalHandler()`, cmd/main.go:146):
+the queue closes, in-flight reconciles finish, and a leader releases its Lease so a standby replica
+takes over at once instead of after the lease duration.
 """
 from __future__ import annotations
 
@@ -11,7 +21,11 @@ import heapq
 import json
 import logging
 import os
+import signal
 import socket
+import ssl
+import subprocess
+import tempfile
 import threading
 import time
 from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
@@ -269,15 +283,90 @@ class Manager:
         t.start()
         self.threads.append(t)
 
-    def shutdown(self):
+    def shutdown(self, drain_timeout: float = 10.0):
+        """Stop watching and dequeuing, let in-flight reconciles finish, release the Lease if held."""
         self.stop.set()
         self.q.close()
+        deadline = time.monotonic() + drain_timeout
+        for t in self.threads:
+            if t is not threading.current_thread():
+                t.join(max(0.0, deadline - time.monotonic()))
+        if self.leader_elect and self.is_leader:
+            self.release_lease()
+
+    def release_lease(self) -> bool:
+        """controller-runtime LeaderElectionReleaseOnCancel: clear the holder so another replica
+        acquires immediately."""
+        try:
+            lease = self.kube.get("Lease", self.lease_ns, LEADER_ELECTION_ID)
+            if not lease or (lease.get("spec") or {}).get("holderIdentity") != self.identity:
+                return False
+            lease["spec"].update({"holderIdentity": "", "leaseDurationSeconds": 1})
+            self.kube.update("Lease", self.lease_ns, lease)
+            self.is_leader = False
+            self.metrics.leader.labels("ollama-operator").set(0)
+            log.info("released leader lease %s", LEADER_ELECTION_ID)
+            return True
+        except (ApiError, OSError) as e:
+            log.info("lease release failed: %s", e)
+            return False
 
 
-def serve_probes(manager: Manager, health_addr: str, metrics_addr: str):
+class MetricsAuth:
+    """kube-rbac-proxy semantics in process: TokenReview (authn) + SubjectAccessReview (authz on the
+    /metrics non-resource URL). Decisions are cached briefly, as the proxy does."""
+
+    def __init__(self, kube, ttl: float = 30.0):
+        self.kube = kube
+        self.ttl = ttl
+        self._cache: dict[str, tuple[float, int]] = {}
+
+    def check(self, header: str | None) -> int:
+        """HTTP status for a request carrying this Authorization header: 200, 401 or 403."""
+        if not header or not header.startswith("Bearer "):
+            return 401
+        token = header[7:].strip()
+        hit = self._cache.get(token)
+        if hit and hit[0] > time.monotonic():
+            return hit[1]
+        try:
+            tr = self.kube.create("TokenReview", None, {
+                "apiVersion": "authentication.k8s.io/v1", "kind": "TokenReview", "spec": {"token": token}})
+            st = tr.get("status") or {}
+            if not st.get("authenticated"):
+                code = 401
+            else:
+                user = st.get("user") or {}
+                sar = self.kube.create("SubjectAccessReview", None, {
+                    "apiVersion": "authorization.k8s.io/v1", "kind": "SubjectAccessReview",
+                    "spec": {"user": user.get("username", ""), "groups": user.get("groups") or [],
+                             "nonResourceAttributes": {"path": "/metrics", "verb": "get"}}})
+                code = 200 if (sar.get("status") or {}).get("allowed") else 403
+        except (ApiError, OSError) as e:
+            log.info("metrics authn/authz failed: %s", e)
+            return 401
+        self._cache[token] = (time.monotonic() + self.ttl, code)
+        return code
+
+
+def self_signed_cert(cert_dir: str | None = None) -> tuple[str, str]:
+    """(cert, key) for TLS metrics: `tls.crt`/`tls.key` from cert_dir, else a self-signed pair (as
+    controller-runtime generates when no certificate is mounted)."""
+    if cert_dir and os.path.exists(os.path.join(cert_dir, "tls.crt")):
+        return os.path.join(cert_dir, "tls.crt"), os.path.join(cert_dir, "tls.key")
+    d = tempfile.mkdtemp(prefix="omx-metrics-tls-")
+    crt, key = os.path.join(d, "tls.crt"), os.path.join(d, "tls.key")
+    subprocess.run(["openssl", "req", "-x509", "-newkey", "rsa:2048", "-nodes", "-days", "365", "-keyout", key,
+                    "-out", crt, "-subj", "/CN=ollama-operator-metrics"], check=True, capture_output=True)
+    return crt, key
+
+
+def serve_probes(manager: Manager, health_addr: str, metrics_addr: str, secure: bool = False,
+                 cert_dir: str | None = None):
     from prometheus_client import generate_latest
+    auth = MetricsAuth(manager.kube) if secure else None
 
-    def make(handler_map):
+    def make(handler_map, authz=None):
         class H(BaseHTTPRequestHandler):
             def do_GET(self):
                 fn = handler_map.get(self.path.split("?")[0])
@@ -285,6 +374,13 @@ def serve_probes(manager: Manager, health_addr: str, metrics_addr: str):
                     self.send_response(404)
                     self.end_headers()
                     return
+                if authz is not None:
+                    code = authz.check(self.headers.get("Authorization"))
+                    if code != 200:
+                        self.send_response(code)
+                        self.end_headers()
+                        self.wfile.write(b"Unauthorized" if code == 401 else b"Forbidden")
+                        return
                 code, body, ctype = fn()
                 self.send_response(code)
                 self.send_header("Content-Type", ctype)
@@ -309,10 +405,39 @@ def serve_probes(manager: Manager, health_addr: str, metrics_addr: str):
         def met():
             manager.metrics.depth.labels("model").set(manager.q.depth())
             return 200, generate_latest(manager.metrics.reg), "text/plain; version=0.0.4"
-        s = ThreadingHTTPServer(addr(metrics_addr), make({"/metrics": met}))
+        s = ThreadingHTTPServer(addr(metrics_addr), make({"/metrics": met}, auth))
+        if secure:
+            crt, key = self_signed_cert(cert_dir)
+            ctx = ssl.SSLContext(ssl.PROTOCOL_TLS_SERVER)
+            ctx.minimum_version = ssl.TLSVersion.TLSv1_2
+            ctx.set_alpn_protocols(["http/1.1"])  # never h2 (reference cmd/main.go:78-92)
+            ctx.load_cert_chain(crt, key)
+            s.socket = ctx.wrap_socket(s.socket, server_side=True)
         threading.Thread(target=s.serve_forever, daemon=True).start()
         servers.append(s)
     return servers
+
+
+def run_until_signal(mgr: Manager, servers: list | None = None, stop: threading.Event | None = None) -> None:
+    """Block until SIGTERM / SIGINT (or `stop`), then shut down gracefully (reference
+    ctrl.SetupSignalHandler, cmd/main.go:146). Must run on the main thread (signal handlers)."""
+    stop = stop or threading.Event()
+    prev = {}
+
+    def handler(signum, _frame):
+        log.info("received signal %d: shutting down", signum)
+        stop.set()
+    for sig in (signal.SIGTERM, signal.SIGINT):
+        prev[sig] = signal.signal(sig, handler)
+    try:
+        while not stop.wait(0.2):
+            pass
+    finally:
+        for sig, h in prev.items():
+            signal.signal(sig, h)
+        mgr.shutdown()
+        for s in servers or []:
+            s.shutdown()
 
 
 def main(argv=None):
@@ -322,8 +447,11 @@ def main(argv=None):
     p.add_argument("--metrics-bind-address", default=":8080")
     p.add_argument("--health-probe-bind-address", default=":8081")
     p.add_argument("--leader-elect", action="store_true")
-    p.add_argument("--metrics-secure", action="store_true")
-    p.add_argument("--enable-http2", action="store_true")
+    p.add_argument("--metrics-secure", action="store_true",
+                   help="serve /metrics over TLS with TokenReview + SubjectAccessReview authorisation")
+    p.add_argument("--metrics-cert-dir", default=os.environ.get("METRICS_CERT_DIR"),
+                   help="directory with tls.crt / tls.key (default: self-signed)")
+    p.add_argument("--enable-http2", action="store_true", help="accepted for compatibility; HTTP/2 is never served")
     p.add_argument("--namespace", default=os.environ.get("WATCH_NAMESPACE") or None)
     p.add_argument("--zap-devel", action="store_true")
     p.add_argument("--zap-log-level", default="info")
@@ -335,16 +463,16 @@ def main(argv=None):
                         format='{"ts":"%(asctime)s","level":"%(levelname)s","logger":"%(name)s","msg":%(message)r}'
                         if a.zap_encoder == "json" else "%(asctime)s %(levelname)s %(name)s %(message)s")
     from .kube import KubeClient
+    if a.enable_http2:
+        log.info("--enable-http2: HTTP/2 is not served by this manager; metrics stay on HTTP/1.1")
     kube = KubeClient.from_env()
     mgr = Manager(kube, namespace=a.namespace, leader_elect=a.leader_elect)
-    serve_probes(mgr, a.health_probe_bind_address, a.metrics_bind_address)
+    servers = serve_probes(mgr, a.health_probe_bind_address, a.metrics_bind_address, secure=a.metrics_secure,
+                           cert_dir=a.metrics_cert_dir)
     mgr.start()
-    log.info("starting manager %s", json.dumps({"leaderElection": a.leader_elect, "namespace": a.namespace}))
-    try:
-        while True:
-            time.sleep(3600)
-    except KeyboardInterrupt:
-        mgr.shutdown()
+    log.info("starting manager %s", json.dumps({"leaderElection": a.leader_elect, "namespace": a.namespace,
+                                                  "metricsSecure": a.metrics_secure}))
+    run_until_signal(mgr, servers)
 
 
 if __name__ == "__main__":

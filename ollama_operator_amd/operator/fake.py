@@ -24,6 +24,10 @@ class FakeKube:
         self._ip = itertools.count(10)
         self.watchers: list = []
         self.log: list[tuple[str, str, str]] = []  # (verb, kind, name)
+        # authn / authz for TokenReview / SubjectAccessReview: bearer token -> user, users allowed
+        # `get` on the /metrics non-resource URL (the metrics-reader ClusterRole)
+        self.tokens: dict[str, str] = {}
+        self.metrics_readers: set[str] = set()
 
     # ------------------------------------------------------------------ storage
     def _key(self, kind, ns, name):
@@ -41,7 +45,22 @@ class FakeKube:
             o = self.objs.get(self._key(kind, ns, name))
             return copy.deepcopy(o) if o else None
 
+    def _review(self, kind, obj):
+        obj = copy.deepcopy(obj)
+        spec = obj.get("spec") or {}
+        if kind == "TokenReview":
+            user = self.tokens.get(spec.get("token", ""))
+            obj["status"] = {"authenticated": user is not None, "user": {"username": user or ""}}
+        else:
+            nra = spec.get("nonResourceAttributes") or {}
+            ok = (spec.get("user") in self.metrics_readers and nra.get("path") == "/metrics"
+                  and nra.get("verb") == "get")
+            obj["status"] = {"allowed": ok}
+        return obj
+
     def create(self, kind, ns, obj):
+        if kind in ("TokenReview", "SubjectAccessReview"):
+            return self._review(kind, obj)
         with self.mu:
             obj = copy.deepcopy(obj)
             md = obj.setdefault("metadata", {})

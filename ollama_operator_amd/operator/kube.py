@@ -41,6 +41,9 @@ KINDS = {
     "Event": ("/api/v1", "events", True),
     "Lease": ("/apis/coordination.k8s.io/v1", "leases", True),
     "CustomResourceDefinition": ("/apis/apiextensions.k8s.io/v1", "customresourcedefinitions", False),
+    # authn / authz reviews for the secure metrics endpoint (create-only, cluster scoped)
+    "TokenReview": ("/apis/authentication.k8s.io/v1", "tokenreviews", False),
+    "SubjectAccessReview": ("/apis/authorization.k8s.io/v1", "subjectaccessreviews", False),
 }
 
 

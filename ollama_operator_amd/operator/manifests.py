@@ -4,8 +4,13 @@ CRD, RBAC, manager Deployment, samples, kustomize overlays and the single-file i
 the committed files are current.
 
 Differences from the reference, on purpose: Events RBAC is cluster-wide (reference only grants it
-in the operator namespace); metrics are served directly (no
-kube-rbac-proxy sidecar image); model pods request `amd.com/gpu`.
+in the operator namespace); model pods request `amd.com/gpu`; and the
+metrics endpoint is protected by the manager itself (`--metrics-secure`: TLS + TokenReview +
+SubjectAccessReview, operator/controller.py `MetricsAuth`) instead of a kube-rbac-proxy sidecar
+image (reference config/default/manager_auth_proxy_patch.yaml:11-39) -- same :8443 https port, same
+`metrics-reader` ClusterRole for scrapers (config/rbac/auth_proxy_client_clusterrole.yaml), same
+tokenreview/subjectaccessreview grant (config/rbac/auth_proxy_role.yaml), and the same optional,
+off-by-default Prometheus ServiceMonitor (config/prometheus/monitor.yaml:1-25).
 """
 from __future__ import annotations
 
@@ -81,9 +86,37 @@ def rbac() -> dict[str, list[dict]]:
                                   "metadata": {"name": "controller-manager-metrics-service", "namespace": "system",
                                                "labels": {"control-plane": "controller-manager"}},
                                   "spec": {"selector": {"control-plane": "controller-manager"},
-                                           "ports": [{"name": "http", "port": 8080, "targetPort": 8080,
+                                           "ports": [{"name": "https", "port": 8443, "targetPort": "https",
                                                       "protocol": "TCP"}]}}],
+        # the manager authorises scrapes itself: it may create token / access reviews
+        "metrics_auth_role.yaml": [{"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "ClusterRole",
+                                    "metadata": {"name": "metrics-auth-role"},
+                                    "rules": [{"apiGroups": ["authentication.k8s.io"], "resources": ["tokenreviews"],
+                                               "verbs": ["create"]},
+                                              {"apiGroups": ["authorization.k8s.io"],
+                                               "resources": ["subjectaccessreviews"], "verbs": ["create"]}]}],
+        "metrics_auth_role_binding.yaml": [{
+            "apiVersion": "rbac.authorization.k8s.io/v1", "kind": "ClusterRoleBinding",
+            "metadata": {"name": "metrics-auth-rolebinding"},
+            "roleRef": {"apiGroup": "rbac.authorization.k8s.io", "kind": "ClusterRole", "name": "metrics-auth-role"},
+            "subjects": [{"kind": "ServiceAccount", "name": "controller-manager", "namespace": "system"}]}],
+        # bind this to a Prometheus service account to let it scrape
+        "metrics_reader_role.yaml": [{"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "ClusterRole",
+                                      "metadata": {"name": "metrics-reader"},
+                                      "rules": [{"nonResourceURLs": ["/metrics"], "verbs": ["get"]}]}],
     }
+
+
+def prometheus() -> list[dict]:
+    """ServiceMonitor for the prometheus-operator (reference config/prometheus/monitor.yaml:1-25);
+    not part of the default overlay or the installer, as in the reference."""
+    return [{"apiVersion": "monitoring.coreos.com/v1", "kind": "ServiceMonitor",
+             "metadata": {"name": "controller-manager-metrics-monitor", "namespace": "system",
+                          "labels": {"control-plane": "controller-manager"}},
+             "spec": {"endpoints": [{"path": "/metrics", "port": "https", "scheme": "https",
+                                     "bearerTokenFile": "/var/run/secrets/kubernetes.io/serviceaccount/token",
+                                     "tlsConfig": {"insecureSkipVerify": True}}],
+                      "selector": {"matchLabels": {"control-plane": "controller-manager"}}}}]
 
 
 def manager() -> list[dict]:
@@ -107,10 +140,10 @@ def manager() -> list[dict]:
                         "name": "manager", "image": OPERATOR_IMAGE,
                         "command": ["python3", "-m", "ollama_operator_amd.operator"],
                         "args": ["--leader-elect", "--health-probe-bind-address=:8081",
-                                 "--metrics-bind-address=:8080"],
+                                 "--metrics-bind-address=:8443", "--metrics-secure"],
                         "env": [{"name": "OMX_SERVER_IMAGE", "value": SERVER_IMAGE},
                                 {"name": "POD_NAMESPACE", "valueFrom": {"fieldRef": {"fieldPath": "metadata.namespace"}}}],
-                        "ports": [{"containerPort": 8080, "name": "metrics"}],
+                        "ports": [{"containerPort": 8443, "name": "https", "protocol": "TCP"}],
                         "securityContext": {"allowPrivilegeEscalation": False, "capabilities": {"drop": ["ALL"]}},
                         "livenessProbe": {"httpGet": {"path": "/healthz", "port": 8081},
                                           "initialDelaySeconds": 15, "periodSeconds": 20},
@@ -146,7 +179,10 @@ def kustomizations() -> dict[str, dict]:
     return {
         "config/default/kustomization.yaml": {
             "namespace": NAMESPACE, "namePrefix": PREFIX,
+            # add "../prometheus" to scrape with the prometheus-operator (off by default, as in the
+            # reference config/default/kustomization.yaml:26-27)
             "resources": ["../crd", "../rbac", "../manager"]},
+        "config/prometheus/kustomization.yaml": {"resources": ["monitor.yaml"]},
         "config/crd/kustomization.yaml": {"resources": ["bases/ollama.ayaka.io_models.yaml"]},
         "config/rbac/kustomization.yaml": {"resources": sorted(rbac())},
         "config/manager/kustomization.yaml": {
@@ -188,6 +224,7 @@ def render_all() -> dict[str, str]:
     files["config/manager/manager.yaml"] = _dump(manager())
     for n, objs in samples().items():
         files[f"config/samples/{n}"] = _dump(objs)
+    files["config/prometheus/monitor.yaml"] = _dump(prometheus())
     for n, k in kustomizations().items():
         files[n] = yaml.safe_dump({"apiVersion": "kustomize.config.k8s.io/v1beta1", "kind": "Kustomization", **k},
                                   sort_keys=False)

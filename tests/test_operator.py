@@ -234,3 +234,76 @@ def test_crd_schema_contract():
         assert f in props["properties"]
     assert props["properties"]["persistentVolumeClaim"]["required"] == ["claimName"]
     assert R.model_app_name("x") == "ollama-model-x"
+
+
+def test_secure_metrics_tokenreview_and_sar():
+    """--metrics-secure: TLS + TokenReview + SubjectAccessReview (kube-rbac-proxy semantics)."""
+    import shutil
+    import ssl
+    import urllib.error
+    import urllib.request
+
+    import pytest
+    if shutil.which("openssl") is None:
+        pytest.skip("openssl not available")
+    from ollama_operator_amd.operator.controller import Manager, serve_probes
+    from ollama_operator_amd.operator.e2e import free_port
+    k = FakeKube()
+    k.tokens = {"good": "system:serviceaccount:monitoring:prometheus", "nobody": "alice"}
+    k.metrics_readers = {"system:serviceaccount:monitoring:prometheus"}
+    mgr = Manager(k)
+    port = free_port()
+    servers = serve_probes(mgr, "0", f"127.0.0.1:{port}", secure=True)
+    ctx = ssl.create_default_context()
+    ctx.check_hostname = False
+    ctx.verify_mode = ssl.CERT_NONE
+
+    def get(token):
+        req = urllib.request.Request(f"https://127.0.0.1:{port}/metrics")
+        if token:
+            req.add_header("Authorization", f"Bearer {token}")
+        try:
+            with urllib.request.urlopen(req, context=ctx, timeout=10) as r:
+                return r.status, r.read()
+        except urllib.error.HTTPError as e:
+            return e.code, b""
+    try:
+        assert get(None)[0] == 401
+        assert get("forged")[0] == 401
+        assert get("nobody")[0] == 403
+        code, body = get("good")
+        assert code == 200 and b"controller_runtime_reconcile_total" in body
+    finally:
+        for s in servers:
+            s.shutdown()
+
+
+def test_sigterm_drains_and_releases_lease():
+    """SIGTERM (reference ctrl.SetupSignalHandler, cmd/main.go:146): the leader stops, finishes its
+    work and releases the Lease so a standby takes over without waiting out the lease duration."""
+    import os
+    import signal
+    import threading
+
+    from ollama_operator_amd.operator.controller import Manager, run_until_signal
+    k = FakeKube()
+    a = Manager(k, leader_elect=True, lease_namespace="ollama-operator-system", identity="a")
+    a.start(watch=False)
+    for _ in range(100):
+        if a.is_leader:
+            break
+        time.sleep(0.05)
+    assert a.is_leader
+    threading.Timer(0.3, os.kill, (os.getpid(), signal.SIGTERM)).start()
+    run_until_signal(a)  # returns after the graceful shutdown
+    lease = k.get("Lease", "ollama-operator-system", "300b498d.ayaka.io")
+    assert lease["spec"]["holderIdentity"] == "" and not a.is_leader
+    assert all(not t.is_alive() for t in a.threads)
+    b = Manager(k, leader_elect=True, lease_namespace="ollama-operator-system", identity="b")
+    b.start(watch=False)
+    for _ in range(100):
+        if b.is_leader:
+            break
+        time.sleep(0.05)
+    assert b.is_leader  # immediate takeover, no 15 s lease wait
+    b.shutdown()
