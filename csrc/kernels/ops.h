@@ -151,6 +151,24 @@ void moe_sort(const int* eids, int n_pairs, int X, int* rows, int* tiles, int* n
 void moe_gemm(const GemvParams& P, hipStream_t s);
 constexpr int MOE_TILE_M = 128;
 
+// One-shot all-reduce / all-gather over peer-mapped (hipIpc) slabs for TP decode (allreduce.hip)
+constexpr int AR_MAX_RANKS = 8;
+constexpr int AR_MAX_BLOCKS = 64;
+constexpr int AR_SLABS = 3;  // call sites rotate over 3 slabs: one barrier per call suffices
+struct ARParams {
+  float* data[AR_MAX_RANKS];      // rank r's slab buffer [AR_SLABS][slab_floats] (peer-mapped for r != rank)
+  unsigned* flags[AR_MAX_RANKS];  // rank r's flags [AR_MAX_BLOCKS][AR_MAX_RANKS] (uncached, peer-mapped)
+  unsigned* epoch;                // this rank's per-block barrier counters [AR_MAX_BLOCKS] (zeroed once)
+  int* err;                       // this rank's error word: 1 + peer that never arrived (0 = ok)
+  int rank, world;
+  long long slab_floats;
+  unsigned long long timeout_ticks;  // 100 MHz wall-clock ticks a barrier may wait
+};
+// y[0:n] += sum_r slab_r[slab][0:n]  (n % 4 == 0), same bits on every rank
+void ar_allreduce_add(const ARParams& P, int slab, float* y, int n, hipStream_t s);
+// out[row][r * n_local + j] = slab_r[slab][row * n_local + j]
+void ar_allgather(const ARParams& P, int slab, float* out, int rows, int n_local, int ld_out, hipStream_t s);
+
 // small elementwise helpers
 void add_inplace(float* y, const float* x, long long n, hipStream_t s);
 void rmsnorm(const float* x, const float* w, float eps, int rows, int n, float* out, hipStream_t s);

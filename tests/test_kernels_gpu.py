@@ -330,3 +330,27 @@ def test_repeat_penalty_changes_argmax():
     d["hist_count"][0] = 3
     C().sample(p, S())
     assert int(d["out"][0]) == 11
+
+
+@pytest.mark.parametrize("qt", QTYPES)
+@pytest.mark.parametrize("B", [2, 4, 5, 8, 15])
+@pytest.mark.parametrize("K,norm", [(4096, 1), (4096, 0), (11008, 0), (2560, 2), (8192, 1)])
+def test_gemv_batch_rows(qt, B, K, norm):
+    """Continuous-batching GEMV (gemv_batch.hip: BT rows per block, register or x-first LDS
+    prologue) against fp32 torch, with no norm / RMSNorm / LayerNorm prologues and a residual add."""
+    N = 400  # partial last 16-row tile
+    m = QM(qt, N, K, seed=K + 7 * B + norm)
+    x = torch.randn(B, K, device="cuda") + 0.2
+    nw = torch.rand(K, device="cuda") + 0.5 if norm else None
+    nb = torch.randn(K, device="cuda") * 0.1 if norm == 2 else None
+    y0 = torch.randn(B, N, device="cuda")
+    y = y0.clone()
+    gemv(m, x, norm=norm, nw=nw, nb=nb, epi=1, y=y)
+    if norm == 1:
+        xn = x * torch.rsqrt(x.pow(2).mean(-1, keepdim=True) + 1e-5) * nw
+    elif norm == 2:
+        xn = torch.nn.functional.layer_norm(x, (K,), nw, nb, 1e-5)
+    else:
+        xn = x
+    ref = xn @ m.w.T
+    assert rel(y - y0, ref) < 1e-2
