@@ -6,6 +6,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <cstring>
 #include <memory>
 #include <stdexcept>
 
@@ -44,6 +45,70 @@ static void check_attn(int H, int n_kv, int D) {
   const int G = H / n_kv;
   if (G != 1 && G != 2 && G != 4 && G != 8) throw std::runtime_error("unsupported GQA group size");
   if (D != 64 && D != 80 && D != 96 && D != 128) throw std::runtime_error("unsupported head dim");
+}
+
+static ARParams ar_params(py::dict d) {
+  ARParams P{};
+  auto data = d["data"].cast<std::vector<uintptr_t>>();
+  auto flags = d["flags"].cast<std::vector<uintptr_t>>();
+  P.rank = d["rank"].cast<int>();
+  P.world = d["world"].cast<int>();
+  if (P.world < 1 || P.world > AR_MAX_RANKS || (int)data.size() != P.world || (int)flags.size() != P.world ||
+      P.rank < 0 || P.rank >= P.world)
+    throw std::runtime_error("ar: bad rank / world / peer pointer lists");
+  for (int r = 0; r < P.world; ++r) {
+    if (!data[r] || !flags[r]) throw std::runtime_error("ar: null peer pointer");
+    P.data[r] = Pp<float>(data[r]);
+    P.flags[r] = Pp<unsigned>(flags[r]);
+  }
+  P.epoch = Pp<unsigned>(d["epoch"].cast<uintptr_t>());
+  P.err = Pp<int>(d["err"].cast<uintptr_t>());
+  P.slab_floats = d["slab_floats"].cast<long long>();
+  P.timeout_ticks = d["timeout_ticks"].cast<unsigned long long>();
+  if (!P.epoch || !P.err || P.slab_floats <= 0 || P.slab_floats % 4) throw std::runtime_error("ar: bad workspace");
+  return P;
+}
+
+static void hip_check(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+static StepInputs step_inputs(py::dict d) {
+  StepInputs in;
+  auto ptr = [&](const char* k) -> uintptr_t { return d.contains(k) ? d[k].cast<uintptr_t>() : 0; };
+  in.B = d.contains("B") ? d["B"].cast<int>() : 0;
+  in.tokens = Pp<const int>(ptr("tokens"));
+  in.pos = Pp<const int>(ptr("pos"));
+  in.slot = Pp<const int>(ptr("slot"));
+  in.q_len = Pp<const int>(ptr("q_len"));
+  in.q_seq = Pp<const int>(ptr("q_seq"));
+  in.block_table = Pp<const int>(ptr("block_table"));
+  in.max_blocks = d["max_blocks"].cast<int>();
+  in.bs = d["bs"].cast<int>();
+  in.prefill = d.contains("prefill") ? d["prefill"].cast<int>() : 0;
+  in.n_logits = d.contains("n_logits") ? d["n_logits"].cast<int>() : 0;
+  in.logit_idx = Pp<const int>(ptr("logit_idx"));
+  in.logits = Pp<float>(ptr("logits"));
+  in.full_logits = Pp<float>(ptr("full_logits"));
+  in.ld_full = d.contains("ld_full") ? d["ld_full"].cast<int>() : 0;
+  return in;
+}
+
+enum { ST_FORWARD = 0, ST_EMBED = 1, ST_ATTN = 2, ST_FFN = 3, ST_HEAD = 4, ST_FORWARD_TP = 5 };
+
+static void run_stage(Executor& e, int stage, int layer, const StepInputs& in, hipStream_t s) {
+  if (in.B > e.ws.max_B) throw std::runtime_error("batch exceeds workspace max_B");
+  if ((stage == ST_ATTN || stage == ST_FFN) && (layer < 0 || layer >= (int)e.layers.size()))
+    throw std::runtime_error("layer index");
+  switch (stage) {
+    case ST_FORWARD: e.forward(in, s); break;
+    case ST_EMBED: e.embed(in, s); break;
+    case ST_ATTN: e.attn_block(layer, in, s); break;
+    case ST_FFN: e.ffn_block(layer, in, s); break;
+    case ST_HEAD: e.head(in, s); break;
+    case ST_FORWARD_TP: e.forward_tp(in, s); break;
+    default: throw std::runtime_error("unknown stage");
+  }
 }
 
 PYBIND11_MODULE(_C, m) {
@@ -306,30 +371,104 @@ PYBIND11_MODULE(_C, m) {
         e.ws.defer = defer;
       }, py::arg("n"), py::arg("defer") = 0)
       .def("run", [](Executor& e, const std::string& what, int layer, py::dict d, uintptr_t stream) {
-        StepInputs in;
-        auto ptr = [&](const char* k) -> uintptr_t { return d.contains(k) ? d[k].cast<uintptr_t>() : 0; };
-        in.B = d["B"].cast<int>();
-        in.tokens = Pp<const int>(ptr("tokens"));
-        in.pos = Pp<const int>(ptr("pos"));
-        in.slot = Pp<const int>(ptr("slot"));
-        in.q_len = Pp<const int>(ptr("q_len"));
-        in.q_seq = Pp<const int>(ptr("q_seq"));
-        in.block_table = Pp<const int>(ptr("block_table"));
-        in.max_blocks = d["max_blocks"].cast<int>();
-        in.bs = d["bs"].cast<int>();
-        in.prefill = d.contains("prefill") ? d["prefill"].cast<int>() : 0;
-        in.n_logits = d.contains("n_logits") ? d["n_logits"].cast<int>() : 0;
-        in.logit_idx = Pp<const int>(ptr("logit_idx"));
-        in.logits = Pp<float>(ptr("logits"));
-        if (in.B > e.ws.max_B) throw std::runtime_error("batch exceeds workspace max_B");
-        hipStream_t s = S(stream);
-        if (what == "forward") e.forward(in, s);
-        else if (what == "embed") e.embed(in, s);
-        else if (what == "attn") e.attn_block(layer, in, s);
-        else if (what == "ffn") e.ffn_block(layer, in, s);
-        else if (what == "head") e.head(in, s);
-        else throw std::runtime_error("unknown stage " + what);
-      });
+        static const std::pair<const char*, int> names[] = {{"forward", ST_FORWARD}, {"embed", ST_EMBED},
+            {"attn", ST_ATTN}, {"ffn", ST_FFN}, {"head", ST_HEAD}, {"forward_tp", ST_FORWARD_TP}};
+        for (const auto& nm : names)
+          if (what == nm.first) return run_stage(e, nm.second, layer, step_inputs(d), S(stream));
+        throw std::runtime_error("unknown stage " + what);
+      })
+      // pre-bound inputs: bind the step buffers once, then each stage call passes only integers
+      .def("set_inputs", [](Executor& e, py::dict d) { e.bound = step_inputs(d); })
+      .def("step", [](Executor& e, int stage, int layer, int B, int n_logits, bool use_idx, bool prefill,
+                      uintptr_t stream) {
+        StepInputs in = e.bound;
+        in.B = B;
+        in.n_logits = n_logits;
+        if (!use_idx) in.logit_idx = nullptr;
+        in.prefill = prefill ? 1 : 0;
+        run_stage(e, stage, layer, in, S(stream));
+      })
+      .def("set_ar", [](Executor& e, py::dict d) {
+        e.ws.ar = ar_params(d);
+        e.ws.ar_on = 1;
+      })
+      .def("clear_ar", [](Executor& e) { e.ws.ar_on = 0; })
+      .def("ar_fits", &Executor::ar_fits);
+  m.attr("ST_FORWARD") = (int)ST_FORWARD;
+  m.attr("ST_EMBED") = (int)ST_EMBED;
+  m.attr("ST_ATTN") = (int)ST_ATTN;
+  m.attr("ST_FFN") = (int)ST_FFN;
+  m.attr("ST_HEAD") = (int)ST_HEAD;
+  m.attr("ST_FORWARD_TP") = (int)ST_FORWARD_TP;
+
+  // ------------------------------------------------------------------ custom all-reduce (TP decode)
+  m.attr("AR_MAX_RANKS") = AR_MAX_RANKS;
+  m.attr("AR_SLABS") = AR_SLABS;
+  // this rank's slab buffer + flags (uncached) + epoch / error words, with IPC handles of the two
+  // peer-visible allocations (bytes) for the other ranks to open
+  m.def("ar_alloc", [](long long slab_floats) {
+    if (slab_floats <= 0 || slab_floats % 4) throw std::runtime_error("ar_alloc: slab_floats must be a positive multiple of 4");
+    void *data = nullptr, *flags = nullptr, *local = nullptr;
+    const size_t dbytes = sizeof(float) * (size_t)AR_SLABS * slab_floats;
+    const size_t fbytes = sizeof(unsigned) * AR_MAX_BLOCKS * AR_MAX_RANKS;
+    hip_check(hipMalloc(&data, dbytes), "ar_alloc data");
+    hip_check(hipMemset(data, 0, dbytes), "ar_alloc memset");
+    if (hipExtMallocWithFlags(&flags, fbytes, hipDeviceMallocUncached) != hipSuccess) {
+      (void)hipGetLastError();
+      hip_check(hipMalloc(&flags, fbytes), "ar_alloc flags");
+    }
+    hip_check(hipMemset(flags, 0, fbytes), "ar_alloc memset");
+    hip_check(hipMalloc(&local, sizeof(unsigned) * AR_MAX_BLOCKS + 64), "ar_alloc local");
+    hip_check(hipMemset(local, 0, sizeof(unsigned) * AR_MAX_BLOCKS + 64), "ar_alloc memset");
+    hip_check(hipDeviceSynchronize(), "ar_alloc sync");
+    hipIpcMemHandle_t hd, hf;
+    hip_check(hipIpcGetMemHandle(&hd, data), "hipIpcGetMemHandle(data)");
+    hip_check(hipIpcGetMemHandle(&hf, flags), "hipIpcGetMemHandle(flags)");
+    py::dict r;
+    r["data"] = reinterpret_cast<uintptr_t>(data);
+    r["flags"] = reinterpret_cast<uintptr_t>(flags);
+    r["epoch"] = reinterpret_cast<uintptr_t>(local);
+    r["err"] = reinterpret_cast<uintptr_t>(local) + sizeof(unsigned) * AR_MAX_BLOCKS;
+    r["data_handle"] = py::bytes(reinterpret_cast<const char*>(&hd), sizeof(hd));
+    r["flags_handle"] = py::bytes(reinterpret_cast<const char*>(&hf), sizeof(hf));
+    return r;
+  });
+  m.def("ar_open", [](py::bytes h) {
+    std::string s = h;
+    hipIpcMemHandle_t hh;
+    if (s.size() != sizeof(hh)) throw std::runtime_error("ar_open: bad handle size");
+    memcpy(&hh, s.data(), sizeof(hh));
+    void* p = nullptr;
+    hip_check(hipIpcOpenMemHandle(&p, hh, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
+    return reinterpret_cast<uintptr_t>(p);
+  });
+  m.def("ar_close", [](uintptr_t p) { hip_check(hipIpcCloseMemHandle(Pp<void>(p)), "hipIpcCloseMemHandle"); });
+  m.def("ar_free", [](uintptr_t p) { hip_check(hipFree(Pp<void>(p)), "hipFree"); });
+  m.def("ar_error", [](uintptr_t err) {  // host read of the error word (synchronous)
+    int v = 0;
+    hip_check(hipMemcpy(&v, Pp<void>(err), sizeof(int), hipMemcpyDeviceToHost), "ar_error");
+    return v;
+  });
+  m.def("wall_clock_khz", []() {
+    int dev = 0, khz = 0;
+    hip_check(hipGetDevice(&dev), "hipGetDevice");
+    hip_check(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev), "wall clock rate");
+    return khz;
+  });
+  m.def("copy_d2d", [](uintptr_t dst, uintptr_t src, size_t bytes, uintptr_t stream) {
+    hip_check(hipMemcpyAsync(Pp<void>(dst), Pp<const void>(src), bytes, hipMemcpyDeviceToDevice, S(stream)), "copy_d2d");
+  });
+  m.def("ar_allreduce_add", [](py::dict d, int slab, uintptr_t y, int n, uintptr_t stream) {
+    ARParams P = ar_params(d);
+    if (slab < 0 || slab >= AR_SLABS || n % 4 || n > P.slab_floats) throw std::runtime_error("ar_allreduce_add: bad slab / n");
+    ar_allreduce_add(P, slab, Pp<float>(y), n, S(stream));
+  });
+  m.def("ar_allgather", [](py::dict d, int slab, uintptr_t out, int rows, int n_local, int ld_out, uintptr_t stream) {
+    ARParams P = ar_params(d);
+    if (slab < 0 || slab >= AR_SLABS || (long long)rows * n_local > P.slab_floats || ld_out < n_local * P.world)
+      throw std::runtime_error("ar_allgather: bad slab / shape");
+    ar_allgather(P, slab, Pp<float>(out), rows, n_local, ld_out, S(stream));
+  });
 
   m.attr("NORM_NONE") = (int)NORM_NONE;
   m.attr("NORM_RMS") = (int)NORM_RMS;

@@ -44,7 +44,9 @@ __device__ __forceinline__ bool ar_barrier(const ARParams& P) {
     __hip_atomic_store(P.flags[t] + b * AR_MAX_RANKS + P.rank, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     unsigned* mine = P.flags[P.rank] + b * AR_MAX_RANKS + t;
     const unsigned long long t0 = wall_clock64();
-    while ((int)(__hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - e) < 0) {
+    // a barrier that already timed out on this rank fails fast instead of waiting again
+    const bool failed = __hip_atomic_load(P.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+    while (!failed && (int)(__hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - e) < 0) {
       if (wall_clock64() - t0 > P.timeout_ticks) {
         ok = false;
         __hip_atomic_store(P.err, 1 + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

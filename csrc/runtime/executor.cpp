@@ -107,7 +107,7 @@ void Executor::attn_block(int i, const StepInputs& in, hipStream_t s) {
   O.bias = L.bo;
   if (cfg.tp > 1) {
     O.epi = EPI_STORE;
-    O.y = ws.ypart;
+    O.y = tp_dst(0, B);
   } else {
     O.epi = EPI_ADD;
     O.y = ws.resid;
@@ -119,7 +119,7 @@ void Executor::attn_block(int i, const StepInputs& in, hipStream_t s) {
 void Executor::ffn_block(int i, const StepInputs& in, hipStream_t s) {
   const LayerW& L = layers[i];
   const int B = in.B, E = cfg.E, F = cfg.F;
-  float* dst = cfg.tp > 1 ? ws.ypart : ws.resid;
+  float* dst = cfg.tp > 1 ? tp_dst(1, B) : ws.resid;
   const int dst_epi = cfg.tp > 1 ? EPI_STORE : EPI_ADD;
   if (cfg.arch == 1) {  // phi2: up+GELU already done in attn_block
     GemvParams Dn = base_params(L.wdown, B, ws.hbuf, F, ws);
@@ -163,7 +163,7 @@ void Executor::ffn_block(int i, const StepInputs& in, hipStream_t s) {
       grouped(G);
       G.moe_gather = 1;
       moe_gemm(G, s);
-      if (cfg.tp > 1) hipMemsetAsync(ws.ypart, 0, sizeof(float) * (size_t)B * E, s);
+      if (cfg.tp > 1) hipMemsetAsync(dst, 0, sizeof(float) * (size_t)B * E, s);
       GemvParams Dn = base_params(L.down_exps, pairs, ws.hbuf, F, ws);
       Dn.epi = EPI_ADD;  // routing-weighted, atomically accumulated per token
       Dn.y = dst;
@@ -186,7 +186,7 @@ void Executor::ffn_block(int i, const StepInputs& in, hipStream_t s) {
     G.n_sel = k;
     G.y_sel_stride = F;
     gemv(G, s);
-    if (cfg.tp > 1) hipMemsetAsync(ws.ypart, 0, sizeof(float) * (size_t)B * E, s);
+    if (cfg.tp > 1) hipMemsetAsync(dst, 0, sizeof(float) * (size_t)B * E, s);
     GemvParams Dn = base_params(L.down_exps, B, ws.hbuf, k * F, ws);
     Dn.epi = EPI_ADD;  // expert-weighted, atomically accumulated
     Dn.y = dst;
@@ -232,6 +232,40 @@ void Executor::head(const StepInputs& in, hipStream_t s) {
   P.y = in.logits;
   P.ldy = lm_head.N;
   gemv(P, s);
+}
+
+float* Executor::tp_dst(int slab, int B) const {
+  if (ar_active_) return ws.ar.data[ws.ar.rank] + (long long)slab * ws.ar.slab_floats;
+  return ws.ypart;  // RCCL path: the caller all-reduces ypart between stages
+}
+
+bool Executor::ar_fits(int B) const {
+  return ws.ar_on && (long long)B * cfg.E <= ws.ar.slab_floats && (long long)B * cfg.V <= ws.ar.slab_floats;
+}
+
+void Executor::forward_tp(const StepInputs& in, hipStream_t s) {
+  if (cfg.tp <= 1 || !ws.ar_on) throw std::runtime_error("forward_tp needs tp > 1 and the custom all-reduce");
+  if (!ar_fits(in.B)) throw std::runtime_error("forward_tp: batch exceeds the all-reduce slabs");
+  if (in.B > ws.max_B) throw std::runtime_error("batch exceeds workspace");
+  const int n = in.B * cfg.E;
+  struct Active {  // the stages write partial sums to the slabs only inside forward_tp
+    int& f;
+    explicit Active(int& x) : f(x) { f = 1; }
+    ~Active() { f = 0; }
+  } active(ar_active_);
+  embed(in, s);
+  for (int i = 0; i < cfg.n_layer; ++i) {
+    attn_block(i, in, s);
+    ar_allreduce_add(ws.ar, 0, ws.resid, n, s);  // resid += sum of the ranks' O partials
+    ffn_block(i, in, s);
+    ar_allreduce_add(ws.ar, 1, ws.resid, n, s);
+  }
+  if (in.n_logits > 0) {
+    StepInputs h = in;
+    h.logits = ws.ar.data[ws.ar.rank] + 2LL * ws.ar.slab_floats;  // this rank's vocab shard -> slab 2
+    head(h, s);
+    ar_allgather(ws.ar, 2, in.full_logits, in.n_logits, cfg.V, in.ld_full, s);
+  }
 }
 
 void Executor::forward(const StepInputs& in, hipStream_t s) {

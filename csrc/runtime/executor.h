@@ -63,6 +63,10 @@ struct Workspace {
   int max_B = 0;
   int n_splits = 1;
   int defer = 0;             // B == 1: attention leaves n_splits partials, the O GEMV merges them
+  // TP decode: one-shot all-reduce over peer-mapped slabs (allreduce.hip). The O / down projections
+  // write their partial sums into this rank's slab 0 / 1, the vocab-sharded LM head into slab 2.
+  ARParams ar{};
+  int ar_on = 0;
 };
 
 struct StepInputs {
@@ -79,6 +83,8 @@ struct StepInputs {
   int n_logits = 0;               // rows that need logits
   const int* logit_idx = nullptr; // [n_logits] (null = first n_logits rows)
   float* logits = nullptr;        // [n_logits][V]
+  float* full_logits = nullptr;   // TP: [n_logits][ld_full] all-gathered vocab
+  int ld_full = 0;
 };
 
 class Executor {
@@ -97,7 +103,14 @@ class Executor {
   void attn_block(int i, const StepInputs& in, hipStream_t s);
   void ffn_block(int i, const StepInputs& in, hipStream_t s);
   void head(const StepInputs& in, hipStream_t s);
-  void forward(const StepInputs& in, hipStream_t s);  // tp == 1 only
+  void forward(const StepInputs& in, hipStream_t s);     // tp == 1 only
+  void forward_tp(const StepInputs& in, hipStream_t s);  // tp > 1, custom all-reduce (graph-capturable)
+  bool ar_fits(int B) const;                             // decode batch B fits the AR slabs
+  StepInputs bound{};                                    // pre-bound step inputs (set_inputs)
+
+ private:
+  float* tp_dst(int slab, int B) const;  // where a row-parallel projection leaves its partial sums
+  int ar_active_ = 0;
 };
 
 }  // namespace omx

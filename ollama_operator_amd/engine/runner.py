@@ -62,21 +62,24 @@ class NativeExec:
                              moe_ntiles=p(r.moe_ntiles),
                              gws_elems=r.gws.numel(), max_B=r.max_batch,
                              n_splits=1))
-        self.inputs = dict(tokens=p(r.d_tokens), pos=p(r.d_pos), slot=p(r.d_slot), q_len=p(r.d_qlen),
-                           q_seq=p(r.d_qseq), block_table=p(r.d_block_table), max_blocks=r.max_blocks,
-                           bs=r.block_size, logits=p(r.logits))
-        self.logit_idx_ptr = p(r.d_logit_idx)
+        # step buffers bound once: every stage call below passes integers only
+        e.set_inputs(dict(tokens=p(r.d_tokens), pos=p(r.d_pos), slot=p(r.d_slot), q_len=p(r.d_qlen),
+                          q_seq=p(r.d_qseq), block_table=p(r.d_block_table), max_blocks=r.max_blocks,
+                          bs=r.block_size, logits=p(r.logits), logit_idx=p(r.d_logit_idx),
+                          full_logits=p(r.full_logits), ld_full=r.full_logits.shape[1]))
+        if r.ar is not None:
+            e.set_ar(r.ar.params)
+        self.stages = dict(forward=C.ST_FORWARD, embed=C.ST_EMBED, attn=C.ST_ATTN, ffn=C.ST_FFN, head=C.ST_HEAD,
+                           forward_tp=C.ST_FORWARD_TP)
+
+    def ar_fits(self, B: int) -> bool:
+        return self.exe.ar_fits(B)
 
     def run(self, stage: str, layer: int, B: int, n_logits: int = 0, use_idx: bool = False,
             prefill: bool = False):
-        d = dict(self.inputs)
-        d["B"] = B
-        d["prefill"] = int(prefill)
-        d["n_logits"] = n_logits
-        d["logit_idx"] = self.logit_idx_ptr if use_idx else 0
         S, defer = self.r.split_plan(B)
         self.exe.set_splits(S, defer)
-        self.exe.run(stage, layer, d, stream_handle())
+        self.exe.step(self.stages[stage], layer, B, n_logits, use_idx, prefill, stream_handle())
 
 
 @dataclass
@@ -174,9 +177,17 @@ class Runner:
         self._defer_ok = (self.is_gpu and os.environ.get("OMX_DEFER_MERGE", "1") != "0" and
                           native().gemv_merge_supported(1, Eq, loc["D"], 8) and self.n_splits(1) >= 8)
         self._decode_S = 0
+        # TP decode collectives: one-shot all-reduce over peer-mapped slabs (parallel/custom_ar.py),
+        # decode-size messages only (<= ~1 MB); prefill chunks keep RCCL
+        self.ar = None
+        if self.is_gpu and tp_size > 1 and os.environ.get("OMX_CUSTOM_AR", "1") != "0":
+            from ..parallel.custom_ar import CustomAllReduce
+            rows = max(1, min(max_batch, max(max_seqs, 16), (1 << 18) // max(E, Vl)))
+            self.ar = CustomAllReduce(tp_group, tp_rank, tp_size, rows * max(E, Vl))
         self.exe = NativeExec(self) if self.is_gpu else TorchExecutor(self)
-        if use_graphs is None:  # TP steps run Python-level collectives between executor stages
-            use_graphs = self.is_gpu and tp_size == 1 and os.environ.get("OMX_NO_GRAPH", "0") != "1"
+        if use_graphs is None:  # TP: graph-captured only through the custom all-reduce
+            use_graphs = (self.is_gpu and (tp_size == 1 or self.ar is not None) and
+                          os.environ.get("OMX_NO_GRAPH", "0") != "1")
         self.use_graphs = use_graphs
         self.graphs: dict[int, torch.cuda.CUDAGraph] = {}
         self._host_sampler: dict[int, tuple] = {}
@@ -187,6 +198,12 @@ class Runner:
             self._tok_host = torch.zeros(max_batch, dtype=torch.int32).pin_memory()
             self._tok_ring = torch.zeros(4, dtype=torch.int32).pin_memory()  # sampled tokens, per step
         self.load_s = time.perf_counter() - t0
+
+    def close(self) -> None:
+        """Release the TP collective workspace (all ranks call this together)."""
+        if self.ar is not None:
+            self.ar.close()
+            self.ar = None
 
     # ------------------------------------------------------------------ sizing helpers
     def n_splits(self, B: int) -> int:
@@ -228,6 +245,9 @@ class Runner:
         """prefill=True: the B rows are one sequence's contiguous positions (MFMA flash attention)."""
         if self.tp_size == 1:
             self.exe.run("forward", 0, B, n_logits, use_idx, prefill)
+            return
+        if self.ar is not None and self.exe.ar_fits(B):  # whole TP step in one native call
+            self.exe.run("forward_tp", 0, B, n_logits, use_idx, prefill)
             return
         import torch.distributed as dist
         self.exe.run("embed", 0, B)
@@ -552,6 +572,8 @@ class Runner:
         finally:
             if ctrl is not None and ctrl.leader:
                 ctrl.signal(False)  # generation over (also when the consumer closed us early)
+            if self.ar is not None:
+                self.ar.check()  # a peer that missed a barrier timed the step out: fail loudly
             if times is not None:
                 times.gen_tokens = n
                 times.gen_s = time.perf_counter() - t1

@@ -21,6 +21,7 @@ import os
 import socket
 import subprocess
 import sys
+import threading
 import time
 
 import torch
@@ -75,6 +76,7 @@ class TPWorld:
     compute_group: object
     ctrl: TPControl
     workers: list
+    stopping: threading.Event = dataclasses.field(default_factory=threading.Event)
 
 
 def _device_for(local_rank: int) -> str:
@@ -108,10 +110,33 @@ def start_leader(size: int) -> TPWorld:
                    MASTER_PORT=str(port))
         workers.append(subprocess.Popen([sys.executable, "-m", "ollama_operator_amd.parallel.tp_worker"], env=env))
     dev, compute, ctrl = _init_groups(0, size, addr, port)
-    return TPWorld(0, size, dev, compute, TPControl(ctrl, leader=True), workers)
+    world = TPWorld(0, size, dev, compute, TPControl(ctrl, leader=True), workers)
+    threading.Thread(target=_watchdog, args=(world,), name="tp-watchdog", daemon=True).start()
+    return world
+
+
+WATCHDOG_PERIOD_S = 1.0
+
+
+def _watchdog(world: TPWorld, period: float = WATCHDOG_PERIOD_S, exit_fn=os._exit) -> None:
+    """A TP group cannot lose a rank: a dead worker leaves the leader blocked in (or timing out of)
+    the next collective while /api/tags keeps answering. Any worker exit outside shutdown ends the
+    server with a non-zero code, so the pod restarts (liveness alone would not see it)."""
+    while not world.stopping.wait(period):
+        for r, p in enumerate(world.workers, start=1):
+            rc = p.poll()
+            if rc is not None and not world.stopping.is_set():
+                print(f"tp watchdog: rank {r} exited with code {rc}; terminating the TP group", file=sys.stderr,
+                      flush=True)
+                for q in world.workers:
+                    if q.poll() is None:
+                        q.kill()
+                exit_fn(rc if rc else 1)
+                return
 
 
 def shutdown_leader(world: TPWorld) -> None:
+    world.stopping.set()
     try:
         world.ctrl.send_cmd({"op": "exit"})
     except Exception:  # noqa: BLE001 - workers may already be gone
@@ -163,6 +188,7 @@ class TPRunnerProxy:
 
     def close(self) -> None:
         self._mirror("unload")
+        self.r.close()
 
 
 def load_tp_runner(world: TPWorld, path: str, max_batch: int, max_seqs: int, ctx: int):
@@ -193,6 +219,8 @@ def worker_main() -> None:
             runner = Runner(cmd["path"], device=dev, max_batch=cmd["max_batch"], max_seqs=cmd["max_seqs"],
                             ctx=cmd["ctx"], tp_rank=rank, tp_size=size, tp_group=compute, tp_ctrl=ctrl)
         elif op == "unload":
+            if runner is not None:
+                runner.close()
             runner = None
             if dev.startswith("cuda"):
                 torch.cuda.empty_cache()

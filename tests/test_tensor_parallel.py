@@ -76,3 +76,39 @@ def test_tp_rejects_indivisible(tmp_path):
     write_random_gguf(path, preset("tiny-llama"), FileType.MOSTLY_Q4_K_M, seed=1)
     with pytest.raises(ValueError):
         DeviceWeights(path, "cpu", tp_rank=0, tp_size=2)  # K=256: one super-block cannot be split
+
+
+def test_tp_watchdog_exits_when_a_worker_dies():
+    """A dead TP worker must take the server down (non-zero), not leave it answering while hung."""
+    import subprocess
+    import sys
+    import threading
+
+    from ollama_operator_amd.parallel.tp import TPWorld, _watchdog
+    dead = subprocess.Popen([sys.executable, "-c", "import sys; sys.exit(3)"])
+    alive = subprocess.Popen([sys.executable, "-c", "import time; time.sleep(30)"])
+    dead.wait()
+    world = TPWorld(0, 3, "cpu", None, None, [alive, dead])
+    codes = []
+    t = threading.Thread(target=_watchdog, args=(world, 0.05, codes.append))
+    t.start()
+    t.join(10)
+    assert codes == [3]
+    assert alive.wait(10) is not None  # the surviving rank is killed with the group
+
+
+def test_tp_watchdog_quiet_on_shutdown():
+    import subprocess
+    import sys
+    import threading
+
+    from ollama_operator_amd.parallel.tp import TPWorld, _watchdog
+    done = subprocess.Popen([sys.executable, "-c", "pass"])
+    done.wait()
+    world = TPWorld(0, 2, "cpu", None, None, [done])
+    world.stopping.set()
+    codes = []
+    t = threading.Thread(target=_watchdog, args=(world, 0.05, codes.append))
+    t.start()
+    t.join(5)
+    assert codes == []
