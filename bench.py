@@ -26,6 +26,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 
+MODEL_LABELS = {"llama2-7b": "Llama-2-7B", "llama2-13b": "Llama-2-13B", "llama2-70b": "Llama-2-70B",
+                "mistral-7b": "Mistral-7B", "mixtral-8x7b": "Mixtral-8x7B", "phi2": "Phi-2"}
+
+
 def ensure_model(path: str, preset_name: str, ftype_name: str) -> str:
     from ollama_operator_amd.gguf.constants import FileType
     from ollama_operator_amd.models.config import preset
@@ -40,6 +44,89 @@ def ensure_model(path: str, preset_name: str, ftype_name: str) -> str:
     os.replace(tmp, path)
     open(marker, "w").close()
     return path
+
+
+def start_server(a, model_path: str):
+    """Spawn `ollama serve` (this framework's server, cli.py) as a child process. Called before this
+    process touches the GPU: a GPU-initialised parent must never fork+exec."""
+    import socket
+    import subprocess
+    with socket.socket() as s_:
+        s_.bind(("127.0.0.1", 0))
+        port = s_.getsockname()[1]
+    env = dict(os.environ)
+    env.update({"OLLAMA_HOST": f"127.0.0.1:{port}", "OLLAMA_MODELS": os.path.join(a.dir, "server-models"),
+                "OLLAMA_NUM_PARALLEL": str(a.server_parallel), "OMX_LOG_LEVEL": "warning",
+                "PYTHONPATH": ROOT + os.pathsep + env.get("PYTHONPATH", "")})
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    log = open(os.path.join(a.dir, f"server-{port}.log"), "w")
+    proc = subprocess.Popen([sys.executable, "-m", "ollama_operator_amd", "serve"], env=env, cwd=ROOT,
+                            stdout=log, stderr=subprocess.STDOUT, start_new_session=True)
+    return proc, f"http://127.0.0.1:{port}"
+
+
+def bench_server(a, url: str, model_path: str, vocab_words: int = 32000):
+    """Headline metric the way BASELINE.json defines it: `/api/generate` (stream=false) through the
+    REST server, tok/s = eval_count / eval_duration * 1e9 (reference docs getting-started.md:135-149).
+    Then `a.server_parallel` concurrent clients (continuous batching) for the aggregate."""
+    import concurrent.futures as cf
+    import random
+
+    import httpx
+    deadline = time.time() + 120
+    with httpx.Client(base_url=url, timeout=600) as c:
+        while True:
+            try:
+                if c.get("/api/version").status_code == 200:
+                    break
+            except httpx.TransportError:
+                pass
+            if time.time() > deadline:
+                raise RuntimeError("server did not come up")
+            time.sleep(0.5)
+        r = c.post("/api/create", json={"model": "bench", "modelfile": f"FROM {model_path}", "stream": False})
+        r.raise_for_status()
+        rng = random.Random(5)
+
+        def prompt():  # synthetic prompt of a.prompt tokens, passed as Ollama `context` token ids
+            return [1] + [rng.randrange(3, vocab_words) for _ in range(a.prompt - 2)]
+
+        def gen(n, p):
+            with httpx.Client(base_url=url, timeout=600) as cc:
+                d = cc.post("/api/generate", json={"model": "bench", "prompt": " a", "context": p, "raw": True, "stream": False,
+                                                   "options": {"num_predict": n, "seed": 42}}).json()
+            return d
+
+        gen(32, prompt())  # load + warm
+        d = gen(a.steps, prompt())
+        single = d["eval_count"] / d["eval_duration"] * 1e9
+        out = {"served_tok_s": round(single, 2), "eval_count": d["eval_count"],
+               "prompt_eval_count": d["prompt_eval_count"],
+               "served_ttft_ms": round(d["prompt_eval_duration"] / 1e6, 2), "num_parallel": a.server_parallel}
+        P = a.server_parallel
+        if P > 1:
+            prompts = [prompt() for _ in range(P)]
+            t0 = time.perf_counter()
+            with cf.ThreadPoolExecutor(P) as ex:
+                res = list(ex.map(lambda p: gen(a.steps, p), prompts))
+            wall = time.perf_counter() - t0
+            out["concurrent_clients"] = P
+            out["concurrent_aggregate_tok_s"] = round(sum(x["eval_count"] for x in res) / wall, 2)
+            out["concurrent_per_client_tok_s"] = [round(x["eval_count"] / x["eval_duration"] * 1e9, 2) for x in res]
+    return out
+
+
+def stop_server(proc):
+    import signal
+    try:
+        os.killpg(proc.pid, signal.SIGTERM)
+        proc.wait(timeout=30)
+    except Exception:
+        try:
+            os.killpg(proc.pid, signal.SIGKILL)
+        except Exception:
+            pass
 
 
 def bench_batched(runner, a, rank, world, sync):
@@ -110,14 +197,25 @@ def main():
     ap.add_argument("--batch-extra", type=int, default=0,
                     help="also measure continuous-batching throughput with this many concurrent sequences per "
                          "GPU (Ollama OLLAMA_NUM_PARALLEL default 4; reported under extra, 0 = skip)")
+    ap.add_argument("--via-server", type=int, default=1,
+                    help="1 (default, single-GPU runs): also measure through the REST server (/api/generate) "
+                         "and report it under extra.server")
+    ap.add_argument("--server-parallel", type=int, default=4,
+                    help="OLLAMA_NUM_PARALLEL of the spawned server (concurrent clients measured)")
     a = ap.parse_args()
-
-    import torch
-    import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    path = os.path.join(a.dir, f"{a.model}-{a.ftype.lower()}.gguf")
+    server = None
+    if a.via_server and world == 1:
+        os.makedirs(a.dir, exist_ok=True)
+        server = start_server(a, path)  # before this process touches the GPU
+
+    import torch
+    import torch.distributed as dist
+
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
@@ -125,7 +223,6 @@ def main():
     from ollama_operator_amd.engine.runner import Runner
     from ollama_operator_amd.engine.sampling import SamplingOptions
 
-    path = os.path.join(a.dir, f"{a.model}-{a.ftype.lower()}.gguf")
     if local == 0:
         ensure_model(path, a.model, a.ftype)
     if world > 1:
@@ -174,9 +271,25 @@ def main():
     batched = None
     if a.batch_extra > 1:
         batched = bench_batched(runner, a, rank, world, sync)
+    served = None
+    if server is not None:
+        weights_gb = runner.w.nbytes / 1e9
+        n_vocab = runner.cfg.n_vocab
+        del runner
+        torch.cuda.empty_cache()
+        try:
+            served = bench_server(a, server[1], path, vocab_words=n_vocab)
+            served["vs_engine"] = round(served["served_tok_s"] / value, 4)
+        except Exception as e:  # the headline line is still printed; the failure is reported
+            served = {"error": f"{type(e).__name__}: {e}"}
+        finally:
+            stop_server(server[0])
+    else:
+        weights_gb = runner.w.nbytes / 1e9
+    label = MODEL_LABELS.get(a.model, a.model) + " " + a.ftype
     if rank == 0:
         print(json.dumps({
-            "metric": "output tokens/sec Llama-2-7B Q4_K_M",
+            "metric": f"output tokens/sec {label}",
             "value": round(value, 2),
             "unit": "tokens/s",
             "n_gpus": world,
@@ -186,14 +299,14 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "Q4_K_M weights (4/6-bit), int8-dot activations, fp32 accumulate, fp16 KV",
-            "data": "synthetic prompt, random-init GGUF weights (real Q4_K_M tensor-type mix)",
-            "config": {"model": "Llama-2-7B Q4_K_M", "global_batch": world, "seq_len": ctx,
+            "dtype": f"{a.ftype} weights, int8-dot activations, fp32 accumulate, fp16 KV",
+            "data": f"synthetic prompt, random-init GGUF weights (real {a.ftype} tensor-type mix)",
+            "config": {"model": label, "global_batch": world, "seq_len": ctx,
                        "parallelism": f"dp{world}", "prompt_tokens": a.prompt, "decode_batch_per_gpu": 1,
                        "sampling": "temperature 0.8, top_k 40, top_p 0.9, repeat_penalty 1.1 (on device)"},
             "extra": {"ttft_ms": round(ttft * 1e3, 2), "load_s": round(load_s, 2),
-                      "weights_gb": round(runner.w.nbytes / 1e9, 3),
-                      "continuous_batching": batched},
+                      "weights_gb": round(weights_gb, 3),
+                      "continuous_batching": batched, "server": served},
         }), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -157,9 +157,9 @@ class ModelManager:
         else:
             # continuous batching (Ollama OLLAMA_NUM_PARALLEL): parallel rows + as many idle sequences
             # kept for prefix reuse; KV is sized for all of them at full context (288 GB HBM)
-            # default 1 (serialised) until the batched GPU path has been run on MI355X hardware
-            # (tests/test_engine_gpu.py::test_batched_decode_matches_single / test_scheduler_concurrent_gpu)
-            par = max(1, int(os.environ.get("OLLAMA_NUM_PARALLEL", "1")))
+            # default 4 as Ollama; the batched path is covered on MI355X by
+            # tests/test_engine_gpu.py::test_batched_decode_matches_single / test_scheduler_concurrent_gpu
+            par = max(1, int(os.environ.get("OLLAMA_NUM_PARALLEL", "4")))
             # rows: par decoding + par idle prefix-cache sequences + 1 kept free for embeddings
             runner = Runner(path, device=self.device, max_batch=chunk, max_seqs=max(2, 2 * par + 1), ctx=ctx)
             runner.warmup()

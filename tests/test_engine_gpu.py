@@ -151,12 +151,28 @@ def test_scheduler_concurrent_gpu(tiny_models):
     def work(i):
         out[i] = list(sch.submit([1, 10 + i, 20 + i], SamplingOptions(temperature=0.7, seed=i), lens[i]))
 
-    th = [threading.Thread(target=work, args=(i,)) for i in range(6)]
-    for t in th:
-        t.start()
-    for t in th:
-        t.join(60)
+    def run_all():
+        th = [threading.Thread(target=work, args=(i,)) for i in range(6)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(60)
+        return [list(o) for o in out]
+
+    first = run_all()
+    again = run_all()  # same requests, different row composition/timing: seeded sampling is per row
     sch.close()
-    assert [len(o) for o in out] == lens
+    assert [len(o) for o in first] == lens
     assert sch.max_batch_seen >= 2
-    assert all(0 <= t < g.cfg.n_vocab for o in out for t in o)
+    assert all(0 <= t < g.cfg.n_vocab for o in first for t in o)
+    assert again == first
+    # parity with solo generation (B == 1 path): same seeded stream; the batched GEMV sums in a
+    # different order, so allow a late divergence on a near-tie but require the opening tokens agree
+    s = Runner(tiny_models["tiny-llama"], device="cuda", max_batch=32, max_seqs=2, ctx=256)
+    for i in range(6):
+        sid = s.new_sequence()
+        solo = list(s.generate(sid, [1, 10 + i, 20 + i], SamplingOptions(temperature=0.7, seed=i), max_tokens=lens[i]))
+        s.free_sequence(sid)
+        k = min(4, lens[i])
+        assert solo[:k] == first[i][:k], i
+        assert sum(a == b for a, b in zip(solo, first[i])) >= lens[i] // 2, i
