@@ -33,9 +33,9 @@ static QMat qmat(py::object o) {
   m.N = t[4].cast<int>();
   m.K = t[5].cast<int>();
   m.qtype = t[6].cast<int>();
-  if (m.qtype != QT_Q4_0 && m.qtype != QT_Q8_0 && m.qtype != QT_Q4_K && m.qtype != QT_Q6_K)
+  if (m.qtype != QT_Q4_0 && m.qtype != QT_Q8_0 && m.qtype != QT_Q4_K && m.qtype != QT_Q5_K && m.qtype != QT_Q6_K)
     throw std::runtime_error("unsupported device quant type " + std::to_string(m.qtype));
-  const int blk = (m.qtype == QT_Q4_K || m.qtype == QT_Q6_K) ? 256 : 32;
+  const int blk = (m.qtype == QT_Q4_K || m.qtype == QT_Q5_K || m.qtype == QT_Q6_K) ? 256 : 32;
   if (m.K % blk || m.K <= 0 || m.N <= 0) throw std::runtime_error("bad qmat geometry");
   return m;
 }
@@ -243,7 +243,7 @@ PYBIND11_MODULE(_C, m) {
      py::arg("scale"), py::arg("window"), py::arg("out"), py::arg("ldo"), py::arg("ws"), py::arg("n_splits"),
      py::arg("counters"), py::arg("stream"), py::arg("prefill") = 0);
   m.def("attention_ws_floats", &attention_ws_floats);
-  m.def("set_attn_tuning", &set_attn_tuning, py::arg("kps"));
+  m.def("set_attn_tuning", &set_attn_tuning, py::arg("kps"), py::arg("hpb") = -1);
   m.def("gemv_merge_supported", &gemv_merge_supported);
   m.def("set_gemv_tuning", &set_gemv_tuning, py::arg("blocks_per_cu") = 0, py::arg("rows") = 0,
         py::arg("debug") = 0, py::arg("ks") = -1, py::arg("xfirst") = -1);

@@ -156,6 +156,7 @@ static void stream_bytes(int qt, int64_t K, int64_t out[4]) {
   out[0] = out[1] = out[2] = out[3] = 0;
   switch (qt) {
     case 12: out[0] = 128 * SB; out[1] = 16 * SB; break;
+    case 13: out[0] = 128 * SB; out[1] = 16 * SB; out[2] = 32 * SB; break;
     case 14: out[0] = 128 * SB; out[1] = 64 * SB; out[2] = 16 * SB; out[3] = 2 * SB; break;
     case 2: out[0] = 128 * SB; out[1] = 16 * SB; break;
     case 8: out[0] = 256 * SB; out[1] = 16 * SB; break;
@@ -165,6 +166,21 @@ static void stream_bytes(int qt, int64_t K, int64_t out[4]) {
 
 static inline void copy_xor80(uint8_t* d, const uint8_t* s) {  // high nibble -> signed (n - 8)
   for (int i = 0; i < 16; ++i) d[i] = s[i] ^ 0x80;
+}
+
+// Q5_K high bits of one super-block (32 B, ggml order: bit j of qh[l] = weight l of sub-block j)
+// -> 8 pieces x 4 B: piece t = 2c + h, byte j holds lo (sub-block 2c) weights 16h + 4k + j at bit k and
+// hi (sub-block 2c + 1) weights at bit 4 + k (quant.py _q5k_qh_split).
+static void q5k_split_qh(const uint8_t* qh, uint8_t* dst, int64_t piece_stride) {
+  for (int t = 0; t < 8; ++t) {
+    const int c = t >> 1, h = t & 1;
+    uint8_t o[4] = {0, 0, 0, 0};
+    for (int i = 0; i < 16; ++i) {
+      const int v = qh[16 * h + i];
+      o[i & 3] |= (uint8_t)((((v >> (2 * c)) & 1) << (i >> 2)) | (((v >> (2 * c + 1)) & 1) << (4 + (i >> 2))));
+    }
+    std::memcpy(dst + t * piece_stride, o, 4);
+  }
 }
 
 // Q6_K high bits of one super-block (64 B, ggml order) -> 8 pieces x (H0 | H1), 8 B each.
@@ -207,6 +223,11 @@ void repack_rows(const uint8_t* src, int qtype, int64_t K_src, const int64_t* ro
           case 12:  // d,dmin,scales | qs (8 pieces)
             std::memcpy(d1 + 16 * b, s, 16);
             for (int t = 0; t < 8; ++t) copy_xor80(d0 + (t * SB + b) * 16, s + 16 + 16 * t);
+            break;
+          case 13:  // d,dmin,scales | qh | qs (unsigned nibbles: the 5th bit is OR-ed in by the kernels)
+            std::memcpy(d1 + 16 * b, s, 16);
+            q5k_split_qh(s + 16, d2 + b * 4, SB * 4);
+            for (int t = 0; t < 8; ++t) std::memcpy(d0 + (t * SB + b) * 16, s + 48 + 16 * t, 16);
             break;
           case 14:  // ql | qh | sc | d
             for (int t = 0; t < 8; ++t) std::memcpy(d0 + (t * SB + b) * 16, s + 16 * t, 16);

@@ -1,7 +1,10 @@
 // Paged-KV grouped-query attention for decode and chunked prefill.
 //
-// Grid (query, kv_head, split); one 512-thread block (8 waves) serves the G = H/H_kv query heads that
-// share a KV head, so each K/V row is read once per group (GQA reuse). Design points (measured with
+// Grid (query, kv_head x head_split, split); one 512-thread block (8 waves) serves G of the H/H_kv
+// query heads that share a KV head, so each K/V row is read once per G heads (GQA reuse). Decode
+// launches few blocks (70B: 8 KV heads), and each lane's per-key work grows with G, so for GQA the
+// group is split over H/H_kv/G blocks (head_split, `hpb` knob): the K/V re-reads hit L2/MALL and
+// the block count / per-lane chain shrink (scripts/bench_attn.py OMX_BENCH_HPB sweep). Design points (measured with
 // scripts/bench_attn.py, profiles/r1_attn):
 //  * 16 lanes cooperate on one key (D/16 dims each: one 16-B load for D = 128); a wave's 4 DPP rows
 //    are 4 key groups, the block's 32 groups x U = 4 slots (2 when G = 8) stream 128 keys per step.
@@ -26,8 +29,10 @@ constexpr int ATT_NW = 8;               // waves per block
 constexpr int ATT_NT = 64 * ATT_NW;
 constexpr int ATT_NG = 4 * ATT_NW;      // key groups (16 lanes each) per block
 int g_attn_kps = 256;                   // target keys per split (runtime knob, set_attn_tuning)
-void set_attn_tuning(int kps) {
+int g_attn_hpb = 0;                     // query heads per decode block (0 = auto, see launch_d)
+void set_attn_tuning(int kps, int hpb) {
   if (kps >= 16) g_attn_kps = kps;
+  if (hpb >= 0) g_attn_hpb = hpb;
 }
 constexpr int ATT_BTW = 1024;           // block-table entries staged in LDS per window
 
@@ -83,7 +88,9 @@ __global__ __launch_bounds__(ATT_NT) void attn_decode_kernel(AttnParams P) {
   constexpr int ATT_U = U, ATT_STEP = ATT_NG * U;
   __shared__ float sm[ATT_NW][G][D + 2];
   __shared__ int sbt[ATT_BTW];
-  const int qi = blockIdx.x, kvh = blockIdx.y, split = blockIdx.z;
+  const int qi = blockIdx.x, split = blockIdx.z;
+  const int kvh = blockIdx.y / (P.H / P.n_kv / G);  // KV head of this block's G query heads
+  const int h0 = blockIdx.y * G;                    // first query head of the block
   const int seq = P.q_seq ? P.q_seq[qi] : qi;
   const int len = P.q_len[qi];
   const int kstart = P.window > 0 ? max(0, len - P.window) : 0;
@@ -101,7 +108,7 @@ __global__ __launch_bounds__(ATT_NT) void attn_decode_kernel(AttnParams P) {
   float q[G][DPL];
 #pragma unroll
   for (int g = 0; g < G; ++g) {
-    const float* qp = P.q + (long long)qi * P.ldq + (kvh * G + g) * D + li * DPL;
+    const float* qp = P.q + (long long)qi * P.ldq + (h0 + g) * D + li * DPL;
 #pragma unroll
     for (int j = 0; j < DPL; ++j) q[g][j] = qp[j] * P.scale;
   }
@@ -232,7 +239,7 @@ __global__ __launch_bounds__(ATT_NT) void attn_decode_kernel(AttnParams P) {
         A += sm[w][g][d] * c;
       }
     }
-    const int h = kvh * G + g;
+    const int h = h0 + g;
     if (P.defer) {  // partial slabs [NQ][S][H*D] + [NQ][S][H]{m, l}; the kernel boundary publishes them
       const long long row = (long long)qi * S + split;
       P.ws[row * P.H * D + h * D + d] = A;
@@ -259,7 +266,7 @@ __global__ __launch_bounds__(ATT_NT) void attn_decode_kernel(AttnParams P) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    int* cnt = P.counters + (long long)qi * P.n_kv + kvh;
+    int* cnt = P.counters + (long long)qi * gridDim.y + blockIdx.y;
     const int old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int last = old == S - 1;
     if (last) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
@@ -272,7 +279,7 @@ __global__ __launch_bounds__(ATT_NT) void attn_decode_kernel(AttnParams P) {
     const int s = threadIdx.x;
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-      const float* ws = P.ws + (((long long)qi * P.H + kvh * G + g) * gridDim.z + (s < S ? s : 0)) * (D + 2);
+      const float* ws = P.ws + (((long long)qi * P.H + h0 + g) * gridDim.z + (s < S ? s : 0)) * (D + 2);
       const float lv = ld1(ws + D + 1);
       const bool live = s < S && lv > 0.f;
       const float mm = live ? ld1(ws + D) : -INFINITY;
@@ -286,12 +293,12 @@ __global__ __launch_bounds__(ATT_NT) void attn_decode_kernel(AttnParams P) {
   __syncthreads();
   for (int i = threadIdx.x; i < G * D; i += ATT_NT) {
     const int g = i / D, d = i % D;
-    const float* ws = P.ws + ((long long)qi * P.H + kvh * G + g) * gridDim.z * (D + 2);
+    const float* ws = P.ws + ((long long)qi * P.H + h0 + g) * gridDim.z * (D + 2);
     float A = 0.f;
 #pragma unroll 8
     for (int s = 0; s < S; ++s) A += sw[g][s] * ld1(ws + s * (D + 2) + d);
     const float L = sL[g];
-    P.out[(long long)qi * P.ldo + (kvh * G + g) * D + d] = L > 0.f ? A / L : 0.f;
+    P.out[(long long)qi * P.ldo + (h0 + g) * D + d] = L > 0.f ? A / L : 0.f;
   }
 }
 
@@ -468,10 +475,19 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(AttnParams P) {
   }
 }
 
+// query heads per block: the whole GQA group (one K/V read) unless the launch would be too narrow
+// to fill the chip; then groups of 2 (G = 4, 8) -- measured, scripts/bench_attn.py OMX_BENCH_HPB
+static int heads_per_block(const AttnParams& P) {
+  const int G = P.H / P.n_kv;
+  int hpb = g_attn_hpb > 0 ? g_attn_hpb : (G >= 4 && P.NQ * P.n_kv < 64 ? 2 : G);
+  while (hpb > 1 && (G % hpb || (hpb != 1 && hpb != 2 && hpb != 4 && hpb != 8))) --hpb;
+  return hpb < 1 ? 1 : hpb;
+}
+
 template <int D>
 static void launch_d(const AttnParams& P, hipStream_t s) {
-  const int G = P.H / P.n_kv;
-  dim3 grid(P.NQ, P.n_kv, P.n_splits);
+  const int G = heads_per_block(P);
+  dim3 grid(P.NQ, P.H / G, P.n_splits);
   switch (G) {
     case 1: hipLaunchKernelGGL((attn_decode_kernel<D, 1>), grid, dim3(ATT_NT), 0, s, P); break;
     case 2: hipLaunchKernelGGL((attn_decode_kernel<D, 2>), grid, dim3(ATT_NT), 0, s, P); break;

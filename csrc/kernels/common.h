@@ -121,6 +121,32 @@ __device__ inline void dequant_piece(const QMat& w, long long row, int p, float*
       lo[i] = sc[0] * (float)(byte & 0xF) - mn[0];
       hi[i] = sc[1] * (float)(byte >> 4) - mn[1];
     }
+  } else if (w.qtype == QT_Q5_K) {
+    const int c = t >> 1, h = t & 1;
+    off_lo = 256 * sb + 64 * c + 16 * h;
+    off_hi = off_lo + 32;
+    const u32x4 q = *(const u32x4*)(w.s0 + row * SB * 128 + 16 * pi);
+    const unsigned H = *(const unsigned*)(w.s2 + row * SB * 32 + 4 * pi);
+    const u32x4 m = *(const u32x4*)(w.s1 + row * SB * 16 + 16LL * sb);
+    const float d = h2f(m.x & 0xFFFF), dmin = h2f(m.x >> 16);
+    float sc[2], mn[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int j = 2 * c + k, sh = 8 * (j & 3);
+      const unsigned a = (m.y >> sh) & 0xFF, b = (m.z >> sh) & 0xFF, e = (m.w >> sh) & 0xFF;
+      const unsigned s = j < 4 ? (a & 63) : ((e & 0xF) | ((a >> 6) << 4));
+      const unsigned mm = j < 4 ? (b & 63) : ((e >> 4) | ((b >> 6) << 4));
+      sc[k] = d * (float)s;
+      mn[k] = dmin * (float)mm;
+    }
+    const unsigned qq[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const unsigned byte = (qq[i >> 2] >> (8 * (i & 3))) & 0xFF;
+      const unsigned hb = H >> (8 * (i & 3));  // byte i & 3: lo bit (i >> 2), hi bit 4 + (i >> 2)
+      lo[i] = sc[0] * (float)((byte & 0xF) | (((hb >> (i >> 2)) & 1) << 4)) - mn[0];
+      hi[i] = sc[1] * (float)((byte >> 4) | (((hb >> (4 + (i >> 2))) & 1) << 4)) - mn[1];
+    }
   } else if (w.qtype == QT_Q6_K) {
     const int n = t >> 2, sub = t & 3;
     off_lo = 256 * sb + 128 * n + 16 * sub;

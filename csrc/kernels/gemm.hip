@@ -86,6 +86,7 @@ struct WRaw {
   u32x4 a[2];
   u32x4 b[QT == QT_Q8_0 ? 2 : 1];
   u32x2 h[QT == QT_Q6_K ? 2 : 1];
+  unsigned q5h[QT == QT_Q5_K ? 2 : 1];
   u32x4 m;
   unsigned d;
 };
@@ -104,6 +105,7 @@ __device__ __forceinline__ void load_wraw(const QMat& w, long long row, int SB, 
     } else {
       R.a[i] = __builtin_nontemporal_load((const u32x4*)(w.s0 + row * SB * 128 + 16 * pi));
       if constexpr (QT == QT_Q6_K) R.h[i] = __builtin_nontemporal_load((const u32x2*)(w.s1 + row * SB * 64 + 8 * pi));
+      if constexpr (QT == QT_Q5_K) R.q5h[i] = __builtin_nontemporal_load((const unsigned*)(w.s2 + row * SB * 32 + 4 * pi));
     }
   }
   if constexpr (QT == QT_Q6_K) {
@@ -153,7 +155,35 @@ __device__ __forceinline__ void dequant_store(const WRaw<QT>& R, int ks, int pp,
     const int t = 4 * half + p;  // piece within the super-block
     unsigned lo[8], hi[8];
     int olo, ohi;
-    if constexpr (QT == QT_Q4_K) {
+    if constexpr (QT == QT_Q5_K) {
+      const int c = t >> 1, h = t & 1;
+      const u32x4 q = R.a[i];  // unsigned nibbles; 5th bits from q5h (quant.py _q5k_qh_split)
+      const unsigned H = R.q5h[i];
+      const float d = h2f(R.m.x & 0xFFFF), dmin = h2f(R.m.x >> 16);
+      float sc[2], mn[2];
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int j = 2 * c + k, sh = 8 * (j & 3);
+        const unsigned a = (R.m.y >> sh) & 0xFF, b = (R.m.z >> sh) & 0xFF, e = (R.m.w >> sh) & 0xFF;
+        const unsigned s = j < 4 ? (a & 63) : ((e & 0xF) | ((a >> 6) << 4));
+        const unsigned mm = j < 4 ? (b & 63) : ((e >> 4) | ((b >> 6) << 4));
+        sc[k] = d * (float)s;
+        mn[k] = -dmin * (float)mm;
+      }
+      const h2 off = hsplat(1024.f), s0 = hsplat(sc[0]), s1 = hsplat(sc[1]), c0 = hsplat(mn[0]), c1 = hsplat(mn[1]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        unsigned l0, l1, g0, g1;
+        nib_pairs(sel4(q, e), l0, l1, g0, g1);
+        // 5th bit of weights 4e + j: H byte j, bit e (lo) / 4 + e (hi) -> bit 4 of each fp16 half
+        lo[2 * e] = dq(l0 | ((H << (4 - e)) & 0x00100010u), off, s0, c0);
+        lo[2 * e + 1] = dq(l1 | ((H >> (4 + e)) & 0x00100010u), off, s0, c0);
+        hi[2 * e] = dq(g0 | ((H >> e) & 0x00100010u), off, s1, c1);
+        hi[2 * e + 1] = dq(g1 | ((H >> (8 + e)) & 0x00100010u), off, s1, c1);
+      }
+      olo = 64 * (c - 2 * half) + 16 * h;
+      ohi = olo + 32;
+    } else if constexpr (QT == QT_Q4_K) {
       const int c = t >> 1, h = t & 1;
       const u32x4 q = R.a[i] ^ 0x80808080u;  // undo the signed-high-nibble repack
       const float d = h2f(R.m.x & 0xFFFF), dmin = h2f(R.m.x >> 16);
@@ -405,6 +435,7 @@ void moe_gemm(const GemvParams& P, hipStream_t s) {
   switch (P.w.qtype) {
     case QT_Q4_K: launch_moe<QT_Q4_K>(P, x16, s); break;
     case QT_Q6_K: launch_moe<QT_Q6_K>(P, x16, s); break;
+    case QT_Q5_K: launch_moe<QT_Q5_K>(P, x16, s); break;
     case QT_Q4_0: launch_moe<QT_Q4_0>(P, x16, s); break;
     case QT_Q8_0: launch_moe<QT_Q8_0>(P, x16, s); break;
     default: break;
@@ -421,6 +452,7 @@ void gemm(const GemvParams& P, hipStream_t s) {
   switch (P.w.qtype) {
     case QT_Q4_K: launch_gemm<QT_Q4_K>(P, x16, s); break;
     case QT_Q6_K: launch_gemm<QT_Q6_K>(P, x16, s); break;
+    case QT_Q5_K: launch_gemm<QT_Q5_K>(P, x16, s); break;
     case QT_Q4_0: launch_gemm<QT_Q4_0>(P, x16, s); break;
     case QT_Q8_0: launch_gemm<QT_Q8_0>(P, x16, s); break;
     default: break;

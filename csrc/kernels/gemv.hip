@@ -50,7 +50,7 @@ void set_gemv_tuning(int blocks_per_cu, int rows, int debug, int ks, int xfirst)
 // the loaded words (memory path alone), bit 1 = skip the activation prologue
 template <int QT, int NSB, int R, int BT, int DBG = 0>
 __global__ __launch_bounds__(GEMV_NT) void qgemv_kernel(GemvParams P) {
-  constexpr int PB = QT == QT_Q8_0 ? 8 : QT == QT_Q6_K ? 6 : 4;  // VGPRs per piece
+  constexpr int PB = QT == QT_Q8_0 ? 8 : QT == QT_Q6_K ? 6 : QT == QT_Q5_K ? 5 : 4;  // VGPRs per piece
   constexpr bool DB = R * NSB * (8 * PB + 5) <= 80;               // room for a prefetch tile
   constexpr int ROWS_W = 4 * R, ROWS_B = GEMV_NW * ROWS_W;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -398,7 +398,7 @@ __global__ __launch_bounds__(GEMV_NT) void qgemv_flight_dual_kernel(GemvParams P
 // register tiles a block keeps in flight: ~150 VGPRs of weight tiles per lane
 template <int QT, int NSB, int R>
 constexpr int flight_jmax() {
-  constexpr int PB = QT == QT_Q8_0 ? 8 : QT == QT_Q6_K ? 6 : 4;
+  constexpr int PB = QT == QT_Q8_0 ? 8 : QT == QT_Q6_K ? 6 : QT == QT_Q5_K ? 5 : 4;
   constexpr int regs = R * NSB * (8 * PB + 5);
   return regs * 3 <= 150 ? 3 : regs * 2 <= 150 ? 2 : 1;
 }
@@ -599,6 +599,7 @@ static bool launch_dual_a(const GemvParams& A, const GemvParams& Bp, int need, h
   switch (Bp.w.qtype) {
     case QT_Q4_K: if (QA != QT_Q4_K) { launch_dual_q<QA, QT_Q4_K>(A, Bp, need, s); return true; } break;
     case QT_Q6_K: if (QA != QT_Q6_K) { launch_dual_q<QA, QT_Q6_K>(A, Bp, need, s); return true; } break;
+    case QT_Q5_K: if (QA != QT_Q5_K) { launch_dual_q<QA, QT_Q5_K>(A, Bp, need, s); return true; } break;
     case QT_Q4_0: if (QA != QT_Q4_0) { launch_dual_q<QA, QT_Q4_0>(A, Bp, need, s); return true; } break;
     case QT_Q8_0: if (QA != QT_Q8_0) { launch_dual_q<QA, QT_Q8_0>(A, Bp, need, s); return true; } break;
     default: break;
@@ -618,6 +619,7 @@ void gemv2(const GemvParams& A0, const GemvParams& B0, hipStream_t s) {
     switch (A.w.qtype) {
       case QT_Q4_K: done = launch_dual_a<QT_Q4_K>(A, Bp, need, s); break;
       case QT_Q6_K: done = launch_dual_a<QT_Q6_K>(A, Bp, need, s); break;
+      case QT_Q5_K: done = launch_dual_a<QT_Q5_K>(A, Bp, need, s); break;
       case QT_Q4_0: done = launch_dual_a<QT_Q4_0>(A, Bp, need, s); break;
       case QT_Q8_0: done = launch_dual_a<QT_Q8_0>(A, Bp, need, s); break;
       default: break;
@@ -646,6 +648,7 @@ void gemv(const GemvParams& P0, hipStream_t s) {
   switch (P.w.qtype) {
     case QT_Q4_K: launch_q<QT_Q4_K>(P, s); break;
     case QT_Q6_K: launch_q<QT_Q6_K>(P, s); break;
+    case QT_Q5_K: launch_q<QT_Q5_K>(P, s); break;
     case QT_Q4_0: launch_q<QT_Q4_0>(P, s); break;
     case QT_Q8_0: launch_q<QT_Q8_0>(P, s); break;
     default: break;

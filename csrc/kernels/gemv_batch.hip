@@ -205,7 +205,7 @@ static void launch_batch_j(const GemvParams& P, int gx, int by, int mode, size_t
 
 template <int QT, int NSB, int BT>
 static void launch_batch_n(const GemvParams& P, size_t lds, hipStream_t s) {
-  constexpr int PB = QT == QT_Q8_0 ? 8 : QT == QT_Q6_K ? 6 : 4;
+  constexpr int PB = QT == QT_Q8_0 ? 8 : QT == QT_Q6_K ? 6 : QT == QT_Q5_K ? 5 : 4;
   constexpr int regs = NSB * (8 * PB + 5);                       // one weight tile per lane
   constexpr int XR = BT * NSB <= 4 ? (BT + 1) * NSB * 16 : 0;     // register prologue
   constexpr int XF = 12 * BT;                                     // activation fragments per piece
@@ -254,6 +254,7 @@ bool gemv_batch(const GemvParams& P, hipStream_t s) {
   switch (P.w.qtype) {
     case QT_Q4_K: launch_batch_q<QT_Q4_K>(P, BT, need, lds, s); return true;
     case QT_Q6_K: launch_batch_q<QT_Q6_K>(P, BT, need, lds, s); return true;
+    case QT_Q5_K: launch_batch_q<QT_Q5_K>(P, BT, need, lds, s); return true;
     case QT_Q4_0: launch_batch_q<QT_Q4_0>(P, BT, need, lds, s); return true;
     case QT_Q8_0: launch_batch_q<QT_Q8_0>(P, BT, need, lds, s); return true;
     default: return false;

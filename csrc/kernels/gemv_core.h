@@ -42,10 +42,11 @@ __device__ __forceinline__ float f16hi(unsigned v) { return h2f(v >> 16); }
 // register tile: R rows x NSB super-blocks x 8 pieces of one lane
 template <int QT, int NSB, int R>
 struct WTile {
-  static constexpr bool Q8 = QT == QT_Q8_0, Q6 = QT == QT_Q6_K;
+  static constexpr bool Q8 = QT == QT_Q8_0, Q6 = QT == QT_Q6_K, Q5 = QT == QT_Q5_K;
   u32x4 a[R][NSB][8];                                  // qs / ql / Q8_0 first 16 B
   u32x4 b[Q8 ? R : 1][Q8 ? NSB : 1][8];                // Q8_0 second 16 B
   u32x2 h[Q6 ? R : 1][Q6 ? NSB : 1][8];                // Q6_K high bits (H0 | H1)
+  unsigned q5h[Q5 ? R : 1][Q5 ? NSB : 1][8];           // Q5_K 5th bits (one dword per piece)
   u32x4 m[R][NSB];                                     // super-block scales
   unsigned d[Q6 ? R : 1][Q6 ? NSB : 1];                // Q6_K super-block scale (fp16)
 };
@@ -93,6 +94,17 @@ __device__ __forceinline__ void load_wtile(const QMat& w, long long row_base, in
           T.h[r][i][t] = __builtin_nontemporal_load((const u32x2*)(hq + 8LL * t * SB));
           OMX_LOAD_ORDER();
         }
+      } else if constexpr (QT == QT_Q5_K) {
+        const uint8_t* q = w.s0 + row * SB * 128 + 16 * sb;
+        const uint8_t* hq = w.s2 + row * SB * 32 + 4 * sb;
+        T.m[r][i] = *(const u32x4*)(w.s1 + row * SB * 16 + 16 * sb);
+        OMX_LOAD_ORDER();
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          T.a[r][i][t] = __builtin_nontemporal_load((const u32x4*)(q + 16LL * t * SB));
+          T.q5h[r][i][t] = __builtin_nontemporal_load((const unsigned*)(hq + 4LL * t * SB));
+          OMX_LOAD_ORDER();
+        }
       } else {
         const uint8_t* q = w.s0 + row * SB * 128 + 16 * sb;
         T.m[r][i] = *(const u32x4*)(w.s1 + row * SB * 16 + 16 * sb);
@@ -135,7 +147,61 @@ __device__ __forceinline__ void compute_wtile(const WTile<QT, NSB, R>& T, int SB
     const int sb = sb0 + s + 16 * i;
     if (sb >= se) continue;
     const int xs0 = sb * XPAD;
-    if constexpr (QT == QT_Q4_K) {
+    if constexpr (QT == QT_Q5_K) {
+      // w = d*sc*q - dmin*m, q = nibble | (5th bit << 4) in 0..31 (unsigned int8 codes)
+      float d[R], dm[R];
+      unsigned sl[R], ml[R], sh[R], mh[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const u32x4 m = T.m[r][i];
+        d[r] = f16lo(m.x);
+        dm[r] = f16hi(m.x);
+        sl[r] = m.y & 0x3F3F3F3Fu;
+        ml[r] = m.z & 0x3F3F3F3Fu;
+        sh[r] = (m.w & 0x0F0F0F0Fu) | ((m.y >> 2) & 0x30303030u);
+        mh[r] = ((m.w >> 4) & 0x0F0F0F0Fu) | ((m.z >> 2) & 0x30303030u);
+      }
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        float fsl[R], fml[R], fsh[R], fmh[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const unsigned S = c < 2 ? sl[r] : sh[r], M = c < 2 ? ml[r] : mh[r];
+          const int k0 = (2 * c) & 3, k1 = (2 * c + 1) & 3;
+          fsl[r] = d[r] * ubyte(S, k0);
+          fml[r] = dm[r] * ubyte(M, k0);
+          fsh[r] = d[r] * ubyte(S, k1);
+          fmh[r] = dm[r] * ubyte(M, k1);
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int t = 2 * c + h, gl = 4 * c + h;
+          XFr<BT> x;
+          load_x<BT>(xq, xf, XS, xs0 + gl, xs0 + gl + 2, x);
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+            const u32x4 a = T.a[r][i][t];
+            const unsigned H = T.q5h[r][i][t];
+            u32x4 lo, hi;
+            lo.x = (a.x & 0x0F0F0F0Fu) | ((H << 4) & 0x10101010u);
+            lo.y = (a.y & 0x0F0F0F0Fu) | ((H << 3) & 0x10101010u);
+            lo.z = (a.z & 0x0F0F0F0Fu) | ((H << 2) & 0x10101010u);
+            lo.w = (a.w & 0x0F0F0F0Fu) | ((H << 1) & 0x10101010u);
+            hi.x = ((a.x >> 4) & 0x0F0F0F0Fu) | (H & 0x10101010u);
+            hi.y = ((a.y >> 4) & 0x0F0F0F0Fu) | ((H >> 1) & 0x10101010u);
+            hi.z = ((a.z >> 4) & 0x0F0F0F0Fu) | ((H >> 2) & 0x10101010u);
+            hi.w = ((a.w >> 4) & 0x0F0F0F0Fu) | ((H >> 3) & 0x10101010u);
+#pragma unroll
+            for (int b = 0; b < BT; ++b) {
+              const float il = (float)dot16(lo, x.lo[b]), ih = (float)dot16(hi, x.hi[b]);
+              acc[r][b] += fsl[r] * (x.fl[b].x * il) - fml[r] * x.fl[b].y + fsh[r] * (x.fh[b].x * ih) -
+                           fmh[r] * x.fh[b].y;
+            }
+          }
+          OMX_PIECE_ORDER();
+        }
+      }
+    } else if constexpr (QT == QT_Q4_K) {
       // w = d*sc*n - dmin*m per 32-weight sub-block; lo nibbles: sub-block 2c, hi: 2c+1 (signed n-8)
       float d[R], dm[R];
       unsigned sl[R], ml[R], sh[R], mh[R];

@@ -106,7 +106,7 @@ struct AttnParams {
   int ldo;
   float* ws;                   // split workspace: [NQ][H][S][D + 2] fp32
   int n_splits;                // <= 64
-  int* counters;               // [NQ][n_kv] arrival tickets, zero before first use (self re-arming)
+  int* counters;               // [NQ][H] arrival tickets (one per block row), zero before first use (self re-arming)
   int prefill;                 // all NQ queries: one sequence, contiguous positions (MFMA flash path)
   int kps;                     // target keys per split (0 -> g_attn_kps)
   int defer;                   // write exactly n_splits unmerged partials (attention_ws_floats layout
@@ -115,7 +115,7 @@ struct AttnParams {
 void attention_decode(const AttnParams& P, hipStream_t s);
 size_t attention_ws_floats(int NQ, int H, int D, int n_splits);
 extern int g_attn_kps;  // decode keys per flash-decode split (scripts/bench_attn.py sweep)
-void set_attn_tuning(int kps);
+void set_attn_tuning(int kps, int hpb = -1);
 
 struct SampleParams {
   const float* logits;         // [B][V] (modified in place by penalties)

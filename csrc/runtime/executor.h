@@ -53,7 +53,7 @@ struct Workspace {
   int* eids = nullptr;       // [maxB][n_sel]
   float* ew = nullptr;       // [maxB][n_sel]
   float* attn_ws = nullptr;  // split-K workspace
-  int* attn_cnt = nullptr;   // [maxB][Hkv] split arrival tickets (zero-initialised)
+  int* attn_cnt = nullptr;   // [maxB][H] split arrival tickets (zero-initialised)
   void* x16 = nullptr;       // [maxB][max K] fp16 activations for the prefill MFMA GEMM
   float* gws = nullptr;      // split-K partial slabs for small-M prefill GEMMs
   int* moe_rows = nullptr;   // [maxB*k] MoE prefill: pairs sorted by expert

@@ -145,7 +145,7 @@ class Runner:
         self.gws = torch.zeros(GEMM_SPLIT_WS_FLOATS if str(dev).startswith("cuda") else 1, **f32)
         ws = max(self._ws_floats(B) for B in range(1, max_batch + 1))
         self.attn_ws = torch.zeros(max(ws, 1), **f32)
-        self.attn_cnt = torch.zeros(max_batch * loc["Hkv"], **i32)  # self re-arming tickets
+        self.attn_cnt = torch.zeros(max_batch * loc["H"], **i32)  # self re-arming tickets
         self.logits = torch.zeros(max_batch, Vl, **f32)
         self.full_logits = torch.zeros(max_batch, cfg.n_vocab, **f32) if tp_size > 1 else self.logits
         # step inputs, packed so one H2D copy refreshes (pos, slot, q_len, q_seq, logit_idx)

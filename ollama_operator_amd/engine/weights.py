@@ -7,7 +7,7 @@ Every projection is uploaded as a `DevQMat` (csrc/kernels/qmat.h) laid out for t
   * gate/up rows interleaved (row 2j = gate j, 2j+1 = up j) so SiLU-GLU fuses into the epilogue;
   * tensor-parallel shards cut on head / row / 256-weight-block boundaries;
   * MoE experts stacked [X][N][K] so the kernel offsets to the routed expert on device.
-Types without a native kernel (Q4_1/Q5_x/F16/BF16/F32 projections) are requantised to Q8_0 at
+Types without a native kernel (Q4_1/Q5_0/Q5_1/F16/BF16/F32 projections) are requantised to Q8_0 at
 load -- documented precision upgrade for those files, never a silent fallback.
 Host staging goes through the native repack (`_C.GGUFMap.repack`, multi-threaded over the mmap).
 """
@@ -25,7 +25,7 @@ from ..models.config import ROPE_NEOX, ModelConfig
 from ..quant import REPACK_STREAMS, dequantize, quantize, repack_row_bytes
 from ..ops import has_native, native
 
-NATIVE_QTYPES = (GGMLType.Q4_0, GGMLType.Q8_0, GGMLType.Q4_K, GGMLType.Q6_K)
+NATIVE_QTYPES = (GGMLType.Q4_0, GGMLType.Q8_0, GGMLType.Q4_K, GGMLType.Q5_K, GGMLType.Q6_K)
 
 
 def stream_bytes(qtype: int, K: int) -> list[int]:

@@ -2,7 +2,8 @@
 
 Names follow the public llama.cpp GGUF conventions (`blk.{i}.attn_q.weight`, ...). The K-quant
 mix for `Q4_K_M` follows llama.cpp's public rule: output.weight Q6_K; attn_v / ffn_down Q6_K in
-the "more bits" layers (first and last eighth, and every third in between), Q4_K elsewhere.
+the "more bits" layers (first and last eighth, and every third in between), Q4_K elsewhere;
+`Q5_K_M` / `Q5_K_S` the same with Q5_K as the base type.
 """
 from __future__ import annotations
 
@@ -33,6 +34,12 @@ def _matrix_type(ftype: FileType, role: str, layer: int, n_layer: int) -> GGMLTy
         if ftype == FileType.MOSTLY_Q4_K_M and role in ("attn_v", "ffn_down") and use_more_bits(layer, n_layer):
             return GGMLType.Q6_K
         return GGMLType.Q4_K
+    if ftype in (FileType.MOSTLY_Q5_K_M, FileType.MOSTLY_Q5_K_S):
+        if role == "output":
+            return GGMLType.Q6_K
+        if ftype == FileType.MOSTLY_Q5_K_M and role in ("attn_v", "ffn_down") and use_more_bits(layer, n_layer):
+            return GGMLType.Q6_K
+        return GGMLType.Q5_K
     raise NotImplementedError(f"file type {ftype!r}")
 
 

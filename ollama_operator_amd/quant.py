@@ -6,11 +6,14 @@ Block layouts follow the public ggml definitions:
   Q8_0 : fp16 d | int8[32]                              (32 weights, 34 B)   x = q * d
   Q4_K : fp16 d | fp16 dmin | 12 B 6-bit (sc, m) x 8 | 128 B nibbles  (256 w, 144 B)
          x = d*sc_j*q - dmin*m_j   (sub-block j of 32)
+  Q5_K : fp16 d | fp16 dmin | 12 B 6-bit (sc, m) x 8 | 32 B qh | 128 B nibbles  (256 w, 176 B)
+         x = d*sc_j*(n + 16*h) - dmin*m_j   (h = bit j of qh[l])
   Q6_K : 128 B ql | 64 B qh | int8 sc[16] | fp16 d    (256 w, 210 B)    x = d*sc_g*(q - 32)
 
 Device layout ("repacked"): every type is stored as separate row-major streams so that one lane's
 16-byte load is always a whole, aligned group of weights (see csrc/kernels/gemv.hip):
   Q4_K -> qs [N, K/2]  + meta [N, K/256, 16]  (d, dmin, scales12: byte-identical to the block head)
+  Q5_K -> qs [N, K/2]  + meta [N, K/16]  + qh [N, K/8]  (high bits regrouped per piece)
   Q6_K -> ql [N, K/2]  + qh [N, K/4] + sc [N, K/16] int8 + d [N, K/256] fp16
   Q4_0 -> qs [N, K/2]  + d [N, K/32] fp16
   Q8_0 -> qs [N, K]    + d [N, K/32] fp16
@@ -198,6 +201,31 @@ def quantize(x: np.ndarray, ggml_type: int) -> np.ndarray:
         out[:, 4:16] = pack_q4k_scales(sc, m)
         out[:, 16:144] = qs.reshape(nblk, 128)
         return out.reshape(-1)
+    if t == GGMLType.Q5_K:
+        sub = xb.reshape(nblk, 8, 32)
+        mn = np.minimum(sub.min(axis=2), 0.0)
+        mx = sub.max(axis=2)
+        scale = (mx - mn) / 31.0
+        mins = -mn
+        d = (scale.max(axis=1) / 63.0).astype(np.float16).astype(np.float32)
+        dmin = (mins.max(axis=1) / 63.0).astype(np.float16).astype(np.float32)
+        sc = np.clip(np.rint(scale / np.where(d > 0, d, 1)[:, None]), 0, 63)
+        m = np.clip(np.rint(mins / np.where(dmin > 0, dmin, 1)[:, None]), 0, 63)
+        eff_d = d[:, None] * sc
+        eff_m = dmin[:, None] * m
+        q = np.rint((sub + eff_m[:, :, None]) / np.where(eff_d > 0, eff_d, 1)[:, :, None])
+        q = np.clip(q, 0, 31).astype(np.uint8)  # [nblk, 8, 32]
+        lo = (q & 0xF).reshape(nblk, 4, 2, 32)
+        qs = lo[:, :, 0, :] | (lo[:, :, 1, :] << 4)
+        qh = np.zeros((nblk, 32), np.uint8)
+        for j in range(8):
+            qh |= ((q[:, j, :] >> 4) & 1) << j
+        out[:, 0:2] = _to_f16_bytes(d)
+        out[:, 2:4] = _to_f16_bytes(dmin)
+        out[:, 4:16] = pack_q4k_scales(sc, m)
+        out[:, 16:48] = qh
+        out[:, 48:176] = qs.reshape(nblk, 128)
+        return out.reshape(-1)
     if t == GGMLType.Q6_K:
         g = xb.reshape(nblk, 16, 16)
         idx = np.abs(g).argmax(axis=2)
@@ -246,6 +274,15 @@ def random_blocks(ggml_type: int, n_rows: int, k: int, rng: np.random.Generator,
         out[:, 0:2] = _to_f16_bytes(d)
         out[:, 2:4] = _to_f16_bytes(dmin)
         out[:, 4:16] = pack_q4k_scales(sc, m)
+    elif t == GGMLType.Q5_K:
+        # q uniform in 0..31 (std 9.2); sc in 32..63, m chosen to centre at zero
+        d = (std / 9.2 / 47.0) * rng.uniform(0.8, 1.2, nblk).astype(np.float32)
+        sc = rng.integers(32, 64, size=(nblk, 8)).astype(np.float32)
+        dmin = d * 15.5 * 64.0 / 63.0
+        m = np.clip(np.rint(sc * d[:, None] * 15.5 / dmin[:, None]), 0, 63)
+        out[:, 0:2] = _to_f16_bytes(d)
+        out[:, 2:4] = _to_f16_bytes(dmin)
+        out[:, 4:16] = pack_q4k_scales(sc, m)
     elif t == GGMLType.Q6_K:
         d = (std / 18.5 / 96.0) * rng.uniform(0.8, 1.2, nblk).astype(np.float32)
         sc = rng.integers(64, 128, size=(nblk, 16)).astype(np.int8)
@@ -269,12 +306,17 @@ def random_blocks(ggml_type: int, n_rows: int, k: int, rng: np.random.Generator,
 # (csrc/kernels/gemv.hip). Scales / mins stay per super-block: meta[row][sb][16 B].
 # 4-bit codes store the HIGH nibble of every byte as a signed two's-complement (n - 8) (byte ^ 0x80),
 # so `q & 0xF0F0F0F0` is directly 16*(n-8) as int8 for v_dot4_i32_i8 (one VALU op, no shift).
+# Q5_K codes are stored unsigned (no ^0x80: the kernels shift the high nibble down and OR in bit 4).
+# Q5_K high bits are regrouped per piece into one dword H: byte j holds the bits of the piece's lo
+# weights j, 4+j, 8+j, 12+j at bits 0-3 and of its hi weights at bits 4-7, so `(H << (4 - k)) & 0x10101010`
+# is bit 4 of the k-th dword of lo codes (hi: `(H >> k) & 0x10101010`).
 # Q6_K high bits are regrouped per piece: byte j of dword H0 (lo half) / H1 (hi half) holds the
 # 2-bit fields of weights j, 4+j, 8+j, 12+j at bits 0-1, 2-3, 4-5, 6-7.
 # ----------------------------------------------------------------------------------------------
 
-REPACK_TYPES = (GGMLType.Q4_0, GGMLType.Q8_0, GGMLType.Q4_K, GGMLType.Q6_K)
-REPACK_STREAMS = {GGMLType.Q4_K: ["qs", "meta"], GGMLType.Q6_K: ["ql", "qh", "sc", "d"],
+REPACK_TYPES = (GGMLType.Q4_0, GGMLType.Q8_0, GGMLType.Q4_K, GGMLType.Q5_K, GGMLType.Q6_K)
+REPACK_STREAMS = {GGMLType.Q4_K: ["qs", "meta"], GGMLType.Q5_K: ["qs", "meta", "qh"],
+                  GGMLType.Q6_K: ["ql", "qh", "sc", "d"],
                   GGMLType.Q4_0: ["qs", "d"], GGMLType.Q8_0: ["qs", "d"]}
 
 
@@ -288,6 +330,8 @@ def repack_row_bytes(ggml_type: int, k: int) -> list[int]:
     t = GGMLType(ggml_type)
     if t == GGMLType.Q4_K:
         return [128 * sb, 16 * sb]
+    if t == GGMLType.Q5_K:
+        return [128 * sb, 16 * sb, 32 * sb]
     if t == GGMLType.Q6_K:
         return [128 * sb, 64 * sb, 16 * sb, 2 * sb]
     if t == GGMLType.Q4_0:
@@ -295,6 +339,33 @@ def repack_row_bytes(ggml_type: int, k: int) -> list[int]:
     if t == GGMLType.Q8_0:
         return [256 * sb, 16 * sb]
     raise ValueError(f"no device layout for {t.name}")
+
+
+def _q5k_qh_split(qh: np.ndarray) -> np.ndarray:
+    """qh [..., 32] (ggml order: bit j of qh[l] = high bit of weight l of sub-block j)
+    -> [..., 8 pieces, 4 B] (piece t = 2c + h: lo = sub-block 2c, hi = 2c + 1, weights l = 16h + i)."""
+    q = qh.astype(np.uint32)
+    out = np.zeros(qh.shape[:-1] + (8, 4), np.uint32)
+    for t in range(8):
+        c, h = t >> 1, t & 1
+        for i in range(16):
+            j, k = i & 3, i >> 2
+            out[..., t, j] |= ((q[..., 16 * h + i] >> (2 * c)) & 1) << k
+            out[..., t, j] |= ((q[..., 16 * h + i] >> (2 * c + 1)) & 1) << (4 + k)
+    return out.astype(np.uint8)
+
+
+def _q5k_qh_join(hp: np.ndarray) -> np.ndarray:
+    """inverse of _q5k_qh_split: [..., 8, 4] -> [..., 32]."""
+    h = hp.astype(np.uint32)
+    q = np.zeros(hp.shape[:-2] + (32,), np.uint32)
+    for t in range(8):
+        c, hh = t >> 1, t & 1
+        for i in range(16):
+            j, k = i & 3, i >> 2
+            q[..., 16 * hh + i] |= ((h[..., t, j] >> k) & 1) << (2 * c)
+            q[..., 16 * hh + i] |= ((h[..., t, j] >> (4 + k)) & 1) << (2 * c + 1)
+    return q.astype(np.uint8)
 
 
 def _q6k_qh_split(qh: np.ndarray) -> np.ndarray:
@@ -340,6 +411,10 @@ def repack(raw: np.ndarray, ggml_type: int, n_rows: int, k: int) -> dict[str, np
     if t == GGMLType.Q4_K:
         return {"qs": pm(b[:, :, 16:144] ^ 0x80, 16),
                 "meta": np.ascontiguousarray(b[:, :, 0:16]).reshape(n_rows, 16 * sb)}
+    if t == GGMLType.Q5_K:
+        return {"qs": pm(b[:, :, 48:176], 16),
+                "meta": np.ascontiguousarray(b[:, :, 0:16]).reshape(n_rows, 16 * sb),
+                "qh": pm(_q5k_qh_split(b[:, :, 16:48]), 4)}
     if t == GGMLType.Q6_K:
         return {"ql": pm(b[:, :, 0:128], 16),
                 "qh": pm(_q6k_qh_split(b[:, :, 128:192]), 8),
@@ -363,11 +438,15 @@ def unrepack(streams: dict[str, np.ndarray], ggml_type: int, n_rows: int, k: int
     def bm(x, w):  # piece-major -> [rows, sb, 8 * w]
         return x.reshape(n_rows, 8, sb, w).transpose(0, 2, 1, 3).reshape(n_rows, sb, 8 * w)
 
-    if t in (GGMLType.Q4_K, GGMLType.Q6_K):
+    if t in (GGMLType.Q4_K, GGMLType.Q5_K, GGMLType.Q6_K):
         out = np.empty((n_rows, sb, nb), np.uint8)
         if t == GGMLType.Q4_K:
             out[:, :, 0:16] = s["meta"].reshape(n_rows, sb, 16)
             out[:, :, 16:144] = bm(s["qs"], 16) ^ 0x80
+        elif t == GGMLType.Q5_K:
+            out[:, :, 0:16] = s["meta"].reshape(n_rows, sb, 16)
+            out[:, :, 16:48] = _q5k_qh_join(bm(s["qh"], 4).reshape(n_rows, sb, 8, 4))
+            out[:, :, 48:176] = bm(s["qs"], 16)
         else:
             out[:, :, 0:128] = bm(s["ql"], 16)
             out[:, :, 128:192] = _q6k_qh_join(bm(s["qh"], 8).reshape(n_rows, sb, 8, 8))

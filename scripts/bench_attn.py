@@ -65,7 +65,7 @@ def attn_kps_sweep(C):
             out = torch.empty(1, H * D, device="cuda")
             S = max(1, min(32, 512 // Hkv))
             ws = torch.empty(max(1, C.attention_ws_floats(1, H, D, S)), device="cuda")
-            cnt = torch.zeros(Hkv, device="cuda", dtype=torch.int32)
+            cnt = torch.zeros(H, device="cuda", dtype=torch.int32)
             row = []
             for kps in (32, 64, 128, 256):
                 C.set_attn_tuning(kps)
@@ -75,6 +75,41 @@ def attn_kps_sweep(C):
                 row.append(f"kps={kps}:{timeit_graph(fn):6.2f}")
             print(f"attn(graph) H={H} Hkv={Hkv} L={L:5d} S<={S}  " + "  ".join(row) + "  (us)", flush=True)
     C.set_attn_tuning(256)
+
+
+def attn_hpb_sweep(C):
+    """Graph-timed decode attention vs query heads per block (GQA group split) and keys per split."""
+    bs = 16
+    for H, Hkv, D in ((64, 8, 128), (32, 8, 128), (32, 32, 128)):
+        for L in (128, 560, 2048):
+            nblk = (L + bs - 1) // bs
+            kc = torch.randn(nblk, Hkv, bs, D, device="cuda").half()
+            vc = torch.randn(nblk, Hkv, bs, D, device="cuda").half()
+            bt = torch.arange(nblk, device="cuda", dtype=torch.int32)
+            qlen = torch.tensor([L], device="cuda", dtype=torch.int32)
+            q = torch.randn(1, H * D, device="cuda")
+            out = torch.empty(1, H * D, device="cuda")
+            S = max(1, min(32, 512 // Hkv))
+            ws = torch.empty(max(1, C.attention_ws_floats(1, H, D, S)), device="cuda")
+            cnt = torch.zeros(H, device="cuda", dtype=torch.int32)
+            ref = None
+            for hpb in sorted({1, 2, 4, 8, H // Hkv}):
+                if hpb > H // Hkv:
+                    continue
+                row = []
+                for kps in (64, 128, 256):
+                    C.set_attn_tuning(kps, hpb)
+                    fn = lambda st: C.attention(q.data_ptr(), H * D, kc.data_ptr(), vc.data_ptr(), bt.data_ptr(), nblk,  # noqa
+                                                0, qlen.data_ptr(), 1, H, Hkv, D, bs, D ** -0.5, 0, out.data_ptr(), H * D,
+                                                ws.data_ptr(), S, cnt.data_ptr(), st)
+                    row.append(f"kps={kps}:{timeit_graph(fn):6.2f}")
+                    torch.cuda.synchronize()
+                    if ref is None:
+                        ref = out.clone()
+                    err = float((out - ref).abs().max())
+                    assert err < 1e-3, (H, Hkv, L, hpb, kps, err)
+                print(f"attn(graph) H={H} Hkv={Hkv} L={L:5d} hpb={hpb}  " + "  ".join(row) + "  (us)", flush=True)
+    C.set_attn_tuning(256, 0)
 
 
 def attn_sweep(C, s):
@@ -91,7 +126,7 @@ def attn_sweep(C, s):
             row = []
             for S in (1, 2, 4, 8, 16, 32):
                 ws = torch.empty(max(1, C.attention_ws_floats(1, H, D, S)), device="cuda")
-                cnt = torch.zeros(Hkv, device="cuda", dtype=torch.int32)
+                cnt = torch.zeros(H, device="cuda", dtype=torch.int32)
                 fn = lambda: C.attention(q.data_ptr(), H * D, kc.data_ptr(), vc.data_ptr(), bt.data_ptr(), nblk,  # noqa
                                          0, qlen.data_ptr(), 1, H, Hkv, D, bs, D ** -0.5, 0, out.data_ptr(), H * D,
                                          ws.data_ptr(), S, cnt.data_ptr(), s)
@@ -121,6 +156,9 @@ def gemv_fixed(C, s):
 def main():
     C = native()
     s = torch.cuda.current_stream().cuda_stream
+    if os.environ.get("OMX_BENCH_HPB"):
+        attn_hpb_sweep(C)
+        return
     if os.environ.get("OMX_BENCH_KPS"):
         attn_kps_sweep(C)
         return

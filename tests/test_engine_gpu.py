@@ -13,7 +13,8 @@ def rel(a, b):
     return float((a - b).norm() / (b.norm() + 1e-12))
 
 
-@pytest.mark.parametrize("name", ["tiny-llama", "tiny-mixtral", "tiny-phi2", "tiny-llama-q8", "tiny-llama-q40"])
+@pytest.mark.parametrize("name", ["tiny-llama", "tiny-mixtral", "tiny-phi2", "tiny-llama-q8", "tiny-llama-q40",
+                                  "tiny-llama-q5km", "tiny-mixtral-q5ks"])
 def test_native_vs_torch_teacher_forced(tiny_models, name):
     path = tiny_models[name]
     g = Runner(path, device="cuda", max_batch=8, max_seqs=2, ctx=128)
@@ -55,7 +56,8 @@ def test_long_context_splits(tiny_models):
     assert rel(g.logits[0, :V].cpu(), c.logits[0, :V]) < 3e-2
 
 
-@pytest.mark.parametrize("name", ["tiny-llama", "tiny-mixtral", "tiny-phi2", "tiny-llama-q8", "tiny-llama-q40"])
+@pytest.mark.parametrize("name", ["tiny-llama", "tiny-mixtral", "tiny-phi2", "tiny-llama-q8", "tiny-llama-q40",
+                                  "tiny-llama-q5km", "tiny-mixtral-q5ks"])
 def test_prefill_gemm_path_vs_torch(tiny_models, name):
     """Prompts >= GEMM_MIN_B take the MFMA GEMM path (and, for Mixtral, the device-sorted grouped
     expert GEMM with the routing-weighted scatter); logits must match the torch twin."""

@@ -32,7 +32,7 @@ def gemm(m, x, norm=0, nw=None, nb=None, epi=0, y=None, bias=None, extra=None, e
 @pytest.mark.parametrize("K", [256, 4096, 11008, 288])
 @pytest.mark.parametrize("split", [True, False])
 def test_gemm_store(qt, B, K, split):
-    if K == 288 and qt in (GGMLType.Q4_K, GGMLType.Q6_K):
+    if K == 288 and qt in (GGMLType.Q4_K, GGMLType.Q5_K, GGMLType.Q6_K):
         pytest.skip("k-quant rows are whole super-blocks")
     N = 384 + 64  # partial N tile
     m = QM(qt, N, K, seed=K + B)
@@ -70,7 +70,7 @@ def test_gemm_layernorm_gelu():
     assert rel(y, ref) < 1e-2
 
 
-@pytest.mark.parametrize("qt", [GGMLType.Q4_K, GGMLType.Q6_K])
+@pytest.mark.parametrize("qt", [GGMLType.Q4_K, GGMLType.Q5_K, GGMLType.Q6_K])
 def test_gemm_glu(qt):
     F, K, B = 320, 1024, 50
     m = QM(qt, 2 * F, K, seed=5)

@@ -8,7 +8,7 @@ from ollama_operator_amd.gguf.constants import BLOCK_GEOMETRY
 from ollama_operator_amd.quant import (dequantize, pack_q4k_scales, quantize, random_blocks, repack,
                                        unpack_q4k_scales, unrepack)
 
-QTYPES = [GGMLType.Q4_0, GGMLType.Q8_0, GGMLType.Q4_K, GGMLType.Q6_K]
+QTYPES = [GGMLType.Q4_0, GGMLType.Q8_0, GGMLType.Q4_K, GGMLType.Q5_K, GGMLType.Q6_K]
 
 
 def test_gguf_roundtrip(tmp_path):
@@ -68,14 +68,15 @@ def test_quant_error_bounded(t):
     x = rng.standard_normal(256 * 64).astype(np.float32)
     y = dequantize(quantize(x, t), t, x.size)
     rel = np.linalg.norm(y - x) / np.linalg.norm(x)
-    bound = {GGMLType.Q4_0: 0.12, GGMLType.Q8_0: 0.01, GGMLType.Q4_K: 0.12, GGMLType.Q6_K: 0.03}[t]
+    bound = {GGMLType.Q4_0: 0.12, GGMLType.Q8_0: 0.01, GGMLType.Q4_K: 0.12, GGMLType.Q5_K: 0.06,
+             GGMLType.Q6_K: 0.03}[t]
     assert rel < bound, rel
 
 
 @pytest.mark.parametrize("t", QTYPES)
 @pytest.mark.parametrize("k", [512, 288])
 def test_repack_roundtrip(t, k):
-    if k % 256 and t in (GGMLType.Q4_K, GGMLType.Q6_K):
+    if k % 256 and t in (GGMLType.Q4_K, GGMLType.Q5_K, GGMLType.Q6_K):
         pytest.skip("k-quants are whole super-blocks")
     rng = np.random.default_rng(2)
     n = 8
@@ -101,6 +102,19 @@ def _kernel_model_dequant(s, t, n, k):
                     w[r, 256 * b + 32 * t_: 256 * b + 32 * t_ + 32] = d * q
                     continue
                 a = s["qs" if t != GGMLType.Q6_K else "ql"][r].reshape(8, sb, 16)[t_, b]
+                if t == GGMLType.Q5_K:  # unsigned nibbles + 5th bit from the piece dword H
+                    m = s["meta"][r].reshape(sb, 16)[b]
+                    d, dmin = f16(m[0:2].copy())[0], f16(m[2:4].copy())[0]
+                    sc, mn = unpack_q4k_scales(m[4:16])
+                    H = int(s["qh"][r].reshape(8, sb, 4)[t_, b].view(np.uint32)[0])
+                    lo5 = np.array([(int(a[i]) & 15) | (((H >> (8 * (i & 3) + (i >> 2))) & 1) << 4) for i in range(16)])
+                    hi5 = np.array([(int(a[i]) >> 4) | (((H >> (8 * (i & 3) + 4 + (i >> 2))) & 1) << 4)
+                                    for i in range(16)])
+                    c, h = t_ >> 1, t_ & 1
+                    o = 256 * b + 64 * c + 16 * h
+                    w[r, o:o + 16] = d * sc[2 * c] * lo5 - dmin * mn[2 * c]
+                    w[r, o + 32:o + 48] = d * sc[2 * c + 1] * hi5 - dmin * mn[2 * c + 1]
+                    continue
                 lo = (a & 0x0F).astype(np.float32)
                 hi16 = (a & 0xF0).view(np.int8).astype(np.float32)  # = 16 * (n - 8) for 4-bit types
                 if t == GGMLType.Q4_0:
@@ -136,7 +150,7 @@ def _kernel_model_dequant(s, t, n, k):
 @pytest.mark.parametrize("t", QTYPES)
 def test_repack_kernel_contract(t):
     rng = np.random.default_rng(3)
-    n, k = 3, 512 if t in (GGMLType.Q4_K, GGMLType.Q6_K) else 288
+    n, k = 3, 512 if t in (GGMLType.Q4_K, GGMLType.Q5_K, GGMLType.Q6_K) else 288
     raw = random_blocks(t, n, k, rng)
     got = _kernel_model_dequant(repack(raw, t, n, k), t, n, k)
     np.testing.assert_allclose(got, dequantize(raw, t, n * k).reshape(n, k), rtol=1e-5, atol=1e-6)
@@ -148,3 +162,29 @@ def test_random_blocks_std(t):
     y = dequantize(random_blocks(t, 64, 1024, rng, std=0.02), t, 64 * 1024)
     assert 0.01 < y.std() < 0.04
     assert abs(y.mean()) < 0.01
+
+
+@pytest.mark.parametrize("t", QTYPES)
+def test_native_repack_matches_numpy(t):
+    """csrc/gguf/gguf.cpp repack_rows (the load path) == quant.repack (the layout spec), incl. a row
+    permutation (TP shards) and a K block range."""
+    from ollama_operator_amd.ops import native
+    from ollama_operator_amd.quant import REPACK_STREAMS, repack_row_bytes
+    try:
+        nat = native()
+    except Exception as e:  # extension not built in this environment
+        pytest.skip(str(e))
+    rng = np.random.default_rng(4)
+    n, k = 6, 1024
+    raw = random_blocks(t, n, k, rng)
+    blk = BLOCK_GEOMETRY[t][0]
+    kb0, kb1 = 256 // blk, 1024 // blk  # columns 256..1023
+    rows = np.array([5, 0, 3], np.int64)
+    dst_rows = np.arange(3, dtype=np.int64)
+    kk = (kb1 - kb0) * blk
+    dst = [np.zeros((3, b), np.uint8) for b in repack_row_bytes(t, kk)]
+    nat.repack_ptr(raw.ctypes.data, int(t), k, rows, dst_rows, kb0, kb1, [d.ctypes.data for d in dst], 2)
+    sub = raw.reshape(n, -1)[rows][:, kb0 * BLOCK_GEOMETRY[t][1]:kb1 * BLOCK_GEOMETRY[t][1]]
+    want = repack(np.ascontiguousarray(sub).reshape(-1), t, 3, kk)
+    for name, d in zip(REPACK_STREAMS[t], dst):
+        np.testing.assert_array_equal(d, want[name].reshape(3, -1), err_msg=name)

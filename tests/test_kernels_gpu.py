@@ -10,8 +10,8 @@ from ollama_operator_amd.quant import dequantize, quantize, random_blocks, repac
 
 pytestmark = pytest.mark.gpu
 
-QTYPES = [GGMLType.Q4_0, GGMLType.Q8_0, GGMLType.Q4_K, GGMLType.Q6_K]
-STREAMS = {GGMLType.Q4_K: ["qs", "meta"], GGMLType.Q6_K: ["ql", "qh", "sc", "d"],
+QTYPES = [GGMLType.Q4_0, GGMLType.Q8_0, GGMLType.Q4_K, GGMLType.Q5_K, GGMLType.Q6_K]
+STREAMS = {GGMLType.Q4_K: ["qs", "meta"], GGMLType.Q5_K: ["qs", "meta", "qh"], GGMLType.Q6_K: ["ql", "qh", "sc", "d"],
            GGMLType.Q4_0: ["qs", "d"], GGMLType.Q8_0: ["qs", "d"]}
 
 
@@ -61,7 +61,7 @@ def test_gemv_store(qt, B, K):
     assert rel(y, ref) < 1e-2
 
 
-@pytest.mark.parametrize("qt", [GGMLType.Q4_K, GGMLType.Q6_K])
+@pytest.mark.parametrize("qt", [GGMLType.Q4_K, GGMLType.Q5_K, GGMLType.Q6_K])
 def test_gemv_rmsnorm_add_bias(qt):
     N, K, B = 512, 2048, 2
     m = QM(qt, N, K, seed=3)
@@ -103,6 +103,7 @@ def test_gemv_glu():
 
 @pytest.mark.parametrize("ks", [1, 2, 3, 4])
 @pytest.mark.parametrize("qt,K", [(GGMLType.Q4_K, 11008), (GGMLType.Q6_K, 11008), (GGMLType.Q4_K, 4096),
+                                  (GGMLType.Q5_K, 11008), (GGMLType.Q5_K, 4096),
                                   (GGMLType.Q8_0, 2560), (GGMLType.Q6_K, 1024)])
 def test_gemv_flight_k_split(qt, K, ks):
     """The decode kernel's in-block K split (KS groups of 4 waves on the same rows, partial sums
@@ -160,9 +161,18 @@ def test_gemv_qkv_rope_kv_scatter(D, n_rot):
 
 
 @pytest.mark.parametrize("D", [64, 80, 128])
-@pytest.mark.parametrize("G", [1, 2, 4, 8])
+@pytest.mark.parametrize("G,hpb", [(1, 0), (2, 0), (4, 0), (4, 1), (4, 4), (8, 0), (8, 1), (8, 2), (8, 8), (3, 0)])
 @pytest.mark.parametrize("splits", [1, 5])
-def test_attention_paged(D, G, splits):
+def test_attention_paged(D, G, hpb, splits):
+    """Decode attention vs fp32 torch; hpb = query heads per block (GQA group split over blocks)."""
+    C().set_attn_tuning(256, hpb)
+    try:
+        _attention_paged(D, G, splits)
+    finally:
+        C().set_attn_tuning(256, 0)
+
+
+def _attention_paged(D, G, splits):
     Hkv, bs, NQ = 2, 16, 3
     H = Hkv * G
     lens = [1, 37, 200]
@@ -176,7 +186,7 @@ def test_attention_paged(D, G, splits):
     qlen = torch.tensor(lens, device="cuda", dtype=torch.int32)
     out = torch.zeros(NQ, H * D, device="cuda")
     ws = torch.zeros(max(1, C().attention_ws_floats(NQ, H, D, splits)), device="cuda")
-    cnt = torch.zeros(NQ * Hkv, device="cuda", dtype=torch.int32)
+    cnt = torch.zeros(NQ * H, device="cuda", dtype=torch.int32)
     scale = 1 / math.sqrt(D)
     for rep in range(3):  # tickets must re-arm themselves between launches
         out.zero_()

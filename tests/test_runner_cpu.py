@@ -9,7 +9,7 @@ from ollama_operator_amd.engine.sampling import SamplingOptions
 from ollama_operator_amd.gguf import read_gguf
 from ollama_operator_amd.models.reference import KVCacheRef, ReferenceModel
 
-MODELS = ["tiny-llama", "tiny-mixtral", "tiny-phi2", "tiny-llama-q8", "tiny-llama-q40"]
+MODELS = ["tiny-llama", "tiny-mixtral", "tiny-phi2", "tiny-llama-q8", "tiny-llama-q40", "tiny-llama-q5km"]
 
 
 @pytest.mark.parametrize("name", MODELS)
