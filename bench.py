@@ -114,6 +114,9 @@ def bench_server(a, url: str, model_path: str, vocab_words: int = 32000):
             out["concurrent_clients"] = P
             out["concurrent_aggregate_tok_s"] = round(sum(x["eval_count"] for x in res) / wall, 2)
             out["concurrent_per_client_tok_s"] = [round(x["eval_count"] / x["eval_duration"] * 1e9, 2) for x in res]
+            # decode-phase aggregate (what the batched steps deliver); the wall aggregate above also
+            # holds the P prefills and request ramp
+            out["concurrent_decode_tok_s"] = round(sum(out["concurrent_per_client_tok_s"]), 2)
     return out
 
 
@@ -200,6 +203,9 @@ def main():
     ap.add_argument("--via-server", type=int, default=1,
                     help="1 (default, single-GPU runs): also measure through the REST server (/api/generate) "
                          "and report it under extra.server")
+    ap.add_argument("--ttft-long", type=int, default=2048,
+                    help="also time prefill + first token of a prompt this long (extra.ttft_long_ms; 0 = skip)")
+    ap.add_argument("--chunk", type=int, default=2048, help="prefill chunk (MFMA GEMM M) = runner max_batch")
     ap.add_argument("--server-parallel", type=int, default=4,
                     help="OLLAMA_NUM_PARALLEL of the spawned server (concurrent clients measured)")
     a = ap.parse_args()
@@ -230,9 +236,9 @@ def main():
     else:
         ensure_model(path, a.model, a.ftype)
 
-    ctx = a.prompt + a.warmup + a.steps + 64
+    ctx = max(a.prompt + a.warmup + a.steps + 64, a.ttft_long + 8 if a.ttft_long else 0)
     t_load = time.perf_counter()
-    runner = Runner(path, device=f"cuda:{local}", max_batch=512, max_seqs=max(1, a.batch_extra), ctx=ctx)
+    runner = Runner(path, device=f"cuda:{local}", max_batch=a.chunk, max_seqs=max(2, a.batch_extra), ctx=ctx)
     runner.warmup()  # load-time decode-graph capture, as the server does at model load
     torch.cuda.synchronize()
     load_s = time.perf_counter() - t_load
@@ -268,6 +274,21 @@ def main():
     value = world * a.steps / dt
     gen.close()
     runner.free_sequence(sid)
+    ttft_long = None
+    if a.ttft_long:
+        p = [1] + torch.randint(3, runner.cfg.n_vocab, (a.ttft_long - 1,), generator=g).tolist()
+        best = None
+        for _ in range(3):  # prefill of a fresh sequence each time (no prefix reuse)
+            sid = runner.new_sequence()
+            torch.cuda.synchronize()
+            t_p = time.perf_counter()
+            gl = runner.generate(sid, p, opts, max_tokens=1)
+            next(gl)
+            dt_l = time.perf_counter() - t_p
+            gl.close()
+            runner.free_sequence(sid)
+            best = dt_l if best is None else min(best, dt_l)
+        ttft_long = round(best * 1e3, 2)
     batched = None
     if a.batch_extra > 1:
         batched = bench_batched(runner, a, rank, world, sync)
@@ -301,10 +322,11 @@ def main():
             "vs_baseline": None,
             "dtype": f"{a.ftype} weights, int8-dot activations, fp32 accumulate, fp16 KV",
             "data": f"synthetic prompt, random-init GGUF weights (real {a.ftype} tensor-type mix)",
-            "config": {"model": label, "global_batch": world, "seq_len": ctx,
+            "config": {"model": label, "global_batch": world, "seq_len": a.prompt + a.warmup + a.steps,
                        "parallelism": f"dp{world}", "prompt_tokens": a.prompt, "decode_batch_per_gpu": 1,
                        "sampling": "temperature 0.8, top_k 40, top_p 0.9, repeat_penalty 1.1 (on device)"},
-            "extra": {"ttft_ms": round(ttft * 1e3, 2), "load_s": round(load_s, 2),
+            "extra": {"ttft_ms": round(ttft * 1e3, 2), f"ttft_{a.ttft_long}_ms": ttft_long, "prefill_chunk": a.chunk,
+                      "load_s": round(load_s, 2),
                       "weights_gb": round(weights_gb, 3),
                       "continuous_batching": batched, "server": served},
         }), flush=True)

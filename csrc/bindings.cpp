@@ -42,8 +42,7 @@ static QMat qmat(py::object o) {
 
 static void check_attn(int H, int n_kv, int D) {
   if (n_kv <= 0 || H % n_kv) throw std::runtime_error("H must be a multiple of n_kv");
-  const int G = H / n_kv;
-  if (G != 1 && G != 2 && G != 4 && G != 8) throw std::runtime_error("unsupported GQA group size");
+  // any group size: decode blocks take a divisor of G in {1, 2, 4, 8} (attention.hip heads_per_block)
   if (D != 64 && D != 80 && D != 96 && D != 128) throw std::runtime_error("unsupported head dim");
 }
 
@@ -261,6 +260,12 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("add_inplace", [](uintptr_t y, uintptr_t x, long long n, uintptr_t stream) {
     add_inplace(Pp<float>(y), Pp<const float>(x), n, S(stream));
+  });
+  m.def("decode_feedback", [](uintptr_t step, int ld, uintptr_t sampled, int B, int advance, uintptr_t block_table,
+                              int max_blocks, int bs, uintptr_t stream) {
+    if (B <= 0 || B > ld) throw std::runtime_error("decode_feedback: bad B");
+    decode_feedback(Pp<int>(step), ld, Pp<const int>(sampled), B, advance, Pp<const int>(block_table), max_blocks,
+                    bs, S(stream));
   });
   m.def("sample", [](py::dict d, uintptr_t stream) {
     SampleParams P{};

@@ -475,11 +475,13 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(AttnParams P) {
   }
 }
 
-// query heads per block: the whole GQA group (one K/V read) unless the launch would be too narrow
-// to fill the chip; then groups of 2 (G = 4, 8) -- measured, scripts/bench_attn.py OMX_BENCH_HPB
+// query heads per block: the whole GQA group (one K/V read) unless the launch would be too narrow to
+// fill the chip; then one head per block (K/V re-reads hit L2/MALL). Measured (profiles/r2_attn,
+// scripts/bench_attn.py OMX_BENCH_HPB): H 64 / 8 KV heads, 560 keys: 9.4 us at 1 head per block vs
+// 23.5 us with the whole group of 8 (Llama-2-70B decode); H 32 / 8, 560 keys: 8.5 vs 14.6 us
 static int heads_per_block(const AttnParams& P) {
   const int G = P.H / P.n_kv;
-  int hpb = g_attn_hpb > 0 ? g_attn_hpb : (G >= 4 && P.NQ * P.n_kv < 64 ? 2 : G);
+  int hpb = g_attn_hpb > 0 ? g_attn_hpb : (P.NQ * P.n_kv < 64 ? 1 : G);
   while (hpb > 1 && (G % hpb || (hpb != 1 && hpb != 2 && hpb != 4 && hpb != 8))) --hpb;
   return hpb < 1 ? 1 : hpb;
 }

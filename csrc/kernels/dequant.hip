@@ -69,6 +69,31 @@ void add_inplace(float* y, const float* x, long long n, hipStream_t s) {
   hipLaunchKernelGGL(add_inplace_kernel, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, s, y, x, n);
 }
 
+// Decode-step feedback, the last node of every decode graph: row b's sampled token becomes its next
+// input (step row 5), and with `advance` (B == 1 pipelined decode) the step inputs move to the next
+// position on device -- pos + 1, its KV slot from the block table, q_len -- so consecutive replays
+// need no host upload (no H2D copy or torch kernel inside the step). step: int32 [6][ld] =
+// (pos, slot, q_len, q_seq, logit_idx, tokens), engine/runner.py d_step.
+__global__ void decode_feedback_kernel(int* step, int ld, const int* sampled, int B, int advance,
+                                       const int* block_table, int max_blocks, int bs) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  step[5 * ld + b] = sampled[b];
+  if (!advance) return;
+  const int pos = step[b] + 1;
+  const int row = step[3 * ld + b];
+  const int bi = min(pos / bs, max_blocks - 1);  // past the context end the host re-uploads anyway
+  step[b] = pos;
+  step[ld + b] = block_table[(long long)row * max_blocks + bi] * bs + pos % bs;
+  step[2 * ld + b] = pos + 1;
+}
+
+void decode_feedback(int* step, int ld, const int* sampled, int B, int advance, const int* block_table,
+                     int max_blocks, int bs, hipStream_t s) {
+  hipLaunchKernelGGL(decode_feedback_kernel, dim3((B + 63) / 64), dim3(64), 0, s, step, ld, sampled, B, advance,
+                     block_table, max_blocks, bs);
+}
+
 __global__ __launch_bounds__(256) void rmsnorm_kernel(const float* x, const float* w, float eps, int n, float* out) {
   __shared__ float red[4];
   const float* xr = x + (long long)blockIdx.x * n;

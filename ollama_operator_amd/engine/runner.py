@@ -177,6 +177,7 @@ class Runner:
         self._defer_ok = (self.is_gpu and os.environ.get("OMX_DEFER_MERGE", "1") != "0" and
                           native().gemv_merge_supported(1, Eq, loc["D"], 8) and self.n_splits(1) >= 8)
         self._decode_S = 0
+        self._adv_next = None  # (sid, pos) the device step inputs were advanced to by the last decode
         # TP decode collectives: one-shot all-reduce over peer-mapped slabs (parallel/custom_ar.py),
         # decode-size messages only (<= ~1 MB); prefill chunks keep RCCL
         self.ar = None
@@ -266,6 +267,7 @@ class Runner:
     def _upload(self, arr: np.ndarray, tokens: np.ndarray | None):
         """arr: int32 [5, B] = (pos, slot, qlen, qseq, logit_idx)."""
         B = arr.shape[1]
+        self._adv_next = None  # device step inputs no longer follow the last B == 1 decode
         if self.is_gpu:
             buf = self._pinned[self._pin_i]
             self._pin_i = (self._pin_i + 1) % len(self._pinned)
@@ -279,15 +281,18 @@ class Runner:
                 self.d_tokens[:len(tokens)] = torch.from_numpy(tokens.astype(np.int32))
 
     def _sync_block_table(self, sid: int):
+        self._adv_next = None
         s = self.kv.seqs[sid]
         row = torch.tensor(s.blocks, dtype=torch.int32)
         self.d_block_table[s.row, :len(s.blocks)].copy_(row.to(self.device))
 
     # ------------------------------------------------------------------ sequences
     def new_sequence(self) -> int:
+        self._adv_next = None
         return self.kv.new_seq()
 
     def free_sequence(self, sid: int) -> None:
+        self._adv_next = None
         self.kv.free_seq(sid)
 
     def prefill(self, sid: int, tokens: list[int], want_logits: bool = True) -> None:
@@ -376,7 +381,12 @@ class Runner:
     def _decode_body(self, B: int):
         self.forward(B, B, use_idx=False)
         self._sample(B)
-        self.d_tokens[:B].copy_(self.s_out[:B])
+        if self.is_gpu:  # token feedback (+ B == 1: on-device advance to the next position)
+            native().decode_feedback(self.d_step.data_ptr(), self.d_step.shape[1], self.s_out.data_ptr(), B,
+                                     int(B == 1), self.d_block_table.data_ptr(), self.max_blocks, self.block_size,
+                                     stream_handle())
+        else:
+            self.d_tokens[:B].copy_(self.s_out[:B])
 
     def _graph(self, B: int):
         key = (B, self._decode_S)
@@ -436,13 +446,19 @@ class Runner:
         row b with sampler row b and feeds the sampled tokens back into d_tokens[:B]."""
         B = len(sids)
         arr = np.empty((5, B), np.int32)
+        reserved = False
         for b, (sid, pos) in enumerate(zip(sids, poss)):
             s = self.kv.seqs[sid]
             if pos + 1 > len(s.blocks) * self.block_size:
                 self.kv.reserve(sid, min(self.ctx, pos + 4 * self.block_size))
                 self._sync_block_table(sid)
+                reserved = True
             arr[:, b] = (pos, self.kv.slot(sid, pos), pos + 1, s.row, b)
-        self._upload(arr, None)
+        # B == 1: the previous step's feedback kernel already advanced the device inputs to exactly
+        # this (sequence, position) -- replay without any host upload
+        nxt = (sids[0], poss[0]) if B == 1 else None
+        if not (self.is_gpu and nxt is not None and not reserved and self._adv_next == nxt):
+            self._upload(arr, None)
         self._decode_S = self.decode_splits(poss[0] + 1) if B == 1 else 0
         try:
             with trace_range(f"decode B={B}"):
@@ -450,6 +466,8 @@ class Runner:
                     self._graph(B).replay()
                 else:
                     self._decode_body(B)
+            if nxt is not None and self.is_gpu:
+                self._adv_next = (nxt[0], nxt[1] + 1)
         finally:
             self._decode_S = 0
 

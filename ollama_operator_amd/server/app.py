@@ -18,6 +18,7 @@ import uuid
 from typing import Any, Iterator
 
 from fastapi import FastAPI, Request
+from starlette.concurrency import run_in_threadpool
 from fastapi.responses import JSONResponse, PlainTextResponse, Response, StreamingResponse
 
 from .. import __version__
@@ -254,10 +255,10 @@ def create_app(store: ModelStore | None = None, manager: ModelManager | None = N
                     manager.unload(model)
                     return {"model": model, "created_at": now_rfc3339(), "response": "", "done": True,
                             "done_reason": "unload"}
-                _load(body)
+                await run_in_threadpool(_load, body)
                 return {"model": model, "created_at": now_rfc3339(), "response": "", "done": True,
                         "done_reason": "load"}
-            lm, load_ns = _load(body)
+            lm, load_ns = await run_in_threadpool(_load, body)
             if body.get("raw"):
                 text = body.get("prompt", "")
             else:
@@ -283,14 +284,16 @@ def create_app(store: ModelStore | None = None, manager: ModelManager | None = N
 
         if body.get("stream", True):
             return _ndjson(events())
-        text_parts, final = [], None
-        for ev in events():
-            if ev["done"]:
-                final = ev
-            else:
-                text_parts.append(ev["response"])
-        final["response"] = "".join(text_parts)
-        return final
+        def collect():  # off the event loop: concurrent requests share batched decode steps
+            text_parts, final = [], None
+            for ev in events():
+                if ev["done"]:
+                    final = ev
+                else:
+                    text_parts.append(ev["response"])
+            final["response"] = "".join(text_parts)
+            return final
+        return await run_in_threadpool(collect)
 
     @app.post("/api/chat")
     async def api_chat(request: Request):
@@ -304,10 +307,10 @@ def create_app(store: ModelStore | None = None, manager: ModelManager | None = N
                     manager.unload(model)
                     return {"model": model, "created_at": now_rfc3339(), "message": {"role": "assistant", "content": ""},
                             "done": True, "done_reason": "unload"}
-                _load(body)
+                await run_in_threadpool(_load, body)
                 return {"model": model, "created_at": now_rfc3339(), "message": {"role": "assistant", "content": ""},
                         "done": True, "done_reason": "load"}
-            lm, load_ns = _load(body)
+            lm, load_ns = await run_in_threadpool(_load, body)
             text = render_chat(lm.template, msgs, lm.system, body.get("tools"))
             ids = lm.tokenizer.encode(text)
         except (StoreError, TemplateError) as e:
@@ -328,24 +331,26 @@ def create_app(store: ModelStore | None = None, manager: ModelManager | None = N
 
         if body.get("stream", True):
             return _ndjson(events())
-        parts, final = [], None
-        for ev in events():
-            if ev["done"]:
-                final = ev
-            else:
-                parts.append(ev["message"]["content"])
-        final["message"]["content"] = "".join(parts)
-        return final
+        def collect():
+            parts, final = [], None
+            for ev in events():
+                if ev["done"]:
+                    final = ev
+                else:
+                    parts.append(ev["message"]["content"])
+            final["message"]["content"] = "".join(parts)
+            return final
+        return await run_in_threadpool(collect)
 
     @app.post("/api/embed")
     async def api_embed(request: Request):
         body = await _json(request)
         t0 = time.perf_counter()
         try:
-            lm, load_ns = _load(body)
+            lm, load_ns = await run_in_threadpool(_load, body)
             inp = body.get("input", "")
             texts = [inp] if isinstance(inp, str) else list(inp)
-            embs, n = manager.embed(lm, texts, body.get("truncate", True))
+            embs, n = await run_in_threadpool(manager.embed, lm, texts, body.get("truncate", True))
         except StoreError as e:
             return _err(str(e), 404 if "not found" in str(e) else 400)
         return {"model": _model_of(body), "embeddings": embs, "total_duration": int((time.perf_counter() - t0) * 1e9),
@@ -355,8 +360,8 @@ def create_app(store: ModelStore | None = None, manager: ModelManager | None = N
     async def api_embeddings(request: Request):
         body = await _json(request)
         try:
-            lm, _ = _load(body)
-            embs, _ = manager.embed(lm, [body.get("prompt", "")])
+            lm, _ = await run_in_threadpool(_load, body)
+            embs, _ = await run_in_threadpool(manager.embed, lm, [body.get("prompt", "")])
         except StoreError as e:
             return _err(str(e), 404 if "not found" in str(e) else 400)
         return {"embedding": embs[0]}
@@ -392,7 +397,7 @@ def create_app(store: ModelStore | None = None, manager: ModelManager | None = N
         t_start = time.perf_counter()
         try:
             model = _model_of(body)
-            lm, load_ns = _load({"model": model, "keep_alive": body.get("keep_alive")})
+            lm, load_ns = await run_in_threadpool(_load, {"model": model, "keep_alive": body.get("keep_alive")})
             msgs = []
             for m in body.get("messages") or []:
                 c = m.get("content", "")
@@ -431,12 +436,15 @@ def create_app(store: ModelStore | None = None, manager: ModelManager | None = N
                                                             "completion_tokens": res.eval_count,
                                                             "total_tokens": res.prompt_eval_count + res.eval_count}}
             return _oa_stream(chunks())
-        parts, res = [], None
-        for piece, r in gen:
-            if r is None:
-                parts.append(piece)
-            else:
-                res = r
+        def collect():
+            parts, res = [], None
+            for piece, r in gen:
+                if r is None:
+                    parts.append(piece)
+                else:
+                    res = r
+            return parts, res
+        parts, res = await run_in_threadpool(collect)
         metrics.observe(res)
         return {"id": cid, "object": "chat.completion", "created": created, "model": model,
                 "system_fingerprint": "fp_omx",
@@ -451,7 +459,7 @@ def create_app(store: ModelStore | None = None, manager: ModelManager | None = N
         t_start = time.perf_counter()
         try:
             model = _model_of(body)
-            lm, load_ns = _load({"model": model})
+            lm, load_ns = await run_in_threadpool(_load, {"model": model})
             prompt = body.get("prompt", "")
             if isinstance(prompt, list):
                 prompt = prompt[0] if prompt else ""
@@ -468,12 +476,15 @@ def create_app(store: ModelStore | None = None, manager: ModelManager | None = N
                            "choices": [{"text": piece, "index": 0,
                                         "finish_reason": None if res is None else res.done_reason}]}
             return _oa_stream(chunks())
-        parts, res = [], None
-        for piece, r in gen:
-            if r is None:
-                parts.append(piece)
-            else:
-                res = r
+        def collect():
+            parts, res = [], None
+            for piece, r in gen:
+                if r is None:
+                    parts.append(piece)
+                else:
+                    res = r
+            return parts, res
+        parts, res = await run_in_threadpool(collect)
         return {"id": cid, "object": "text_completion", "created": created, "model": model,
                 "choices": [{"text": "".join(parts), "index": 0, "finish_reason": res.done_reason}],
                 "usage": {"prompt_tokens": res.prompt_eval_count, "completion_tokens": res.eval_count,
@@ -496,10 +507,10 @@ def create_app(store: ModelStore | None = None, manager: ModelManager | None = N
     async def oa_embeddings(request: Request):
         body = await _json(request)
         try:
-            lm, _ = _load({"model": _model_of(body)})
+            lm, _ = await run_in_threadpool(_load, {"model": _model_of(body)})
             inp = body.get("input", "")
             texts = [inp] if isinstance(inp, str) else list(inp)
-            embs, n = manager.embed(lm, texts)
+            embs, n = await run_in_threadpool(manager.embed, lm, texts)
         except StoreError as e:
             return JSONResponse({"error": {"message": str(e)}}, status_code=404)
         return {"object": "list", "data": [{"object": "embedding", "embedding": e, "index": i}

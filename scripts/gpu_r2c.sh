@@ -12,3 +12,5 @@ timeout -k 10 300 python -u bench.py --model llama2-7b --ftype Q5_K_M --steps 12
 tail -1 $O/bench_q5km.log
 timeout -k 10 300 python -u bench.py --model mistral-7b --ftype Q4_0 --steps 128 --prompt 512 --via-server 0 > $O/bench_mistral.log 2>&1 || { tail -20 $O/bench_mistral.log; exit 1; }
 tail -1 $O/bench_mistral.log
+timeout -k 10 400 python -u bench.py --steps 128 > $O/bench_server.log 2>&1 || { tail -20 $O/bench_server.log; exit 1; }
+tail -1 $O/bench_server.log
