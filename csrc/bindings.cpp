@@ -262,10 +262,27 @@ PYBIND11_MODULE(_C, m) {
     add_inplace(Pp<float>(y), Pp<const float>(x), n, S(stream));
   });
   m.def("decode_feedback", [](uintptr_t step, int ld, uintptr_t sampled, int B, int advance, uintptr_t block_table,
-                              int max_blocks, int bs, uintptr_t stream) {
+                              int max_blocks, int bs, uintptr_t host_ring, int ring, uintptr_t stream) {
     if (B <= 0 || B > ld) throw std::runtime_error("decode_feedback: bad B");
+    if (host_ring && ring <= 0) throw std::runtime_error("decode_feedback: bad ring");
     decode_feedback(Pp<int>(step), ld, Pp<const int>(sampled), B, advance, Pp<const int>(block_table), max_blocks,
-                    bs, S(stream));
+                    bs, Pp<int>(host_ring), ring, S(stream));
+  });
+  // host-mapped pinned buffer: (host pointer, device pointer); kernels store tokens into it directly
+  m.def("host_alloc_mapped", [](size_t bytes) {
+    void* h = nullptr;
+    void* d = nullptr;
+    if (hipHostMalloc(&h, bytes, hipHostMallocMapped) != hipSuccess || !h)
+      throw std::runtime_error("hipHostMalloc(mapped) failed");
+    if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess || !d) {
+      (void)hipHostFree(h);
+      throw std::runtime_error("hipHostGetDevicePointer failed");
+    }
+    std::memset(h, 0, bytes);
+    return py::make_tuple((uintptr_t)h, (uintptr_t)d);
+  });
+  m.def("host_free_mapped", [](uintptr_t h) {
+    if (h) (void)hipHostFree((void*)h);
   });
   m.def("sample", [](py::dict d, uintptr_t stream) {
     SampleParams P{};

@@ -74,11 +74,18 @@ void add_inplace(float* y, const float* x, long long n, hipStream_t s) {
 // position on device -- pos + 1, its KV slot from the block table, q_len -- so consecutive replays
 // need no host upload (no H2D copy or torch kernel inside the step). step: int32 [6][ld] =
 // (pos, slot, q_len, q_seq, logit_idx, tokens), engine/runner.py d_step.
+// host_ring (B == 1, optional): the sampled token also goes straight to host-mapped pinned memory,
+// slot = input position % ring, so the host reads it after the step's event (no D2H copy command).
 __global__ void decode_feedback_kernel(int* step, int ld, const int* sampled, int B, int advance,
-                                       const int* block_table, int max_blocks, int bs) {
+                                       const int* block_table, int max_blocks, int bs, int* host_ring, int ring) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
-  step[5 * ld + b] = sampled[b];
+  const int tok = sampled[b];
+  step[5 * ld + b] = tok;
+  if (host_ring && b == 0) {
+    __hip_atomic_store(host_ring + step[0] % ring, tok, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __threadfence_system();
+  }
   if (!advance) return;
   const int pos = step[b] + 1;
   const int row = step[3 * ld + b];
@@ -89,9 +96,9 @@ __global__ void decode_feedback_kernel(int* step, int ld, const int* sampled, in
 }
 
 void decode_feedback(int* step, int ld, const int* sampled, int B, int advance, const int* block_table,
-                     int max_blocks, int bs, hipStream_t s) {
+                     int max_blocks, int bs, int* host_ring, int ring, hipStream_t s) {
   hipLaunchKernelGGL(decode_feedback_kernel, dim3((B + 63) / 64), dim3(64), 0, s, step, ld, sampled, B, advance,
-                     block_table, max_blocks, bs);
+                     block_table, max_blocks, bs, host_ring, ring);
 }
 
 __global__ __launch_bounds__(256) void rmsnorm_kernel(const float* x, const float* w, float eps, int n, float* out) {

@@ -11,9 +11,11 @@ step behind, so the GPU never waits on Python.
 """
 from __future__ import annotations
 
+import ctypes
 import gc
 import os
 import time
+import weakref
 from dataclasses import dataclass
 from typing import Callable, Iterator
 
@@ -197,7 +199,13 @@ class Runner:
             self._pinned = [torch.zeros(5, max_batch, dtype=torch.int32).pin_memory() for _ in range(4)]
             self._pin_i = 0
             self._tok_host = torch.zeros(max_batch, dtype=torch.int32).pin_memory()
-            self._tok_ring = torch.zeros(4, dtype=torch.int32).pin_memory()  # sampled tokens, per step
+            # sampled tokens of the B == 1 steps, written by the feedback kernel straight into host-mapped
+            # pinned memory (slot = input position % ring): no D2H copy command per step
+            self._ring_n = 8
+            h, d = native().host_alloc_mapped(4 * self._ring_n)
+            self._host_ring_dev = d
+            self._host_ring = np.ctypeslib.as_array((ctypes.c_int32 * self._ring_n).from_address(h))
+            weakref.finalize(self, native().host_free_mapped, h)
         self.load_s = time.perf_counter() - t0
 
     def close(self) -> None:
@@ -384,7 +392,7 @@ class Runner:
         if self.is_gpu:  # token feedback (+ B == 1: on-device advance to the next position)
             native().decode_feedback(self.d_step.data_ptr(), self.d_step.shape[1], self.s_out.data_ptr(), B,
                                      int(B == 1), self.d_block_table.data_ptr(), self.max_blocks, self.block_size,
-                                     stream_handle())
+                                     self._host_ring_dev if B == 1 else 0, self._ring_n, stream_handle())
         else:
             self.d_tokens[:B].copy_(self.s_out[:B])
 
@@ -490,19 +498,17 @@ class Runner:
         leaving the GPU idle between steps (was ~130 us per step, profiles/r1_attn). A step issued
         past a stop is wasted work whose KV position is never recorded in `tokens`."""
         base = st.length  # position of `first`
-        ring = self._tok_ring
-        R = ring.numel()
+        ring = self._host_ring  # host-mapped: step at input position p stores its token at p % R
+        R = self._ring_n
         evs: list = [None] * R
         issued = 0
 
         def issue():
             nonlocal issued
             self.decode_step(sid, base + issued)
-            slot = issued % R
-            ring[slot:slot + 1].copy_(self.s_out[:1], non_blocking=True)
             e = torch.cuda.Event()
             e.record()
-            evs[slot] = e
+            evs[(base + issued) % R] = e
             issued += 1
 
         n = 0
@@ -519,7 +525,7 @@ class Runner:
                 yield tok
                 if done:
                     break
-                slot = (n - 1) % R  # step n-1 produced token n+1
+                slot = (base + n - 1) % R  # step n-1 produced token n+1
                 evs[slot].synchronize()
                 tok = int(ring[slot])
         finally:

@@ -42,6 +42,8 @@ def _ndjson(it: Iterator[dict]) -> StreamingResponse:
                 yield json.dumps(ev) + "\n"
         except (PullError, StoreError, TemplateError) as e:
             yield json.dumps({"error": str(e)}) + "\n"
+        except Exception as e:  # engine failure mid-stream: Ollama ends the stream with an error line
+            yield json.dumps({"error": f"{type(e).__name__}: {e}"}) + "\n"
     return StreamingResponse(gen(), media_type="application/x-ndjson")
 
 
@@ -66,6 +68,13 @@ def create_app(store: ModelStore | None = None, manager: ModelManager | None = N
     app.state.store = store
     app.state.manager = manager
     metrics = _Metrics()
+
+    @app.exception_handler(Exception)
+    async def _engine_error(request: Request, exc: Exception):
+        # an engine failure (HIP error, out of KV blocks, ...) answers as Ollama does -- {"error"} with
+        # 500 -- and the server keeps serving (the failed request's rows are released by the runner /
+        # scheduler; tests/test_server.py::test_engine_fault_injection)
+        return JSONResponse({"error": f"{type(exc).__name__}: {exc}"}, status_code=500)
 
     preload = os.environ.get("OMX_PRELOAD")
     if preload:  # operator-managed model pods load weights at start-up (the probe stays /api/tags)

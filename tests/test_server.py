@@ -325,3 +325,55 @@ def test_concurrent_generate_batched(client):
     for t in th:
         t.join(60)
     assert got == alone
+
+
+@pytest.mark.parametrize("parallel", ["1", "4"])
+def test_engine_fault_injection(tmp_path, tiny_models, monkeypatch, parallel):
+    """A decode step that fails mid-generation (injected, as a HIP error would) answers that request
+    with Ollama's {"error"} / 500; the model stays loaded and the next request matches a clean run."""
+    monkeypatch.setenv("OLLAMA_NUM_PARALLEL", parallel)
+    st = ModelStore(str(tmp_path / "store"))
+    st.create("tiny", gguf_path=tiny_models["tiny-llama"], params={"temperature": 0.0, "num_ctx": 128})
+    mgr = ModelManager(st, device="cpu")
+    c = TestClient(create_app(st, mgr), raise_server_exceptions=False)
+    body = {"model": "tiny", "prompt": "alpha beta gamma", "stream": False, "options": {"num_predict": 8}}
+    clean = c.post("/api/generate", json=body).json()["response"]
+    runner = mgr.get("tiny").runner
+    real = runner.decode_batch
+    calls = {"n": 0}
+
+    def flaky(*a, **k):
+        calls["n"] += 1
+        if calls["n"] == 3:
+            raise RuntimeError("injected: hipErrorLaunchFailure")
+        return real(*a, **k)
+
+    monkeypatch.setattr(runner, "decode_batch", flaky)
+    r = c.post("/api/generate", json=body)
+    assert r.status_code == 500 and "injected" in r.json()["error"]
+    again = c.post("/api/generate", json=body)
+    assert again.status_code == 200 and again.json()["response"] == clean
+    assert mgr.get("tiny").runner is runner  # not reloaded: the failure stayed with its request
+
+
+def test_engine_fault_mid_stream(tmp_path, tiny_models, monkeypatch):
+    """Streaming: an engine failure ends the NDJSON stream with an {"error"} line, as Ollama does."""
+    monkeypatch.setenv("OLLAMA_NUM_PARALLEL", "1")
+    st = ModelStore(str(tmp_path / "store"))
+    st.create("tiny", gguf_path=tiny_models["tiny-llama"], params={"temperature": 0.0, "num_ctx": 128})
+    mgr = ModelManager(st, device="cpu")
+    c = TestClient(create_app(st, mgr), raise_server_exceptions=False)
+    runner = mgr.get("tiny").runner
+    real, calls = runner.decode_batch, {"n": 0}
+
+    def flaky(*a, **k):
+        calls["n"] += 1
+        if calls["n"] == 4:
+            raise RuntimeError("injected fault")
+        return real(*a, **k)
+
+    monkeypatch.setattr(runner, "decode_batch", flaky)
+    lines = [json.loads(x) for x in c.post("/api/generate", json={"model": "tiny", "prompt": "a b c",
+                                                                  "options": {"num_predict": 12}}).iter_lines() if x]
+    assert "injected fault" in lines[-1]["error"]
+    assert not any(x.get("done") for x in lines)
