@@ -6,9 +6,9 @@
 //    weight row for EVERY quant type (Q4_K: two sub-block pairs, Q6_K: one 128-weight half, Q4_0 /
 //    Q8_0: four 32-blocks), so the dequant unit is uniform. 4 waves, each a 64 x 64 sub-tile of
 //    2 x 2 `v_mfma_f32_32x32x16_f16` accumulators (64 fp32 acc registers per lane).
-//  * Dequant is fused into the LDS staging: the next K step's raw quant bytes (+ scales) and fp16
-//    activation tile are loaded into registers right after the barrier and stay in flight through
-//    the MFMA work of the current step (register-staged pipeline, "write after barrier"); the
+//  * Dequant is fused into the LDS staging: the raw quant bytes (+ scales) and fp16 activation tile
+//    of the step two ahead are loaded into one of two register stages right after the barrier and
+//    stay in flight through the MFMA work of two steps (register-staged pipeline); the
 //    weights cross HBM once per 128 prompt tokens instead of once per 4 (batched GEMV).
 //  * Both operands use the same "8 consecutive K of one row" fragment (A = X rows, B = W rows, see
 //    the gfx950 32x32x16 lane map), so X and dequantised W share one padded row-major LDS format:
@@ -268,7 +268,7 @@ __device__ __forceinline__ void dequant_store(const WRaw<QT>& R, int ks, int pp,
 }
 
 template <int QT, bool GROUPED = false>
-__global__ __launch_bounds__(GM_NT) void qgemm_kernel(GemvParams P, const f16* __restrict__ X) {
+__global__ __launch_bounds__(GM_NT, 2) void qgemm_kernel(GemvParams P, const f16* __restrict__ X) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   f16* Xs = (f16*)smem;             // [BM][LD]
   f16* Ws = Xs + GM_BM * GM_LD;     // [BN][LD]
@@ -293,10 +293,15 @@ __global__ __launch_bounds__(GM_NT) void qgemm_kernel(GemvParams P, const f16* _
   const long long wrow = row_base + min(n0 + srow, N - 1);
   const f16* xrow = X + (long long)min(m0 + srow, M - 1) * K;
 
-  WRaw<QT> wr;
+  // quant bytes in two register stages (A, B): the weights of K step ks + 2 (HBM) are requested while
+  // ks + 1's wait in the other stage, so two steps of MFMA work cover their latency; the fp16
+  // activation tile (L2-resident, shared by every N tile) keeps one stage, issued one step ahead.
+  // One stage for both left the MFMA pipe mostly idle at the barrier (313 TFLOP/s at M = 2048,
+  // profiles/r1_gemm); both in two stages needs > 256 VGPRs (1 wave per SIMD)
+  WRaw<QT> wrA, wrB;
   f16x8 xr[8];
-  auto issue = [&](int ks) {
-    load_wraw<QT>(w, wrow, SB, ks, 2 * spart, wr);
+  auto issue_w = [&](int ks, WRaw<QT>& wr) { load_wraw<QT>(w, wrow, SB, ks, 2 * spart, wr); };
+  auto issue_x = [&](int ks) {
     const int k0 = ks * GM_BK + 64 * spart;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -315,14 +320,14 @@ __global__ __launch_bounds__(GM_NT) void qgemm_kernel(GemvParams P, const f16* _
 
   const int wm = wave >> 1, wn = wave & 1;
   const int fr = lane & 31, fk = 8 * (lane >> 5);
-  issue(ks0);
-  for (int ks = ks0; ks < ks1; ++ks) {
+  auto step = [&](int ks, WRaw<QT>& wr) {
     __syncthreads();  // the previous step's fragment reads are done
 #pragma unroll
     for (int j = 0; j < 8; ++j) *(f16x8*)(Xs + srow * GM_LD + 64 * spart + 8 * j) = xr[j];
     dequant_store<QT>(wr, ks, 2 * spart, Ws + srow * GM_LD);
     __syncthreads();
-    if (ks + 1 < ks1) issue(ks + 1);  // in flight during this step's MFMAs
+    if (ks + 1 < ks1) issue_x(ks + 1);      // in flight during this step's MFMAs
+    if (ks + 2 < ks1) issue_w(ks + 2, wr);  // this stage is free again: two steps ahead
 #pragma unroll
     for (int kk = 0; kk < GM_BK / 16; ++kk) {
       f16x8 a[2], b[2];
@@ -335,6 +340,14 @@ __global__ __launch_bounds__(GM_NT) void qgemm_kernel(GemvParams P, const f16* _
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[i], b[j], acc[i][j], 0, 0, 0);
     }
+  };
+  issue_w(ks0, wrA);
+  issue_x(ks0);
+  if (ks0 + 1 < ks1) issue_w(ks0 + 1, wrB);
+  for (int ks = ks0; ks < ks1; ks += 2) {
+    step(ks, wrA);
+    if (ks + 1 >= ks1) break;
+    step(ks + 1, wrB);
   }
 
   // C map: row = (r&3) + 8(r>>2) + 4(lane>>5), col = lane&31

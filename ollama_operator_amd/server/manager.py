@@ -148,7 +148,7 @@ class ModelManager:
         ctx_cap = int(os.environ.get("OMX_MAX_CTX", "0")) or None
         ctx = min(num_ctx, ctx_cap) if ctx_cap else num_ctx
         # prefill chunk = MFMA GEMM M dimension (weights cross HBM once per chunk)
-        chunk = int(os.environ.get("OMX_PREFILL_CHUNK", "512"))
+        chunk = int(os.environ.get("OMX_PREFILL_CHUNK", "2048"))  # 2048-token TTFT 117 -> 94 ms vs 512
         scheduler = None
         if self.tp_world is not None:  # tensor parallel: every rank loads its shard (parallel/tp.py)
             from ..parallel.tp import load_tp_runner
