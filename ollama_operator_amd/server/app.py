@@ -13,6 +13,7 @@ from __future__ import annotations
 import hashlib
 import json
 import os
+import threading
 import time
 import uuid
 from typing import Any, Iterator
@@ -31,11 +32,18 @@ from .template import TemplateError, render_chat, render_generate
 OLLAMA_COMPAT_VERSION = "0.5.4"
 
 
+def is_device_fault(exc: BaseException) -> bool:
+    """A HIP runtime error (sticky: the context is lost), as opposed to an engine-level failure."""
+    name = type(exc).__name__
+    msg = str(exc)
+    return name == "AcceleratorError" or "HIP error" in msg or "hipError" in msg
+
+
 def _err(msg: str, code: int = 400) -> JSONResponse:
     return JSONResponse({"error": msg}, status_code=code)
 
 
-def _ndjson(it: Iterator[dict]) -> StreamingResponse:
+def _ndjson(it: Iterator[dict], on_fault=None) -> StreamingResponse:
     def gen():
         try:
             for ev in it:
@@ -43,6 +51,8 @@ def _ndjson(it: Iterator[dict]) -> StreamingResponse:
         except (PullError, StoreError, TemplateError) as e:
             yield json.dumps({"error": str(e)}) + "\n"
         except Exception as e:  # engine failure mid-stream: Ollama ends the stream with an error line
+            if on_fault is not None and is_device_fault(e):
+                on_fault()
             yield json.dumps({"error": f"{type(e).__name__}: {e}"}) + "\n"
     return StreamingResponse(gen(), media_type="application/x-ndjson")
 
@@ -69,11 +79,18 @@ def create_app(store: ModelStore | None = None, manager: ModelManager | None = N
     app.state.manager = manager
     metrics = _Metrics()
 
+    # GPU health: a HIP runtime fault leaves the device context unusable, so after
+    # answering the request the process exits non-zero and Kubernetes restarts the pod
+    # (liveness / restartPolicy); tests replace the hook
+    app.state.on_device_fault = lambda: threading.Timer(0.2, os._exit, args=(70,)).start()
+
     @app.exception_handler(Exception)
     async def _engine_error(request: Request, exc: Exception):
-        # an engine failure (HIP error, out of KV blocks, ...) answers as Ollama does -- {"error"} with
-        # 500 -- and the server keeps serving (the failed request's rows are released by the runner /
-        # scheduler; tests/test_server.py::test_engine_fault_injection)
+        # an engine failure answers as Ollama does -- {"error"} with 500. Recoverable ones (out of KV
+        # blocks, a bad request that got this far) keep the server serving: the failed request's rows
+        # are released by the runner / scheduler (tests/test_server.py::test_engine_fault_injection)
+        if is_device_fault(exc):
+            app.state.on_device_fault()
         return JSONResponse({"error": f"{type(exc).__name__}: {exc}"}, status_code=500)
 
     preload = os.environ.get("OMX_PRELOAD")
@@ -292,7 +309,7 @@ def create_app(store: ModelStore | None = None, manager: ModelManager | None = N
                     yield d
 
         if body.get("stream", True):
-            return _ndjson(events())
+            return _ndjson(events(), lambda: app.state.on_device_fault())
         def collect():  # off the event loop: concurrent requests share batched decode steps
             text_parts, final = [], None
             for ev in events():
@@ -339,7 +356,7 @@ def create_app(store: ModelStore | None = None, manager: ModelManager | None = N
                     yield d
 
         if body.get("stream", True):
-            return _ndjson(events())
+            return _ndjson(events(), lambda: app.state.on_device_fault())
         def collect():
             parts, final = [], None
             for ev in events():

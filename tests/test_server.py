@@ -345,7 +345,7 @@ def test_engine_fault_injection(tmp_path, tiny_models, monkeypatch, parallel):
     def flaky(*a, **k):
         calls["n"] += 1
         if calls["n"] == 3:
-            raise RuntimeError("injected: hipErrorLaunchFailure")
+            raise RuntimeError("injected: no free KV blocks")
         return real(*a, **k)
 
     monkeypatch.setattr(runner, "decode_batch", flaky)
@@ -354,6 +354,28 @@ def test_engine_fault_injection(tmp_path, tiny_models, monkeypatch, parallel):
     again = c.post("/api/generate", json=body)
     assert again.status_code == 200 and again.json()["response"] == clean
     assert mgr.get("tiny").runner is runner  # not reloaded: the failure stayed with its request
+
+
+def test_device_fault_exits_process(tmp_path, tiny_models, monkeypatch):
+    """A HIP runtime fault is not recoverable in-process: the request gets {"error"} / 500 and the
+    server's device-fault hook (default: exit 70 -> Kubernetes restarts the pod) fires."""
+    monkeypatch.setenv("OLLAMA_NUM_PARALLEL", "1")
+    st = ModelStore(str(tmp_path / "store"))
+    st.create("tiny", gguf_path=tiny_models["tiny-llama"], params={"temperature": 0.0, "num_ctx": 128})
+    mgr = ModelManager(st, device="cpu")
+    app = create_app(st, mgr)
+    fired = []
+    app.state.on_device_fault = lambda: fired.append(1)
+    c = TestClient(app, raise_server_exceptions=False)
+    runner = mgr.get("tiny").runner
+
+    def broken(*a, **k):
+        raise RuntimeError("HIP error: an illegal memory access was encountered")
+
+    monkeypatch.setattr(runner, "decode_batch", broken)
+    r = c.post("/api/generate", json={"model": "tiny", "prompt": "x", "stream": False, "options": {"num_predict": 4}})
+    assert r.status_code == 500 and "HIP error" in r.json()["error"]
+    assert fired == [1]
 
 
 def test_engine_fault_mid_stream(tmp_path, tiny_models, monkeypatch):
