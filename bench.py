@@ -63,6 +63,8 @@ def start_server(a, model_path: str):
     log = open(os.path.join(a.dir, f"server-{port}.log"), "w")
     proc = subprocess.Popen([sys.executable, "-m", "ollama_operator_amd", "serve"], env=env, cwd=ROOT,
                             stdout=log, stderr=subprocess.STDOUT, start_new_session=True)
+    import atexit
+    atexit.register(stop_server, proc)  # never leave the child behind, also when the bench fails
     return proc, f"http://127.0.0.1:{port}"
 
 
@@ -74,7 +76,7 @@ def bench_server(a, url: str, model_path: str, vocab_words: int = 32000):
     import random
 
     import httpx
-    deadline = time.time() + 120
+    deadline = time.time() + 300  # a fresh box pages torch in for 1-2 min
     with httpx.Client(base_url=url, timeout=600) as c:
         while True:
             try:
@@ -122,6 +124,8 @@ def bench_server(a, url: str, model_path: str, vocab_words: int = 32000):
 
 def stop_server(proc):
     import signal
+    if proc.poll() is not None:
+        return
     try:
         os.killpg(proc.pid, signal.SIGTERM)
         proc.wait(timeout=30)
