@@ -25,7 +25,7 @@ static QMat qmat(py::object o) {
   QMat m{};
   if (o.is_none()) return m;
   auto t = o.cast<py::tuple>();
-  if (t.size() != 7) throw std::runtime_error("qmat tuple must be (s0, s1, s2, s3, N, K, qtype)");
+  if (t.size() != 7 && t.size() != 8) throw std::runtime_error("qmat tuple must be (s0, s1, s2, s3, N, K, qtype[, s4])");
   m.s0 = Pp<const uint8_t>(t[0].cast<uintptr_t>());
   m.s1 = Pp<const uint8_t>(t[1].cast<uintptr_t>());
   m.s2 = Pp<const uint8_t>(t[2].cast<uintptr_t>());
@@ -33,6 +33,8 @@ static QMat qmat(py::object o) {
   m.N = t[4].cast<int>();
   m.K = t[5].cast<int>();
   m.qtype = t[6].cast<int>();
+  m.s4 = t.size() == 8 ? Pp<const uint8_t>(t[7].cast<uintptr_t>()) : nullptr;
+  if (m.s4 && m.qtype != QT_Q6_K) throw std::runtime_error("widened codes are for Q6_K only");
   if (m.qtype != QT_Q4_0 && m.qtype != QT_Q8_0 && m.qtype != QT_Q4_K && m.qtype != QT_Q5_K && m.qtype != QT_Q6_K)
     throw std::runtime_error("unsupported device quant type " + std::to_string(m.qtype));
   const int blk = (m.qtype == QT_Q4_K || m.qtype == QT_Q5_K || m.qtype == QT_Q6_K) ? 256 : 32;
@@ -267,6 +269,11 @@ PYBIND11_MODULE(_C, m) {
     if (host_ring && ring <= 0) throw std::runtime_error("decode_feedback: bad ring");
     decode_feedback(Pp<int>(step), ld, Pp<const int>(sampled), B, advance, Pp<const int>(block_table), max_blocks,
                     bs, Pp<int>(host_ring), ring, S(stream));
+  });
+  m.def("widen_q6k", [](py::object w, uintptr_t out, uintptr_t stream) {
+    QMat q = qmat(w);
+    if (q.qtype != QT_Q6_K || !out) throw std::runtime_error("widen_q6k: Q6_K matrix and output required");
+    widen_q6k(q, Pp<void>(out), S(stream));
   });
   // host-mapped pinned buffer: (host pointer, device pointer); kernels store tokens into it directly
   m.def("host_alloc_mapped", [](size_t bytes) {

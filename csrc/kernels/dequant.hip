@@ -59,6 +59,48 @@ void dequant_f16(const QMat& w, void* out, hipStream_t s) {
   hipLaunchKernelGGL(dequant_f16_kernel, dim3(blocks), dim3(256), 0, s, w, (f16*)out);
 }
 
+// Q6_K -> QT_Q6_K8 widening at load (qmat.h): one thread per (row, super-block, piece) writes the
+// piece's 32 signed codes q - 32 (lo 16 | hi 16 weights), in the Q6_K piece order the GEMV uses
+__global__ void widen_q6k_kernel(QMat w, int8_t* out) {
+  const int SB = n_sb(w.K);
+  const long long total = (long long)w.N * SB * 8;
+  for (long long u = (long long)blockIdx.x * blockDim.x + threadIdx.x; u < total;
+       u += (long long)gridDim.x * blockDim.x) {
+    const long long row = u / (SB * 8);
+    const int rem = (int)(u % (SB * 8)), t = rem / SB, sb = rem % SB;
+    const long long pi = (long long)t * SB + sb;
+    const u32x4 ql = *(const u32x4*)(w.s0 + row * SB * 128 + 16 * pi);
+    const u32x2 qh = *(const u32x2*)(w.s1 + row * SB * 64 + 8 * pi);
+    const unsigned L[4] = {ql.x, ql.y, ql.z, ql.w};
+    int8_t c[32];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const unsigned lb = (L[i >> 2] >> (8 * (i & 3))) & 0xFF;
+      const int sh = 8 * (i & 3) + 2 * (i >> 2);  // field (i >> 2) of byte (i & 3)
+      c[i] = (int8_t)((int)((lb & 0xF) | (((qh.x >> sh) & 3) << 4)) - 32);
+      c[16 + i] = (int8_t)((int)((lb >> 4) | (((qh.y >> sh) & 3) << 4)) - 32);
+    }
+    int8_t* o = out + row * SB * 256 + 32 * pi;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      u32x4 v;
+      unsigned wd[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        wd[j] = (unsigned)(uint8_t)c[16 * k + 4 * j] | ((unsigned)(uint8_t)c[16 * k + 4 * j + 1] << 8) |
+                ((unsigned)(uint8_t)c[16 * k + 4 * j + 2] << 16) | ((unsigned)(uint8_t)c[16 * k + 4 * j + 3] << 24);
+      v.x = wd[0]; v.y = wd[1]; v.z = wd[2]; v.w = wd[3];
+      *(u32x4*)(o + 16 * k) = v;
+    }
+  }
+}
+
+void widen_q6k(const QMat& w, void* out, hipStream_t s) {
+  const long long total = (long long)w.N * ((w.K + 255) / 256) * 8;
+  const int blocks = (int)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192);
+  hipLaunchKernelGGL(widen_q6k_kernel, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, s, w, (int8_t*)out);
+}
+
 __global__ void add_inplace_kernel(float* y, const float* x, long long n) {
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
     y[i] += x[i];

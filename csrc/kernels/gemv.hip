@@ -50,7 +50,7 @@ void set_gemv_tuning(int blocks_per_cu, int rows, int debug, int ks, int xfirst)
 // the loaded words (memory path alone), bit 1 = skip the activation prologue
 template <int QT, int NSB, int R, int BT, int DBG = 0>
 __global__ __launch_bounds__(GEMV_NT) void qgemv_kernel(GemvParams P) {
-  constexpr int PB = QT == QT_Q8_0 ? 8 : QT == QT_Q6_K ? 6 : QT == QT_Q5_K ? 5 : 4;  // VGPRs per piece
+  constexpr int PB = (QT == QT_Q8_0 || QT == QT_Q6_K8) ? 8 : QT == QT_Q6_K ? 6 : QT == QT_Q5_K ? 5 : 4;  // VGPRs per piece
   constexpr bool DB = R * NSB * (8 * PB + 5) <= 80;               // room for a prefetch tile
   constexpr int ROWS_W = 4 * R, ROWS_B = GEMV_NW * ROWS_W;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -398,7 +398,7 @@ __global__ __launch_bounds__(GEMV_NT) void qgemv_flight_dual_kernel(GemvParams P
 // register tiles a block keeps in flight: ~150 VGPRs of weight tiles per lane
 template <int QT, int NSB, int R>
 constexpr int flight_jmax() {
-  constexpr int PB = QT == QT_Q8_0 ? 8 : QT == QT_Q6_K ? 6 : QT == QT_Q5_K ? 5 : 4;
+  constexpr int PB = (QT == QT_Q8_0 || QT == QT_Q6_K8) ? 8 : QT == QT_Q6_K ? 6 : QT == QT_Q5_K ? 5 : 4;
   constexpr int regs = R * NSB * (8 * PB + 5);
   return regs * 3 <= 150 ? 3 : regs * 2 <= 150 ? 2 : 1;
 }
@@ -486,7 +486,7 @@ static int flight_ks(int need, int tiles, int bz) {
 // (KS = 4 NSB = 1, KS = 2 NSB = 2) were the only ones spilling to scratch.
 template <int QT, int NSB, int KS, int NRM>
 constexpr bool flight_ks_fits() {
-  constexpr int PB = QT == QT_Q8_0 ? 8 : QT == QT_Q6_K ? 6 : QT == QT_Q5_K ? 5 : 4;
+  constexpr int PB = (QT == QT_Q8_0 || QT == QT_Q6_K8) ? 8 : QT == QT_Q6_K ? 6 : QT == QT_Q5_K ? 5 : 4;
   return NSB * (8 * PB + 5) + NSB * 16 * (1 + (NRM != 0) + (NRM == 2)) + 24 <= 512 / KS;
 }
 
@@ -568,17 +568,19 @@ static void launch_q(const GemvParams& P, hipStream_t s) {
         default: launch_flight<QT, 4, 1>(P, s); return;
       }
     }
-    if (g_tune.rows == 2) launch_nsb<QT, 2, 1>(P, s);
+    if (g_tune.rows == 2 && QT != QT_Q6_K8) launch_nsb<QT, (QT == QT_Q6_K8 ? 1 : 2), 1>(P, s);
     else launch_nsb<QT, 1, 1>(P, s);
     return;
   }
-  // continuous-batching rows: all-in-flight small-batch kernel (gemv_batch.hip)
-  if (gemv_batch(P, s)) return;
-  // batch tiles: the weights are unpacked once per piece and dotted against BT activation rows;
-  // BT bounded by the LDS the staged activations take
-  if (lds_bytes(P.w.K, 4) <= 96 * 1024) launch_nsb<QT, 1, 4>(P, s);
-  else if (lds_bytes(P.w.K, 2) <= 120 * 1024) launch_nsb<QT, 1, 2>(P, s);
-  else launch_nsb<QT, 1, 1>(P, s);
+  if constexpr (QT != QT_Q6_K8) {  // widened codes serve batch-1 only (eff_qtype)
+    // continuous-batching rows: all-in-flight small-batch kernel (gemv_batch.hip)
+    if (gemv_batch(P, s)) return;
+    // batch tiles: the weights are unpacked once per piece and dotted against BT activation rows;
+    // BT bounded by the LDS the staged activations take
+    if (lds_bytes(P.w.K, 4) <= 96 * 1024) launch_nsb<QT, 1, 4>(P, s);
+    else if (lds_bytes(P.w.K, 2) <= 120 * 1024) launch_nsb<QT, 1, 2>(P, s);
+    else launch_nsb<QT, 1, 1>(P, s);
+  }
 }
 
 template <int QA, int QB, int NSB>
@@ -594,12 +596,18 @@ static void launch_dual_q(const GemvParams& A, const GemvParams& Bp, int need, h
   else launch_dual_n<QA, QB, 2>(A, Bp, s);
 }
 
+// batch-1 GEMVs of a Q6_K matrix with widened codes read them (QT_Q6_K8, qmat.h)
+static int eff_qtype(const GemvParams& P) {
+  return P.w.qtype == QT_Q6_K && P.w.s4 && P.B == 1 && !P.expert_ids ? (int)QT_Q6_K8 : P.w.qtype;
+}
+
 template <int QA>
 static bool launch_dual_a(const GemvParams& A, const GemvParams& Bp, int need, hipStream_t s) {
-  switch (Bp.w.qtype) {
+  switch (eff_qtype(Bp)) {
     case QT_Q4_K: if (QA != QT_Q4_K) { launch_dual_q<QA, QT_Q4_K>(A, Bp, need, s); return true; } break;
     case QT_Q6_K: if (QA != QT_Q6_K) { launch_dual_q<QA, QT_Q6_K>(A, Bp, need, s); return true; } break;
     case QT_Q5_K: if (QA != QT_Q5_K) { launch_dual_q<QA, QT_Q5_K>(A, Bp, need, s); return true; } break;
+    case QT_Q6_K8: if (QA != QT_Q6_K8) { launch_dual_q<QA, QT_Q6_K8>(A, Bp, need, s); return true; } break;
     case QT_Q4_0: if (QA != QT_Q4_0) { launch_dual_q<QA, QT_Q4_0>(A, Bp, need, s); return true; } break;
     case QT_Q8_0: if (QA != QT_Q8_0) { launch_dual_q<QA, QT_Q8_0>(A, Bp, need, s); return true; } break;
     default: break;
@@ -616,10 +624,11 @@ void gemv2(const GemvParams& A0, const GemvParams& B0, hipStream_t s) {
                   A.x == Bp.x && g_tune.debug == 0;
   if (ok) {
     bool done = false;
-    switch (A.w.qtype) {
+    switch (eff_qtype(A)) {
       case QT_Q4_K: done = launch_dual_a<QT_Q4_K>(A, Bp, need, s); break;
       case QT_Q6_K: done = launch_dual_a<QT_Q6_K>(A, Bp, need, s); break;
       case QT_Q5_K: done = launch_dual_a<QT_Q5_K>(A, Bp, need, s); break;
+      case QT_Q6_K8: done = launch_dual_a<QT_Q6_K8>(A, Bp, need, s); break;
       case QT_Q4_0: done = launch_dual_a<QT_Q4_0>(A, Bp, need, s); break;
       case QT_Q8_0: done = launch_dual_a<QT_Q8_0>(A, Bp, need, s); break;
       default: break;
@@ -645,7 +654,8 @@ void gemv(const GemvParams& P0, hipStream_t s) {
     gemm(P, s);
     return;
   }
-  switch (P.w.qtype) {
+  switch (eff_qtype(P)) {
+    case QT_Q6_K8: launch_q<QT_Q6_K8>(P, s); break;
     case QT_Q4_K: launch_q<QT_Q4_K>(P, s); break;
     case QT_Q6_K: launch_q<QT_Q6_K>(P, s); break;
     case QT_Q5_K: launch_q<QT_Q5_K>(P, s); break;

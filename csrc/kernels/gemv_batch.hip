@@ -205,7 +205,7 @@ static void launch_batch_j(const GemvParams& P, int gx, int by, int mode, size_t
 
 template <int QT, int NSB, int BT>
 static void launch_batch_n(const GemvParams& P, size_t lds, hipStream_t s) {
-  constexpr int PB = QT == QT_Q8_0 ? 8 : QT == QT_Q6_K ? 6 : QT == QT_Q5_K ? 5 : 4;
+  constexpr int PB = (QT == QT_Q8_0 || QT == QT_Q6_K8) ? 8 : QT == QT_Q6_K ? 6 : QT == QT_Q5_K ? 5 : 4;
   constexpr int regs = NSB * (8 * PB + 5);                       // one weight tile per lane
   constexpr int XR = BT * NSB <= 4 ? (BT + 1) * NSB * 16 : 0;     // register prologue
   constexpr int XF = 12 * BT;                                     // activation fragments per piece

@@ -42,13 +42,14 @@ __device__ __forceinline__ float f16hi(unsigned v) { return h2f(v >> 16); }
 // register tile: R rows x NSB super-blocks x 8 pieces of one lane
 template <int QT, int NSB, int R>
 struct WTile {
-  static constexpr bool Q8 = QT == QT_Q8_0, Q6 = QT == QT_Q6_K, Q5 = QT == QT_Q5_K;
+  static constexpr bool Q8 = QT == QT_Q8_0 || QT == QT_Q6_K8, Q6 = QT == QT_Q6_K, Q5 = QT == QT_Q5_K;
+  static constexpr bool Q6D = QT == QT_Q6_K || QT == QT_Q6_K8;  // fp16 super-block scale
   u32x4 a[R][NSB][8];                                  // qs / ql / Q8_0 first 16 B
   u32x4 b[Q8 ? R : 1][Q8 ? NSB : 1][8];                // Q8_0 second 16 B
   u32x2 h[Q6 ? R : 1][Q6 ? NSB : 1][8];                // Q6_K high bits (H0 | H1)
   unsigned q5h[Q5 ? R : 1][Q5 ? NSB : 1][8];           // Q5_K 5th bits (one dword per piece)
   u32x4 m[R][NSB];                                     // super-block scales
-  unsigned d[Q6 ? R : 1][Q6 ? NSB : 1];                // Q6_K super-block scale (fp16)
+  unsigned d[Q6D ? R : 1][Q6D ? NSB : 1];              // Q6_K super-block scale (fp16)
 };
 
 // the machine scheduler otherwise permutes independent loads; vmcnt retires in issue order, so a
@@ -71,7 +72,19 @@ __device__ __forceinline__ void load_wtile(const QMat& w, long long row_base, in
       // issue order = consumption order: vmcnt retires loads in order, so the super-block scales go
       // first and each piece's operands together; otherwise the first dot product waits for the
       // wave's last load and no compute overlaps the stream
-      if constexpr (QT == QT_Q8_0) {
+      if constexpr (QT == QT_Q6_K8) {
+        const uint8_t* q = w.s4 + row * SB * 256 + 32 * sb;
+        T.m[r][i] = *(const u32x4*)(w.s2 + row * SB * 16 + 16 * sb);
+        OMX_LOAD_ORDER();
+        T.d[r][i] = *(const uint16_t*)(w.s3 + row * SB * 2 + 2 * sb);
+        OMX_LOAD_ORDER();
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          T.a[r][i][t] = __builtin_nontemporal_load((const u32x4*)(q + 32LL * t * SB));
+          T.b[r][i][t] = __builtin_nontemporal_load((const u32x4*)(q + 32LL * t * SB + 16));
+          OMX_LOAD_ORDER();
+        }
+      } else if constexpr (QT == QT_Q8_0) {
         const uint8_t* q = w.s0 + row * SB * 256 + 32 * sb;
         T.m[r][i] = *(const u32x4*)(w.s1 + row * SB * 16 + 16 * sb);
         OMX_LOAD_ORDER();
@@ -246,6 +259,28 @@ __device__ __forceinline__ void compute_wtile(const WTile<QT, NSB, R>& T, int SB
           }
           OMX_PIECE_ORDER();
         }
+      }
+    } else if constexpr (QT == QT_Q6_K8) {
+      // widened Q6_K: w = d*sc*c with c = q - 32 already signed int8 (lo | hi 16-weight halves)
+      float dq[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) dq[r] = h2f((uint16_t)T.d[r][i]);
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const int n = t >> 2, sub = t & 3, il_ = 8 * n + sub, ih_ = il_ + 4;
+        XFr<BT> x;
+        load_x<BT>(xq, xf, XS, xs0 + il_, xs0 + ih_, x);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const u32x4 m = T.m[r][i];
+          const float fl = dq[r] * sbyte(m[il_ >> 2], il_ & 3), fh = dq[r] * sbyte(m[ih_ >> 2], ih_ & 3);
+#pragma unroll
+          for (int b = 0; b < BT; ++b) {
+            const float il = (float)dot16(T.a[r][i][t], x.lo[b]), ih = (float)dot16(T.b[r][i][t], x.hi[b]);
+            acc[r][b] += fl * (x.fl[b].x * il) + fh * (x.fh[b].x * ih);
+          }
+        }
+        OMX_PIECE_ORDER();
       }
     } else if constexpr (QT == QT_Q6_K) {
       // w = d*sc*(q - 32); q = ql nibble | (2 high bits << 4)

@@ -171,6 +171,7 @@ void ar_allgather(const ARParams& P, int slab, float* out, int rows, int n_local
 
 // small elementwise helpers
 void add_inplace(float* y, const float* x, long long n, hipStream_t s);
+void widen_q6k(const QMat& w, void* out, hipStream_t s);  // out: N * SB * 256 bytes
 void decode_feedback(int* step, int ld, const int* sampled, int B, int advance, const int* block_table,
                      int max_blocks, int bs, int* host_ring, int ring, hipStream_t s);
 void rmsnorm(const float* x, const float* w, float eps, int rows, int n, float* out, hipStream_t s);

@@ -11,7 +11,12 @@
 #pragma once
 #include <stdint.h>
 
-enum QType : int { QT_Q4_0 = 2, QT_Q8_0 = 8, QT_Q4_K = 12, QT_Q5_K = 13, QT_Q6_K = 14 };
+// QT_Q6_K8 is internal (no ggml type): a Q6_K matrix whose codes were widened at load to signed int8
+// (q - 32), 32 B per piece (lo 16 weights | hi 16 weights) in s4, piece-major as Q8_0; scales stay in
+// s2 (int8 per 16) / s3 (fp16 per 256). Opt-in (OMX_Q6K_WIDEN=1) for the batch-1 GEMV: it trades the
+// 6-bit unpack chain (~5 us per down-projection launch, profiles/r2_gemv) for +30 % bytes, and in the
+// engine that measured slower (down 13.2 -> 14.6 us). Prefill GEMM and batched GEMV read 6-bit streams.
+enum QType : int { QT_Q4_0 = 2, QT_Q8_0 = 8, QT_Q4_K = 12, QT_Q5_K = 13, QT_Q6_K = 14, QT_Q6_K8 = 114 };
 
 struct QMat {
   const uint8_t* s0;
@@ -19,4 +24,5 @@ struct QMat {
   const uint8_t* s2;
   const uint8_t* s3;
   int N, K, qtype;
+  const uint8_t* s4;  // optional widened Q6_K codes (QT_Q6_K8), null otherwise
 };

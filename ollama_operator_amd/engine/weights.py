@@ -39,11 +39,14 @@ class DevQMat:
     N: int
     K: int
     streams: list[torch.Tensor] = field(default_factory=list)
+    # Q6_K only, GPU: codes widened to signed int8 at load for the batch-1 GEMV (qmat.h QT_Q6_K8)
+    wide: torch.Tensor | None = None
 
     @property
     def tup(self) -> tuple:
         p = [s.data_ptr() for s in self.streams] + [0] * (4 - len(self.streams))
-        return (p[0], p[1], p[2], p[3], self.N, self.K, int(self.qtype))
+        t = (p[0], p[1], p[2], p[3], self.N, self.K, int(self.qtype))
+        return t + (self.wide.data_ptr(),) if self.wide is not None else t
 
     @property
     def nbytes(self) -> int:
@@ -113,7 +116,7 @@ class WeightSource:
 
 
 def build_qmat(src: WeightSource, parts: list[tuple[str, np.ndarray, np.ndarray]], N: int, K_src: int,
-               kb: tuple[int, int] | None, device, expert_rows: int = 0) -> DevQMat:
+               kb: tuple[int, int] | None, device, expert_rows: int = 0, widen: bool = False) -> DevQMat:
     """parts: (tensor, source rows, destination rows). All parts must share one device qtype."""
     qts = {src.qtype_of(p[0]) for p in parts}
     if len(qts) != 1:
@@ -127,7 +130,16 @@ def build_qmat(src: WeightSource, parts: list[tuple[str, np.ndarray, np.ndarray]
     for name, rows, drows in parts:
         src.repack_into(name, K_src, rows, drows, kb0, kb1, host)
     streams = [torch.from_numpy(h).to(device) for h in host]
-    return DevQMat(qt, expert_rows or N, K, streams)
+    m = DevQMat(qt, expert_rows or N, K, streams)
+    # opt-in (OMX_Q6K_WIDEN=1): Q6_K projections (down, V, O) get int8-widened codes for the batch-1
+    # GEMV. Measured in the engine it loses: down 13.2 -> 14.6 us, the +30 % bytes cost more than the
+    # 6-bit unpack it saves (profiles/r2_gemv/engine_widened_step.txt); kept as a tested knob
+    if (widen and qt == int(GGMLType.Q6_K) and not expert_rows and str(device).startswith("cuda")
+            and os.environ.get("OMX_Q6K_WIDEN", "0") == "1"):
+        from ..ops import native, stream_handle
+        m.wide = torch.empty(N * ((K + 255) // 256) * 256, dtype=torch.uint8, device=device)
+        native().widen_q6k(m.tup, m.wide.data_ptr(), stream_handle())
+    return m
 
 
 def neox_pair_perm(D: int, n_rot: int) -> np.ndarray:
@@ -193,12 +205,12 @@ class DeviceWeights:
                 L["attn_norm"] = t(src.f32(b + "attn_norm.weight"))
                 L["attn_norm_b"] = t(src.f32(b + "attn_norm.bias"))
                 L["wo"] = build_qmat(src, [(b + "attn_output.weight", ar(E), ar(E))], E, E,
-                                     kblocks(E, b + "attn_output.weight"), dev)
+                                     kblocks(E, b + "attn_output.weight"), dev, widen=True)
                 L["bo"] = t(src.f32(b + "attn_output.bias")) if r == 0 else None
                 L["wgu"] = build_qmat(src, [(b + "ffn_up.weight", ar(Fl, r * Fl), ar(Fl))], Fl, E, None, dev)
                 L["bup"] = t(src.f32(b + "ffn_up.bias")[r * Fl:(r + 1) * Fl])
                 L["wdown"] = build_qmat(src, [(b + "ffn_down.weight", ar(E), ar(E))], E, F,
-                                        kblocks(F, b + "ffn_down.weight"), dev)
+                                        kblocks(F, b + "ffn_down.weight"), dev, widen=True)
                 L["bdown"] = t(src.f32(b + "ffn_down.bias")) if r == 0 else None
             else:
                 rq = head_rows(r * Hl, Hl, cfg.rope_mode == ROPE_NEOX)
@@ -210,11 +222,11 @@ class DeviceWeights:
                                           Eq + 2 * Ekv, E, None, dev)
                 else:
                     L["wqk"] = build_qmat(src, [(nq, rq, ar(Eq)), (nk, rk, ar(Ekv, Eq))], Eq + Ekv, E, None, dev)
-                    L["wv"] = build_qmat(src, [(nv, rv, ar(Ekv))], Ekv, E, None, dev)
+                    L["wv"] = build_qmat(src, [(nv, rv, ar(Ekv))], Ekv, E, None, dev, widen=True)
                 L["attn_norm"] = t(src.f32(b + "attn_norm.weight"))
                 L["ffn_norm"] = t(src.f32(b + "ffn_norm.weight"))
                 L["wo"] = build_qmat(src, [(b + "attn_output.weight", ar(E), ar(E))], E, E,
-                                     kblocks(E, b + "attn_output.weight"), dev)
+                                     kblocks(E, b + "attn_output.weight"), dev, widen=True)
                 if cfg.n_expert:
                     X = cfg.n_expert
                     L["router"] = build_qmat(src, [(b + "ffn_gate_inp.weight", ar(X), ar(X))], X, E, None, dev)
@@ -231,7 +243,7 @@ class DeviceWeights:
                     loc = ar(Fl, r * Fl)
                     L["wgu"] = build_qmat(src, [(ng, loc, 2 * ar(Fl)), (nu, loc, 2 * ar(Fl) + 1)], 2 * Fl, E, None, dev)
                     L["wdown"] = build_qmat(src, [(b + "ffn_down.weight", ar(E), ar(E))], E, F,
-                                            kblocks(F, b + "ffn_down.weight"), dev)
+                                            kblocks(F, b + "ffn_down.weight"), dev, widen=True)
             self.layers.append(L)
         self.out_norm = t(src.f32("output_norm.weight"))
         self.out_norm_b = t(src.f32("output_norm.bias")) if src.has("output_norm.bias") else None

@@ -364,3 +364,25 @@ def test_gemv_batch_rows(qt, B, K, norm):
         xn = x
     ref = xn @ m.w.T
     assert rel(y - y0, ref) < 1e-2
+
+
+@pytest.mark.parametrize("K", [4096, 11008])
+@pytest.mark.parametrize("B", [1, 3])
+def test_gemv_q6k_widened(K, B):
+    """Q6_K with load-time int8-widened codes (qmat.h QT_Q6_K8): the batch-1 GEMV reads the widened
+    stream, batched rows the 6-bit streams; both against fp32 torch (store and residual-add)."""
+    N = 512
+    m = QM(GGMLType.Q6_K, N, K, seed=K + 7)
+    wide = torch.empty(N * (K // 256) * 256, dtype=torch.uint8, device="cuda")
+    C().widen_q6k(m.tup, wide.data_ptr(), S())
+    m.tup = m.tup + (wide.data_ptr(),)
+    x = torch.randn(B, K, device="cuda")
+    y = torch.zeros(B, N, device="cuda")
+    gemv(m, x, y=y)
+    torch.cuda.synchronize()
+    assert rel(y, x @ m.w.T) < 1e-2
+    res = torch.randn(B, N, device="cuda")
+    y2 = res.clone()
+    gemv(m, x, epi=1, y=y2)
+    torch.cuda.synchronize()
+    assert rel(y2, res + x @ m.w.T) < 1e-2
