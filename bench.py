@@ -12,6 +12,14 @@ Weights: random-init GGUF with the real Q4_K_M tensor-type mix (no network for c
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--prompt P]
     torchrun --nproc-per-node N bench.py --gpus N ...
+    python bench.py --model llama2-70b --ftype Q4_0 --tp 8      # tensor parallel (BASELINE config 4)
+
+`--gpus N` without torchrun: this process launches the N rank processes itself (one per GPU, before
+it touches any GPU) and exits with their status; it refuses (non-zero) when fewer than N GPUs are
+visible instead of silently measuring one. `--tp T` serves ONE sequence on T GPUs through the real
+tensor-parallel serving stack (parallel/tp.py: leader + T-1 worker processes, one-shot IPC
+all-reduce in the decode graph) and reports its tokens/s with parallelism `tpT`. `--device cpu`
+runs the same orchestration on the CPU (gloo, torch twin executor) -- the multi-rank CPU tests use it.
 """
 from __future__ import annotations
 
@@ -192,9 +200,142 @@ def bench_batched(runner, a, rank, world, sync):
             "ms_per_step": round(dt / a.steps * 1e3, 4)}
 
 
+def free_port() -> int:
+    import socket
+    with socket.socket() as s_:
+        s_.bind(("127.0.0.1", 0))
+        return s_.getsockname()[1]
+
+
+def visible_devices(device: str) -> int:
+    if device == "cpu":
+        return 1 << 30
+    import torch
+    return torch.cuda.device_count()  # counts devices without initialising the GPU on this image
+
+
+def launch_ranks(a) -> int:
+    """`--gpus N` outside torchrun: spawn the N data-parallel ranks (one process per GPU, env
+    RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* as torchrun sets them) and return the worst exit code.
+    Runs before this process touches any GPU; the model file is written once, here."""
+    import subprocess
+    n = a.gpus
+    have = visible_devices(a.device)
+    if have < n:
+        print(f"bench.py: --gpus {n} requested but only {have} GPU(s) are visible; refusing to report a "
+              f"{have}-GPU number as {n}", file=sys.stderr, flush=True)
+        return 2
+    ensure_model(model_path(a), a.model, a.ftype)
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env, cwd=ROOT))
+    rc = 0
+    try:
+        for p in procs:
+            c = p.wait()
+            if c != 0 and rc == 0:
+                rc = c
+                for q in procs:  # one rank failed: the others would hang in the next collective
+                    if q.poll() is None:
+                        q.kill()
+    finally:
+        for q in procs:
+            if q.poll() is None:
+                q.kill()
+    return rc
+
+
+def model_path(a) -> str:
+    return os.path.join(a.dir, f"{a.model}-{a.ftype.lower()}.gguf")
+
+
+def bench_tp(a) -> None:
+    """One sequence on T GPUs through the tensor-parallel serving stack: the leader (this process)
+    spawns T-1 workers before touching the GPU (parallel/tp.py start_leader), loads the model sharded
+    (TPRunnerProxy), and streams `generate` exactly as the server does. On a box with fewer GPUs than
+    T, ranks share GPUs (gloo compute group; decode collectives stay on the one-shot IPC all-reduce)
+    -- a correctness rehearsal, reported with `shared_gpus` in config."""
+    T = a.tp
+    have = visible_devices(a.device)
+    shared = have < T
+    if shared and not a.allow_shared:
+        print(f"bench.py: --tp {T} needs {T} GPUs, {have} visible (pass --allow-shared to rehearse on fewer)",
+              file=sys.stderr, flush=True)
+        sys.exit(2)
+    path = ensure_model(model_path(a), a.model, a.ftype)
+    if shared or a.device == "cpu":
+        os.environ["OMX_TP_BACKEND"] = "gloo"
+    from ollama_operator_amd.parallel import tp
+    world = tp.start_leader(T)
+    import torch
+    from ollama_operator_amd.engine.sampling import SamplingOptions
+    gpu = world.device.startswith("cuda")
+
+    def sync():
+        if gpu:
+            torch.cuda.synchronize()
+
+    try:
+        ctx = a.prompt + a.warmup + a.steps + 64
+        t_load = time.perf_counter()
+        r = tp.load_tp_runner(world, path, max_batch=a.chunk, max_seqs=2, ctx=ctx)
+        r.warmup()
+        sync()
+        load_s = time.perf_counter() - t_load
+        g = torch.Generator().manual_seed(1234)
+        prompt = [1] + torch.randint(3, r.cfg.n_vocab, (a.prompt - 1,), generator=g).tolist()
+        sid = r.new_sequence()
+        gen = r.generate(sid, prompt, SamplingOptions(seed=42), max_tokens=a.warmup + a.steps + 2)
+        t_p = time.perf_counter()
+        next(gen)
+        ttft = time.perf_counter() - t_p
+        for _ in range(a.warmup):
+            next(gen)
+        sync()
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            next(gen)
+        sync()
+        dt = time.perf_counter() - t0
+        gen.close()
+        r.free_sequence(sid)
+        weights_gb = r.w.nbytes / 1e9
+        r.close()
+    finally:
+        tp.shutdown_leader(world)
+    label = MODEL_LABELS.get(a.model, a.model) + " " + a.ftype
+    print(json.dumps({
+        "metric": f"output tokens/sec {label}",
+        "value": round(a.steps / dt, 2),
+        "unit": "tokens/s",
+        "n_gpus": T,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(dt / a.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": f"{a.ftype} weights, int8-dot activations, fp32 accumulate, fp16 KV",
+        "data": f"synthetic prompt, random-init GGUF weights (real {a.ftype} tensor-type mix)",
+        "config": {"model": label, "global_batch": 1, "seq_len": a.prompt + a.warmup + a.steps,
+                   "parallelism": f"tp{T}", "prompt_tokens": a.prompt, "shared_gpus": shared,
+                   "device": a.device, "sampling": "temperature 0.8, top_k 40, top_p 0.9, repeat_penalty 1.1"},
+        "extra": {"ttft_ms": round(ttft * 1e3, 2), "load_s": round(load_s, 2),
+                  "weights_gb_rank0": round(weights_gb, 3)},
+    }), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--tp", type=int, default=1, help="tensor-parallel degree: one sequence sharded over T GPUs")
+    ap.add_argument("--allow-shared", action="store_true",
+                    help="--tp T on fewer than T GPUs: ranks share GPUs (correctness rehearsal)")
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
+                    help="cpu: same orchestration on the CPU (gloo, torch twin executor) for tests")
     ap.add_argument("--steps", type=int, default=256)
     ap.add_argument("--warmup", type=int, default=16)
     ap.add_argument("--prompt", type=int, default=128)
@@ -213,22 +354,35 @@ def main():
     ap.add_argument("--server-parallel", type=int, default=4,
                     help="OLLAMA_NUM_PARALLEL of the spawned server (concurrent clients measured)")
     a = ap.parse_args()
+    os.makedirs(a.dir, exist_ok=True)
+    if a.tp > 1:
+        bench_tp(a)
+        return
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        sys.exit(launch_ranks(a))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    path = os.path.join(a.dir, f"{a.model}-{a.ftype.lower()}.gguf")
+    if world != a.gpus:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {a.gpus}", file=sys.stderr, flush=True)
+        sys.exit(2)
+    gpu = a.device == "cuda"
+    path = model_path(a)
     server = None
-    if a.via_server and world == 1:
-        os.makedirs(a.dir, exist_ok=True)
+    if a.via_server and world == 1 and gpu:
         server = start_server(a, path)  # before this process touches the GPU
 
     import torch
     import torch.distributed as dist
 
-    torch.cuda.set_device(local)
+    if gpu:
+        torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        if gpu:
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        else:
+            dist.init_process_group("gloo")
 
     from ollama_operator_amd.engine.runner import Runner
     from ollama_operator_amd.engine.sampling import SamplingOptions
@@ -242,9 +396,11 @@ def main():
 
     ctx = max(a.prompt + a.warmup + a.steps + 64, a.ttft_long + 8 if a.ttft_long else 0)
     t_load = time.perf_counter()
-    runner = Runner(path, device=f"cuda:{local}", max_batch=a.chunk, max_seqs=max(2, a.batch_extra), ctx=ctx)
+    runner = Runner(path, device=f"cuda:{local}" if gpu else "cpu", max_batch=a.chunk,
+                    max_seqs=max(2, a.batch_extra), ctx=ctx)
     runner.warmup()  # load-time decode-graph capture, as the server does at model load
-    torch.cuda.synchronize()
+    if gpu:
+        torch.cuda.synchronize()
     load_s = time.perf_counter() - t_load
 
     g = torch.Generator().manual_seed(1234 + rank)
@@ -259,10 +415,12 @@ def main():
         next(gen)
 
     def sync():
-        torch.cuda.synchronize()
+        if gpu:
+            torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
-        torch.cuda.synchronize()
+        if gpu:
+            torch.cuda.synchronize()
 
     sync()
     t0 = time.perf_counter()
@@ -270,7 +428,7 @@ def main():
         next(gen)
     sync()
     dt = time.perf_counter() - t0
-    t = torch.tensor([dt], device="cuda")
+    t = torch.tensor([dt], device="cuda" if gpu else "cpu")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt = float(t)
@@ -284,7 +442,8 @@ def main():
         best = None
         for _ in range(3):  # prefill of a fresh sequence each time (no prefix reuse)
             sid = runner.new_sequence()
-            torch.cuda.synchronize()
+            if gpu:
+                torch.cuda.synchronize()
             t_p = time.perf_counter()
             gl = runner.generate(sid, p, opts, max_tokens=1)
             next(gl)
@@ -294,7 +453,7 @@ def main():
             best = dt_l if best is None else min(best, dt_l)
         ttft_long = round(best * 1e3, 2)
     batched = None
-    if a.batch_extra > 1:
+    if a.batch_extra > 1 and gpu:
         batched = bench_batched(runner, a, rank, world, sync)
     served = None
     if server is not None:
@@ -328,6 +487,7 @@ def main():
             "data": f"synthetic prompt, random-init GGUF weights (real {a.ftype} tensor-type mix)",
             "config": {"model": label, "global_batch": world, "seq_len": a.prompt + a.warmup + a.steps,
                        "parallelism": f"dp{world}", "prompt_tokens": a.prompt, "decode_batch_per_gpu": 1,
+                       "device": a.device,
                        "sampling": "temperature 0.8, top_k 40, top_p 0.9, repeat_penalty 1.1 (on device)"},
             "extra": {"ttft_ms": round(ttft * 1e3, 2), f"ttft_{a.ttft_long}_ms": ttft_long, "prefill_chunk": a.chunk,
                       "load_s": round(load_s, 2),

@@ -64,6 +64,7 @@ static ARParams ar_params(py::dict d) {
   }
   P.epoch = Pp<unsigned>(d["epoch"].cast<uintptr_t>());
   P.err = Pp<int>(d["err"].cast<uintptr_t>());
+  P.err_host = Pp<int>(d.contains("err_host") ? d["err_host"].cast<uintptr_t>() : 0);
   P.slab_floats = d["slab_floats"].cast<long long>();
   P.timeout_ticks = d["timeout_ticks"].cast<unsigned long long>();
   if (!P.epoch || !P.err || P.slab_floats <= 0 || P.slab_floats % 4) throw std::runtime_error("ar: bad workspace");

@@ -24,7 +24,10 @@
 //    consecutive slabs distinct, also across steps (2 -> 0).
 //  * Spins are bounded (timeout_ticks of the 100 MHz wall clock): a dead peer turns into an error
 //    flag (err[0] = 1 + rank of the first missing peer) and a finished kernel, never a hung GPU.
-//    The host (parallel/tp.py watchdog) polls err and kills the pod.
+//    Once err is set every later collective on this rank skips its slab reads and leaves y untouched
+//    (the group is out of step: reading would mix slabs of different calls). The host notices on the
+//    next poll: the TP watchdog (parallel/tp.py `_watchdog`, leader) and the per-generate check
+//    (engine/runner.py, every rank) raise TPCollectiveError / exit non-zero, so the pod restarts.
 // Reference parity: the reference has replica parallelism only (pkg/model/model.go:149-186); this is
 // the MI355X-native TP collective the north star adds.
 #include "common.h"
@@ -34,10 +37,11 @@ namespace omx {
 
 constexpr int AR_NT = 256;
 
+// returns false (block-uniform) when this rank's collectives have failed: a barrier timed out now
+// or in an earlier call -- the caller must not read peers' slabs then
 __device__ __forceinline__ bool ar_barrier(const ARParams& P) {
   const int t = threadIdx.x, b = blockIdx.x;
   const unsigned e = P.epoch[b] + 1u;
-  bool ok = true;
   if (t < P.world) {
     // make this rank's slab (written by earlier kernels in stream order) visible system-wide
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
@@ -48,8 +52,8 @@ __device__ __forceinline__ bool ar_barrier(const ARParams& P) {
     const bool failed = __hip_atomic_load(P.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
     while (!failed && (int)(__hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - e) < 0) {
       if (wall_clock64() - t0 > P.timeout_ticks) {
-        ok = false;
         __hip_atomic_store(P.err, 1 + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (P.err_host) __hip_atomic_store(P.err_host, 1 + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         break;
       }
       __builtin_amdgcn_s_sleep(1);
@@ -58,12 +62,14 @@ __device__ __forceinline__ bool ar_barrier(const ARParams& P) {
   }
   __syncthreads();
   if (t == 0) P.epoch[b] = e;
-  return ok;
+  // every thread re-reads the error word after the barrier: a timeout by any thread of this block
+  // (or an earlier call) is visible here, so the whole block takes the same branch
+  return __hip_atomic_load(P.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0;
 }
 
 template <int W>
 __global__ __launch_bounds__(AR_NT) void ar_add_kernel(ARParams P, int slab, float* __restrict__ y, int n) {
-  ar_barrier(P);
+  if (!ar_barrier(P)) return;
   const long long off = (long long)slab * P.slab_floats;
   const int n4 = n >> 2;
   for (int i = blockIdx.x * AR_NT + threadIdx.x; i < n4; i += gridDim.x * AR_NT) {
@@ -81,7 +87,7 @@ __global__ __launch_bounds__(AR_NT) void ar_add_kernel(ARParams P, int slab, flo
 // out[row][r * n_local + j] = slab_r[row][j]  (vocab-sharded logits -> full rows)
 __global__ __launch_bounds__(AR_NT) void ar_gather_kernel(ARParams P, int slab, float* __restrict__ out, int rows,
                                                           int n_local, int ld_out) {
-  ar_barrier(P);
+  if (!ar_barrier(P)) return;
   const long long off = (long long)slab * P.slab_floats;
   const long long per = (long long)rows * n_local;
   const long long total = per * P.world;

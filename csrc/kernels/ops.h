@@ -160,6 +160,7 @@ struct ARParams {
   unsigned* flags[AR_MAX_RANKS];  // rank r's flags [AR_MAX_BLOCKS][AR_MAX_RANKS] (uncached, peer-mapped)
   unsigned* epoch;                // this rank's per-block barrier counters [AR_MAX_BLOCKS] (zeroed once)
   int* err;                       // this rank's error word: 1 + peer that never arrived (0 = ok)
+  int* err_host;                  // host-mapped mirror of err (null: none); the host polls it without a HIP call
   int rank, world;
   long long slab_floats;
   unsigned long long timeout_ticks;  // 100 MHz wall-clock ticks a barrier may wait

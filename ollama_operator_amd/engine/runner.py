@@ -108,6 +108,7 @@ class Runner:
             if os.environ.get("OMX_GEMV_XFIRST") in ("0", "1"):  # decode GEMV x-first knob (gemv.hip)
                 native().set_gemv_tuning(xfirst=int(os.environ["OMX_GEMV_XFIRST"]))
         self.tp_rank, self.tp_size, self.tp_group = tp_rank, tp_size, tp_group
+        self._closed = False
         # TP serving (parallel/tp.py): rank 0 signals each decode step, followers mirror it
         self.tp_ctrl = tp_ctrl
         self.w = weights or DeviceWeights(model_path, self.device, tp_rank, tp_size)
@@ -209,10 +210,16 @@ class Runner:
         self.load_s = time.perf_counter() - t0
 
     def close(self) -> None:
-        """Release the TP collective workspace (all ranks call this together)."""
+        """Release the TP collective workspace (all ranks call this together). The executor forgets
+        the slabs and the captured graphs (which point at them) go first, so no later step can write
+        into freed memory; a closed runner refuses further steps."""
         if self.ar is not None:
+            if isinstance(self.exe, NativeExec):
+                self.exe.exe.clear_ar()
+            self.graphs.clear()
             self.ar.close()
             self.ar = None
+        self._closed = True
 
     # ------------------------------------------------------------------ sizing helpers
     def n_splits(self, B: int) -> int:
@@ -252,6 +259,8 @@ class Runner:
 
     def forward(self, B: int, n_logits: int, use_idx: bool = False, prefill: bool = False):
         """prefill=True: the B rows are one sequence's contiguous positions (MFMA flash attention)."""
+        if self._closed:
+            raise RuntimeError("runner is closed")
         if self.tp_size == 1:
             self.exe.run("forward", 0, B, n_logits, use_idx, prefill)
             return
@@ -452,6 +461,8 @@ class Runner:
         """One decode step for B = len(sids) sequences (continuous batching: engine/scheduler.py).
         Row b's input token is d_tokens[b] on device and sits at position poss[b]; the step samples
         row b with sampler row b and feeds the sampled tokens back into d_tokens[:B]."""
+        if self._closed:
+            raise RuntimeError("runner is closed")
         B = len(sids)
         arr = np.empty((5, B), np.int32)
         reserved = False

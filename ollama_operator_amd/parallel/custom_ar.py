@@ -11,13 +11,21 @@ world x n bytes per rank, which only wins while latency dominates (SURVEY.md §5
 """
 from __future__ import annotations
 
+import ctypes
 import os
 
+import numpy as np
 import torch.distributed as dist
 
 from ..ops import native
 
 DEFAULT_TIMEOUT_S = float(os.environ.get("OMX_AR_TIMEOUT_S", "20"))
+
+
+class TPCollectiveError(RuntimeError):
+    """A peer missed a one-shot all-reduce barrier: the TP group is out of step and every later
+    collective on this rank is skipped on device (allreduce.hip), so the process must end -- the
+    server treats this like a HIP fault (server/app.py `is_device_fault`) and exits non-zero."""
 
 
 class CustomAllReduce:
@@ -41,8 +49,13 @@ class CustomAllReduce:
             flags.append(pf)
         self.group = group
         self.rank, self.world, self.slab_floats = rank, world, slab_floats
-        self.params = dict(data=data, flags=flags, epoch=loc["epoch"], err=loc["err"], rank=rank, world=world,
-                           slab_floats=slab_floats,
+        # host-mapped mirror of the error word: the watchdog thread polls it with a plain memory read
+        # (a hipMemcpy from another thread would queue behind -- or disturb the capture of -- the
+        # decode graph)
+        self._err_h, err_d = C.host_alloc_mapped(64)
+        self._err_view = np.ctypeslib.as_array((ctypes.c_int32 * 1).from_address(self._err_h))
+        self.params = dict(data=data, flags=flags, epoch=loc["epoch"], err=loc["err"], err_host=err_d, rank=rank,
+                           world=world, slab_floats=slab_floats,
                            timeout_ticks=int(timeout_s * C.wall_clock_khz() * 1000))
         dist.barrier(group=group)  # every rank mapped every peer before any kernel signals
 
@@ -50,13 +63,16 @@ class CustomAllReduce:
         return self._local["data"] + 4 * slab * self.slab_floats
 
     def error(self) -> int:
-        """0, or 1 + the peer whose barrier flag never arrived (a dead / wedged rank)."""
-        return self.C.ar_error(self.params["err"])
+        """0, or 1 + the peer whose barrier flag never arrived (a dead / wedged rank). A plain read of
+        the host-mapped mirror: safe from any thread, never waits on the GPU."""
+        if self._local is None:
+            return 0
+        return int(self._err_view[0])
 
     def check(self) -> None:
         e = self.error()
         if e:
-            raise RuntimeError(f"tensor-parallel rank {self.rank}: peer {e - 1} missed an all-reduce barrier")
+            raise TPCollectiveError(f"tensor-parallel rank {self.rank}: peer {e - 1} missed an all-reduce barrier")
 
     def all_reduce_add(self, slab: int, y_ptr: int, n: int, stream: int) -> None:
         self.C.ar_allreduce_add(self.params, slab, y_ptr, n, stream)
@@ -76,3 +92,6 @@ class CustomAllReduce:
         for k in ("data", "flags", "epoch"):
             self.C.ar_free(self._local[k])
         self._opened, self._local = [], None
+        self._err_view = None
+        self.C.host_free_mapped(self._err_h)
+        self._err_h = 0

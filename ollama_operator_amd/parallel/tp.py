@@ -77,6 +77,9 @@ class TPWorld:
     ctrl: TPControl
     workers: list
     stopping: threading.Event = dataclasses.field(default_factory=threading.Event)
+    # leader's custom all-reduce error probe (CustomAllReduce.error, a host-mapped read): set while a
+    # TP model is loaded
+    ar_probe: object = None
 
 
 def _device_for(local_rank: int) -> str:
@@ -105,13 +108,18 @@ def start_leader(size: int) -> TPWorld:
     """Server process (rank 0): spawn workers first (GPU untouched so far), then join the groups."""
     addr, port = "127.0.0.1", _free_port()
     workers = []
+    pkg_root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     for r in range(1, size):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(size), MASTER_ADDR=addr,
-                   MASTER_PORT=str(port))
+                   MASTER_PORT=str(port),
+                   PYTHONPATH=pkg_root + os.pathsep + os.environ.get("PYTHONPATH", ""))
         workers.append(subprocess.Popen([sys.executable, "-m", "ollama_operator_amd.parallel.tp_worker"], env=env))
-    dev, compute, ctrl = _init_groups(0, size, addr, port)
-    world = TPWorld(0, size, dev, compute, TPControl(ctrl, leader=True), workers)
+    world = TPWorld(0, size, "", None, None, workers)
+    # watch the workers from the start: one that dies before the rendezvous would otherwise leave the
+    # leader blocked in init_process_group
     threading.Thread(target=_watchdog, args=(world,), name="tp-watchdog", daemon=True).start()
+    dev, compute, ctrl = _init_groups(0, size, addr, port)
+    world.device, world.compute_group, world.ctrl = dev, compute, TPControl(ctrl, leader=True)
     return world
 
 
@@ -120,18 +128,28 @@ WATCHDOG_PERIOD_S = 1.0
 
 def _watchdog(world: TPWorld, period: float = WATCHDOG_PERIOD_S, exit_fn=os._exit) -> None:
     """A TP group cannot lose a rank: a dead worker leaves the leader blocked in (or timing out of)
-    the next collective while /api/tags keeps answering. Any worker exit outside shutdown ends the
-    server with a non-zero code, so the pod restarts (liveness alone would not see it)."""
+    the next collective while /api/tags keeps answering. Any worker exit outside shutdown, and any
+    all-reduce barrier timeout on the leader (a wedged peer: the device skips every later collective,
+    allreduce.hip), ends the server with a non-zero code, so the pod restarts (SURVEY.md §5.3;
+    liveness alone would not see it)."""
+    def die(msg: str, rc: int) -> None:
+        print(f"tp watchdog: {msg}; terminating the TP group", file=sys.stderr, flush=True)
+        for q in world.workers:
+            if q.poll() is None:
+                q.kill()
+        exit_fn(rc)
+
     while not world.stopping.wait(period):
         for r, p in enumerate(world.workers, start=1):
             rc = p.poll()
             if rc is not None and not world.stopping.is_set():
-                print(f"tp watchdog: rank {r} exited with code {rc}; terminating the TP group", file=sys.stderr,
-                      flush=True)
-                for q in world.workers:
-                    if q.poll() is None:
-                        q.kill()
-                exit_fn(rc if rc else 1)
+                die(f"rank {r} exited with code {rc}", rc if rc else 1)
+                return
+        probe = world.ar_probe
+        if probe is not None and not world.stopping.is_set():
+            e = probe()
+            if e:
+                die(f"rank 0: peer {e - 1} missed a one-shot all-reduce barrier", 1)
                 return
 
 
@@ -187,6 +205,7 @@ class TPRunnerProxy:
         return self.r.generate(sid, prompt, o, max_tokens=max_tokens, stop=stop, times=times)
 
     def close(self) -> None:
+        self.world.ar_probe = None
         self._mirror("unload")
         self.r.close()
 
@@ -197,6 +216,8 @@ def load_tp_runner(world: TPWorld, path: str, max_batch: int, max_seqs: int, ctx
     world.ctrl.send_cmd({"op": "load", **cmd})
     r = Runner(path, device=world.device, max_batch=max_batch, max_seqs=max_seqs, ctx=ctx, tp_rank=0,
                tp_size=world.size, tp_group=world.compute_group, tp_ctrl=world.ctrl)
+    if r.ar is not None:
+        world.ar_probe = r.ar.error
     return TPRunnerProxy(world, r, cmd)
 
 

@@ -33,10 +33,11 @@ OLLAMA_COMPAT_VERSION = "0.5.4"
 
 
 def is_device_fault(exc: BaseException) -> bool:
-    """A HIP runtime error (sticky: the context is lost), as opposed to an engine-level failure."""
+    """A HIP runtime error (sticky: the context is lost) or a tensor-parallel group that fell out of
+    step (parallel/custom_ar.py TPCollectiveError), as opposed to an engine-level failure."""
     name = type(exc).__name__
     msg = str(exc)
-    return name == "AcceleratorError" or "HIP error" in msg or "hipError" in msg
+    return (name in ("AcceleratorError", "TPCollectiveError") or "HIP error" in msg or "hipError" in msg)
 
 
 def _err(msg: str, code: int = 400) -> JSONResponse:

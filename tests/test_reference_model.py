@@ -42,3 +42,23 @@ def test_reference_mixtral_incremental_matches_full(tiny_models):
 
 def test_reference_phi2_incremental_matches_full(tiny_models):
     _check_incremental(tiny_models["tiny-phi2"])
+
+
+def test_unknown_architecture_fails_loudly(tmp_path):
+    """An architecture the engine does not implement must raise at load, never run as llama."""
+    import pytest as _pt
+
+    from ollama_operator_amd.gguf.constants import FileType
+    from ollama_operator_amd.gguf.reader import read_gguf
+    from ollama_operator_amd.models.config import ModelConfig, UnsupportedArchitecture, preset
+    from ollama_operator_amd.models.random_init import write_random_gguf
+    path = str(tmp_path / "t.gguf")
+    write_random_gguf(path, preset("tiny-llama"), FileType.MOSTLY_Q8_0, seed=0)
+    md = dict(read_gguf(path).metadata)
+    md2 = {k.replace("llama.", "starcoder2."): v for k, v in md.items()}
+    md2["general.architecture"] = "starcoder2"
+    with _pt.raises(UnsupportedArchitecture, match="starcoder2"):
+        ModelConfig.from_gguf_metadata(md2)
+    del md["general.architecture"]
+    with _pt.raises(UnsupportedArchitecture):
+        ModelConfig.from_gguf_metadata(md)

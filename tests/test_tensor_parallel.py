@@ -112,3 +112,34 @@ def test_tp_watchdog_quiet_on_shutdown():
     t.start()
     t.join(5)
     assert codes == []
+
+
+def test_tp_watchdog_exits_on_allreduce_error():
+    """A one-shot all-reduce barrier timeout on the leader (a wedged peer) must end the
+    server non-zero even though every worker process is still alive."""
+    import subprocess
+    import sys
+    import threading
+
+    from ollama_operator_amd.parallel.tp import TPWorld, _watchdog
+    alive = subprocess.Popen([sys.executable, "-c", "import time; time.sleep(30)"])
+    world = TPWorld(0, 2, "cpu", None, None, [alive])
+    err = [0]
+    world.ar_probe = lambda: err[0]
+    codes = []
+    t = threading.Thread(target=_watchdog, args=(world, 0.05, codes.append))
+    t.start()
+    import time
+    time.sleep(0.2)
+    assert codes == []  # healthy: quiet
+    err[0] = 2  # peer 1 missed a barrier
+    t.join(10)
+    assert codes == [1]
+    assert alive.wait(10) is not None
+
+
+def test_tp_collective_error_is_a_device_fault():
+    from ollama_operator_amd.parallel.custom_ar import TPCollectiveError
+    from ollama_operator_amd.server.app import is_device_fault
+    assert is_device_fault(TPCollectiveError("peer 1 missed an all-reduce barrier"))
+    assert not is_device_fault(RuntimeError("out of KV blocks"))
