@@ -17,6 +17,8 @@ takes over at once instead of after the lease duration.
 from __future__ import annotations
 
 import argparse
+import collections
+import hashlib
 import heapq
 import json
 import logging
@@ -316,19 +318,41 @@ class MetricsAuth:
     """kube-rbac-proxy semantics in process: TokenReview (authn) + SubjectAccessReview (authz on the
     /metrics non-resource URL). Decisions are cached briefly, as the proxy does."""
 
+    MAX_ENTRIES = 1024       # bounded: random bearer tokens cannot grow memory
+    REVIEWS_PER_S = 20.0     # TokenReview calls for unseen tokens (token bucket, burst = 1 s)
+
     def __init__(self, kube, ttl: float = 30.0):
         self.kube = kube
         self.ttl = ttl
-        self._cache: dict[str, tuple[float, int]] = {}
+        self._cache: "collections.OrderedDict[str, tuple[float, int]]" = collections.OrderedDict()
+        self._lock = threading.Lock()
+        self._bucket = self.REVIEWS_PER_S
+        self._bucket_t = time.monotonic()
+
+    def _allow_review(self) -> bool:
+        now = time.monotonic()
+        self._bucket = min(self.REVIEWS_PER_S, self._bucket + (now - self._bucket_t) * self.REVIEWS_PER_S)
+        self._bucket_t = now
+        if self._bucket < 1.0:
+            return False
+        self._bucket -= 1.0
+        return True
 
     def check(self, header: str | None) -> int:
         """HTTP status for a request carrying this Authorization header: 200, 401 or 403."""
         if not header or not header.startswith("Bearer "):
             return 401
+        # keyed by a digest: raw bearer tokens are never kept in memory
+        key = hashlib.sha256(header[7:].strip().encode()).hexdigest()
         token = header[7:].strip()
-        hit = self._cache.get(token)
-        if hit and hit[0] > time.monotonic():
-            return hit[1]
+        now = time.monotonic()
+        with self._lock:
+            hit = self._cache.get(key)
+            if hit and hit[0] > now:
+                self._cache.move_to_end(key)
+                return hit[1]
+            if not self._allow_review():  # a flood of unseen tokens: no apiserver call
+                return 401
         try:
             tr = self.kube.create("TokenReview", None, {
                 "apiVersion": "authentication.k8s.io/v1", "kind": "TokenReview", "spec": {"token": token}})
@@ -345,7 +369,13 @@ class MetricsAuth:
         except (ApiError, OSError) as e:
             log.info("metrics authn/authz failed: %s", e)
             return 401
-        self._cache[token] = (time.monotonic() + self.ttl, code)
+        with self._lock:
+            now = time.monotonic()
+            for k in [k for k, (exp, _) in self._cache.items() if exp <= now]:
+                del self._cache[k]  # expired entries go on insert
+            self._cache[key] = (now + self.ttl, code)
+            while len(self._cache) > self.MAX_ENTRIES:
+                self._cache.popitem(last=False)
         return code
 
 
@@ -368,6 +398,16 @@ def serve_probes(manager: Manager, health_addr: str, metrics_addr: str, secure: 
 
     def make(handler_map, authz=None):
         class H(BaseHTTPRequestHandler):
+            timeout = 10  # per-connection socket timeout (StreamRequestHandler.setup)
+
+            def setup(self):
+                # TLS handshake in this per-connection thread, bounded by the timeout: a client that
+                # connects and never sends a ClientHello cannot block accept() for everyone
+                if isinstance(self.request, ssl.SSLSocket):
+                    self.request.settimeout(self.timeout)
+                    self.request.do_handshake()
+                super().setup()
+
             def do_GET(self):
                 fn = handler_map.get(self.path.split("?")[0])
                 if fn is None:
@@ -412,7 +452,7 @@ def serve_probes(manager: Manager, health_addr: str, metrics_addr: str, secure: 
             ctx.minimum_version = ssl.TLSVersion.TLSv1_2
             ctx.set_alpn_protocols(["http/1.1"])  # never h2 (reference cmd/main.go:78-92)
             ctx.load_cert_chain(crt, key)
-            s.socket = ctx.wrap_socket(s.socket, server_side=True)
+            s.socket = ctx.wrap_socket(s.socket, server_side=True, do_handshake_on_connect=False)
         threading.Thread(target=s.serve_forever, daemon=True).start()
         servers.append(s)
     return servers

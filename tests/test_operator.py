@@ -267,15 +267,42 @@ def test_secure_metrics_tokenreview_and_sar():
                 return r.status, r.read()
         except urllib.error.HTTPError as e:
             return e.code, b""
+    import socket
     try:
+        # a client that connects and never sends a ClientHello must not block the endpoint (the TLS
+        # handshake runs in the per-connection thread)
+        idle = socket.create_connection(("127.0.0.1", port))
         assert get(None)[0] == 401
         assert get("forged")[0] == 401
         assert get("nobody")[0] == 403
         code, body = get("good")
         assert code == 200 and b"controller_runtime_reconcile_total" in body
+        idle.close()
     finally:
         for s in servers:
             s.shutdown()
+
+
+def test_metrics_auth_cache_bounded_and_hashed():
+    from ollama_operator_amd.operator.controller import MetricsAuth
+    k = FakeKube()
+    k.tokens = {"good": "system:serviceaccount:monitoring:prometheus"}
+    k.metrics_readers = {"system:serviceaccount:monitoring:prometheus"}
+    a = MetricsAuth(k)
+    a.MAX_ENTRIES = 8
+    a.REVIEWS_PER_S = 1e9  # no rate limit for the size check
+    a._bucket = 1e9
+    for i in range(50):
+        assert a.check(f"Bearer random{i}") == 401
+    assert len(a._cache) <= 8
+    assert all("random" not in key for key in a._cache)  # digests, not raw tokens
+    assert a.check("Bearer good") == 200
+    b = MetricsAuth(k)
+    b.REVIEWS_PER_S = 2.0
+    b._bucket = 2.0
+    calls = [b.check(f"Bearer flood{i}") for i in range(10)]
+    assert calls.count(401) == 10
+    assert len(b._cache) <= 3  # at most the bucket's reviews were made (and cached)
 
 
 def test_sigterm_drains_and_releases_lease():
