@@ -166,9 +166,18 @@ class DeviceWeights:
         self.tp_rank, self.tp_size = tp_rank, tp_size
         T, r = tp_size, tp_rank
         E, H, Hkv, D, F, V = cfg.n_embd, cfg.n_head, cfg.n_head_kv, cfg.head_dim, cfg.n_ff, cfg.n_vocab
-        if H % T or Hkv % T or F % T or V % T:
-            raise ValueError(f"tp={T} must divide heads ({H}/{Hkv}), n_ff ({F}) and vocab ({V})")
-        Hl, Hkvl, Fl, Vl = H // T, Hkv // T, F // T, V // T
+        if H % T or Hkv % T or V % T:
+            raise ValueError(f"tp={T} must divide heads ({H}/{Hkv}) and vocab ({V})")
+        # FFN rows per rank: whole 256-weight super-blocks of the down projection's K, split as evenly
+        # as they go -- Llama-2-7B's n_ff = 11008 is 43 super-blocks, so TP=2 ranks hold 22 / 21
+        # (Megatron row-parallel needs no equal split: the all-reduce sums E-wide partials)
+        f_unit = 256 if F % 256 == 0 else 32
+        nbf = F // f_unit
+        if F % f_unit or nbf < T or (cfg.n_expert and F % T):
+            raise ValueError(f"tp={T} cannot split n_ff={F} on quant-block boundaries")
+        f0, f1 = (r * nbf // T) * f_unit, ((r + 1) * nbf // T) * f_unit
+        self.f_range = (f0, f1)
+        Hl, Hkvl, Fl, Vl = H // T, Hkv // T, (f1 - f0) if not cfg.n_expert else F // T, V // T
         self.cfg = cfg
         self.local = dict(E=E, H=Hl, Hkv=Hkvl, D=D, F=Fl, V=Vl)
         dev = device
@@ -183,6 +192,10 @@ class DeviceWeights:
         def kblocks(K_full: int, name: str) -> tuple[int, int]:
             blk = BLOCK_GEOMETRY[GGMLType(src.qtype_of(name))][0]
             nb = K_full // blk
+            if K_full == F and not cfg.n_expert:  # row-parallel over the (possibly uneven) FFN split
+                if f0 % blk or f1 % blk:
+                    raise ValueError(f"{name}: FFN split {f0}:{f1} not on {blk}-weight blocks")
+                return (f0 // blk, f1 // blk)
             if nb % T:
                 raise ValueError(f"{name}: {nb} blocks of {blk} not divisible by tp={T}")
             return (r * nb // T, (r + 1) * nb // T)
@@ -207,8 +220,8 @@ class DeviceWeights:
                 L["wo"] = build_qmat(src, [(b + "attn_output.weight", ar(E), ar(E))], E, E,
                                      kblocks(E, b + "attn_output.weight"), dev, widen=True)
                 L["bo"] = t(src.f32(b + "attn_output.bias")) if r == 0 else None
-                L["wgu"] = build_qmat(src, [(b + "ffn_up.weight", ar(Fl, r * Fl), ar(Fl))], Fl, E, None, dev)
-                L["bup"] = t(src.f32(b + "ffn_up.bias")[r * Fl:(r + 1) * Fl])
+                L["wgu"] = build_qmat(src, [(b + "ffn_up.weight", ar(Fl, f0), ar(Fl))], Fl, E, None, dev)
+                L["bup"] = t(src.f32(b + "ffn_up.bias")[f0:f1])
                 L["wdown"] = build_qmat(src, [(b + "ffn_down.weight", ar(E), ar(E))], E, F,
                                         kblocks(F, b + "ffn_down.weight"), dev, widen=True)
                 L["bdown"] = t(src.f32(b + "ffn_down.bias")) if r == 0 else None
@@ -240,7 +253,7 @@ class DeviceWeights:
                                                 kblocks(F, b + "ffn_down_exps.weight"), dev, expert_rows=E)
                 else:
                     ng, nu = b + "ffn_gate.weight", b + "ffn_up.weight"
-                    loc = ar(Fl, r * Fl)
+                    loc = ar(Fl, f0)
                     L["wgu"] = build_qmat(src, [(ng, loc, 2 * ar(Fl)), (nu, loc, 2 * ar(Fl) + 1)], 2 * Fl, E, None, dev)
                     L["wdown"] = build_qmat(src, [(b + "ffn_down.weight", ar(E), ar(E))], E, F,
                                             kblocks(F, b + "ffn_down.weight"), dev, widen=True)

@@ -150,6 +150,9 @@ PRESETS: dict[str, ModelConfig] = {
     # tensor-parallel test shapes: every row-parallel K spans >= 2 super-blocks per rank at TP=2
     "tiny-llama-tp": ModelConfig(name="tiny-llama-tp", n_vocab=512, n_embd=1024, n_layer=2, n_head=16,
                                  n_head_kv=4, n_ff=1024, n_rot=64, ctx_len=256),
+    # n_ff = 3 super-blocks: TP=2 ranks hold an uneven 512 / 256 FFN split (as Llama-2-7B's 43 blocks)
+    "tiny-llama-tp-odd": ModelConfig(name="tiny-llama-tp-odd", n_vocab=512, n_embd=1024, n_layer=2, n_head=16,
+                                     n_head_kv=4, n_ff=768, n_rot=64, ctx_len=256),
     "tiny-phi2-tp": ModelConfig(name="tiny-phi2-tp", arch="phi2", n_vocab=512, n_embd=1024, n_layer=2,
                                 n_head=16, n_head_kv=16, n_ff=2048, n_rot=32, rope_mode=ROPE_NEOX,
                                 ctx_len=256, bos_id=0, eos_id=0),

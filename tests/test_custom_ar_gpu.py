@@ -202,6 +202,7 @@ def _run(r, prompt=PROMPT):
 
 
 @pytest.mark.parametrize("name,ft", [("tiny-llama-tp", FileType.MOSTLY_Q4_K_M),
+                                     ("tiny-llama-tp-odd", FileType.MOSTLY_Q4_K_M),
                                      ("tiny-mixtral-tp", FileType.MOSTLY_Q8_0)])
 def test_tp2_graph_decode_matches_tp1(tmp_path, name, ft):
     path = str(tmp_path / f"{name}.gguf")

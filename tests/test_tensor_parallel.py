@@ -50,6 +50,7 @@ def _worker(rank, world, port, path, out_dir):
 
 
 @pytest.mark.parametrize("name,ft", [("tiny-llama-tp", FileType.MOSTLY_Q4_K_M),
+                                     ("tiny-llama-tp-odd", FileType.MOSTLY_Q4_K_M),
                                      ("tiny-phi2-tp", FileType.MOSTLY_Q4_0),
                                      ("tiny-mixtral-tp", FileType.MOSTLY_Q8_0)])
 def test_tp2_matches_tp1(tmp_path, name, ft):
