@@ -1,6 +1,6 @@
 """Disassemble the gfx950 kernels of the built extension whose (mangled) name matches a regex.
 
-    python scripts/dis.py REGEX [--so path] [--stats]   (--stats: opcode histogram per kernel)
+    python scripts/disasm.py REGEX [--so path] [--stats]   (--stats: opcode histogram per kernel)
 """
 from __future__ import annotations
 
