@@ -19,6 +19,7 @@ import sysconfig
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(ROOT, "csrc")
+CPU_SRC = os.path.join(CSRC, "cpu")
 BUILD = os.path.join(ROOT, "build", "native")
 ARCH = os.environ.get("OMX_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
@@ -62,8 +63,9 @@ def build(jobs: int | None = None, clean: bool = False, verbose: bool = False) -
     if clean:
         for f in glob.glob(os.path.join(BUILD, "*.o")):
             os.remove(f)
-    srcs = sorted(glob.glob(os.path.join(CSRC, "**", "*.hip"), recursive=True) +
-                  glob.glob(os.path.join(CSRC, "**", "*.cpp"), recursive=True))
+    srcs = sorted(s for s in glob.glob(os.path.join(CSRC, "**", "*.hip"), recursive=True) +
+                  glob.glob(os.path.join(CSRC, "**", "*.cpp"), recursive=True)
+                  if not s.startswith(CPU_SRC + os.sep))  # the CPU backend is its own module (build_cpu)
     hdr_mtime = max((os.path.getmtime(h) for h in _headers()), default=0.0)
     py_inc = sysconfig.get_paths()["include"]
     common = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", CSRC,
@@ -112,9 +114,38 @@ def build(jobs: int | None = None, clean: bool = False, verbose: bool = False) -
     return out
 
 
+def cpu_target_path() -> str:
+    return os.path.join(ROOT, "ollama_operator_amd", "_cpu" + _ext_suffix())
+
+
+def build_cpu(verbose: bool = False) -> str:
+    """`ollama_operator_amd/_cpu*.so`: the CPU serving backend (csrc/cpu), host compiler only (no HIP
+    runtime dependency, so it loads on a CPU-only node). AVX2 + FMA + F16C baseline, OpenMP threads."""
+    import pybind11
+    srcs = sorted(glob.glob(os.path.join(CPU_SRC, "*.cpp")))
+    hdrs = glob.glob(os.path.join(CPU_SRC, "*.h"))
+    out = cpu_target_path()
+    newest = max(os.path.getmtime(f) for f in srcs + hdrs)
+    if os.path.exists(out) and os.path.getmtime(out) >= newest:
+        return out
+    cxx = os.environ.get("CXX", "g++")
+    cmd = [cxx, "-O3", "-std=c++17", "-fPIC", "-shared", "-fopenmp", "-mavx2", "-mfma", "-mf16c",
+           "-fvisibility=hidden", "-I", CPU_SRC, "-I", pybind11.get_include(), "-I", sysconfig.get_paths()["include"],
+           *srcs, "-o", out]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("CPU backend build failed:\n" + " ".join(cmd) + "\n" + r.stdout + r.stderr)
+    if verbose:
+        print("built", os.path.relpath(out, ROOT))
+    return out
+
+
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--clean", action="store_true")
     ap.add_argument("--jobs", type=int, default=None)
+    ap.add_argument("--cpu-only", action="store_true", help="build only the CPU backend module")
     a = ap.parse_args()
-    print(build(a.jobs, a.clean, verbose=True))
+    print(build_cpu(verbose=True))
+    if not a.cpu_only:
+        print(build(a.jobs, a.clean, verbose=True))

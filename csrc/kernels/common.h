@@ -71,6 +71,18 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
   return t;
 }
 
+// runtime block size variant: nw = blockDim.x / 64 waves
+__device__ __forceinline__ float block_sum_rt(float v, float* red, int nw) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __syncthreads();
+  if (l == 0) red[w] = v;
+  __syncthreads();
+  float t = 0.f;
+  for (int i = 0; i < nw; ++i) t += red[i];
+  return t;
+}
+
 template <int NT>
 __device__ __forceinline__ float block_max(float v, float* red) {
   v = wave_max(v);

@@ -34,9 +34,10 @@ namespace omx {
 
 
 GemvTuning g_tune;
-void set_gemv_tuning(int blocks_per_cu, int rows, int debug, int ks, int xfirst) {
+void set_gemv_tuning(int blocks_per_cu, int rows, int debug, int ks, int xfirst, int xbar) {
   g_tune.debug = debug > 0 ? debug : 0;
   if (xfirst == 0 || xfirst == 1) g_tune.xfirst = xfirst;
+  if (xbar == 0 || xbar == 1) g_tune.xbar = xbar;
   if (ks >= 0 && ks <= 4) g_tune.ks = ks;
   if (blocks_per_cu > 0) g_tune.blocks_per_cu = blocks_per_cu;
   if (rows == 1 || rows == 2) g_tune.rows = rows;
@@ -157,9 +158,22 @@ __global__ __launch_bounds__(GEMV_NT) void qgemv_kernel(GemvParams P) {
 // MRG > 0 (B == 1 decode, O projection): x holds MRG unmerged flash-decode partial slabs
 // (attention.hip `defer`); the prologue merges them per head in registers -- the merge rides on the
 // activation round trip this kernel pays anyway, instead of an in-launch ticket + re-read (~2.5 us).
-template <int QT, int NSB, int R, int J, int NRM, int DBG = 0, int KS = 1, int MRG = 0>
+// JG > 1: the block holds JG independent groups of GEMV_NW * KS waves, each acting as its own
+// (sub-)block over the tiles vb = bx * JG + jg (+ j * gxn * JG); they share the staged activations.
+// XB (x barrier): every wave's activation loads are drained and the block meets at a barrier BEFORE
+// any weight is requested. Measured (profiles/r3_gemv, scripts/gemv_timeline.py): a CU returns vector
+// loads in issue order across its waves, so an activation load issued by any wave after another
+// wave's weight burst waits for that whole burst -- the prologue ended only after the CU's entire
+// weight share had streamed (gate_up 6.3 us, down Q6_K 8.2 us), and every dot product then ran after
+// the stream instead of under it. With XB and one block per CU (JG / J sized so the grid = #CUs) the
+// activations land in ~1 us and the tiles are consumed as they arrive.
+// JG == 0: the group count is read from the launch (blockDim.x / (64 * GEMV_NW)).
+template <int QT, int NSB, int R, int J, int NRM, int DBG = 0, int KS = 1, int MRG = 0, int JG = 1, int XB = 0>
 __device__ __forceinline__ void flight_body(const GemvParams& P, const int bx, const int gxn) {
-  constexpr int ROWS_B = GEMV_NW * 4 * R, NT = GEMV_NT * KS;
+  static_assert(KS == 1 || JG == 1, "tile groups and the in-block K split do not combine");
+  constexpr int ROWS_B = GEMV_NW * 4 * R;
+  const int NT = JG == 0 ? (int)blockDim.x : GEMV_NT * KS * JG;
+  const int JGr = JG == 0 ? (int)blockDim.x / GEMV_NT : JG;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const QMat& w = P.w;
   auto stamp = [&](int k) {
@@ -173,11 +187,13 @@ __device__ __forceinline__ void flight_body(const GemvParams& P, const int bx, c
   f32x2* lf = (f32x2*)(smem + (size_t)(XS + 1) * 16);  // [XS + 1]
   float* red = (float*)(lf + XS + 1);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = lane >> 4, s = lane & 15;
+  const int jg = JG != 1 ? wave / GEMV_NW : 0;      // tile group
   const int kg = KS > 1 ? wave / GEMV_NW : 0, gtid = tid - kg * GEMV_NT;
   const int CH = KS > 1 ? (SB + KS - 1) / KS : SB;
   const int sb0 = kg * CH, se = min(SB, sb0 + CH);
   const int n_tiles = (N + ROWS_B - 1) / ROWS_B;
-  const int rbase = (wave - kg * GEMV_NW) * (4 * R) + g * R;
+  const int rbase = (wave - kg * GEMV_NW - jg * GEMV_NW) * (4 * R) + g * R;
+  const int vb = bx * JGr + jg, gv = gxn * JGr;    // this group's first tile and tile stride
 
   long long row_base = 0;
   const float* x = P.x;
@@ -216,6 +232,10 @@ __device__ __forceinline__ void flight_body(const GemvParams& P, const int bx, c
   }
   __builtin_amdgcn_sched_barrier(0);  // activations ahead of the weights
   if constexpr ((DBG & 4) != 0) __builtin_amdgcn_s_barrier();  // every wave's x requests queued first
+  if constexpr (XB) {  // every activation byte of the block landed before the first weight request
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
   // x-first (GemvTuning::xfirst): wait for the activations BEFORE requesting any weight. The x lines
   // were just written by the previous kernel and miss L2; issued behind the whole matrix's requests
   // they return only after most of the weight stream (profiles/r1_defer/gemv_timeline.log: prologue
@@ -226,7 +246,7 @@ __device__ __forceinline__ void flight_body(const GemvParams& P, const int bx, c
   WTile<QT, NSB, R> T[J];
 #pragma unroll
   for (int j = 0; j < J; ++j) {
-    const int t = min(bx + j * gxn, n_tiles - 1);
+    const int t = min(vb + j * gv, n_tiles - 1);
     load_wtile<QT, NSB, R>(w, row_base, t * ROWS_B + rbase, N, SB, sb0, s, T[j], se);
   }
   __builtin_amdgcn_sched_barrier(0);  // every load issued before the prologue's first wait
@@ -272,9 +292,9 @@ __device__ __forceinline__ void flight_body(const GemvParams& P, const int bx, c
         sm += v.x + v.y + v.z + v.w;
         ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
       }
-    ss = block_sum<NT>(ss, red);
+    ss = block_sum_rt(ss, red, NT / 64);
     if (NRM == 2 || P.norm == NORM_LAYER) {
-      sm = block_sum<NT>(sm, red);
+      sm = block_sum_rt(sm, red, NT / 64);
       mean = sm / K;
       rstd = rsqrtf(fmaxf(ss / K - mean * mean, 0.f) + P.eps);
     } else {
@@ -344,12 +364,12 @@ __device__ __forceinline__ void flight_body(const GemvParams& P, const int bx, c
       for (int r = 0; r < R; ++r) part[((kg - 1) * R + r) * GEMV_NT + gtid] = acc[r][0];
     }
     __syncthreads();
-    if (kg == 0 && bx < n_tiles) {
+    if (kg == 0 && vb < n_tiles) {
 #pragma unroll
       for (int k = 1; k < KS; ++k)
 #pragma unroll
         for (int r = 0; r < R; ++r) acc[r][0] += part[((k - 1) * R + r) * GEMV_NT + gtid];
-      finish_rows<R, 1>(P, acc, bx * ROWS_B + rbase, N, 0, s);
+      finish_rows<R, 1>(P, acc, vb * ROWS_B + rbase, N, 0, s);
     }
     stamp(3);
     return;
@@ -357,8 +377,8 @@ __device__ __forceinline__ void flight_body(const GemvParams& P, const int bx, c
   // 4. consume the tiles in issue order
 #pragma unroll
   for (int j = 0; j < J; ++j) {
-    const int t = bx + j * gxn;
-    if (t >= n_tiles) break;  // block-uniform
+    const int t = vb + j * gv;
+    if (t >= n_tiles) break;  // group-uniform (no barrier follows)
     float acc[R][1];
 #pragma unroll
     for (int r = 0; r < R; ++r) acc[r][0] = 0.f;
@@ -381,9 +401,24 @@ __device__ __forceinline__ void flight_body(const GemvParams& P, const int bx, c
   stamp(3);
 }
 
-template <int QT, int NSB, int R, int J, int NRM, int DBG = 0, int KS = 1, int MRG = 0>
+template <int QT, int NSB, int R, int J, int NRM, int DBG = 0, int KS = 1, int MRG = 0, int XB = 0>
 __global__ __launch_bounds__(GEMV_NT * KS) void qgemv_flight_kernel(GemvParams P) {
-  flight_body<QT, NSB, R, J, NRM, DBG, KS, MRG>(P, blockIdx.x, gridDim.x);
+  flight_body<QT, NSB, R, J, NRM, DBG, KS, MRG, 1, XB>(P, blockIdx.x, gridDim.x);
+}
+
+// x-barrier flight kernel, one block per CU: 1-3 groups of 4 waves (blockDim.x = 256 * groups).
+// Variants whose registers exceed the 168 VGPRs of 3 waves per SIMD (NSB = 2, 8-split merges,
+// LayerNorm Q8_0 / Q6_K pairs) are built for one group (MJ = 1, 512 VGPRs) -- no scratch.
+constexpr int XB_MAX_JG = 3;
+template <int QT, int NSB, int J, int NRM, int MRG>
+constexpr int xb_maxjg() {
+  constexpr int PB = QT == QT_Q8_0 ? 8 : QT == QT_Q6_K ? 6 : QT == QT_Q5_K ? 5 : 4;
+  constexpr int regs = J * NSB * (8 * PB + 5) + NSB * 16 * (1 + (NRM != 0) + (NRM == 2)) + MRG * NSB * 18 + 30;
+  return regs <= 150 ? XB_MAX_JG : 1;
+}
+template <int QT, int NSB, int J, int NRM, int MRG>
+__global__ __launch_bounds__((GEMV_NT * xb_maxjg<QT, NSB, J, NRM, MRG>())) void qgemv_flight_xb_kernel(GemvParams P) {
+  flight_body<QT, NSB, 1, J, NRM, 0, 1, MRG, 0, 1>(P, blockIdx.x, gridDim.x);
 }
 
 // two matrices that read the same normalised x in ONE launch (Q4_K_M QKV: q,k rows Q4_K + v rows
@@ -395,6 +430,15 @@ __global__ __launch_bounds__(GEMV_NT) void qgemv_flight_dual_kernel(GemvParams P
   else flight_body<QB, NSB, 1, 1, NRM>(PB, (int)blockIdx.x - gxa, (int)gridDim.x - gxa);
 }
 
+// x-barrier dual launch: one block per CU, JG tile groups per block; side A takes JA tiles per
+// group, side B JB (q,k rows Q4_K: 512 tiles, v rows Q6_K: 256 tiles -> JA = 2, JB = 1)
+template <int QA, int QB, int NSB, int NRM, int JA, int JB>
+__global__ __launch_bounds__(GEMV_NT * XB_MAX_JG) void qgemv_flight_dual_xb_kernel(GemvParams PA, GemvParams PB,
+                                                                                   int gxa) {
+  if ((int)blockIdx.x < gxa) flight_body<QA, NSB, 1, JA, NRM, 0, 1, 0, 0, 1>(PA, blockIdx.x, gxa);
+  else flight_body<QB, NSB, 1, JB, NRM, 0, 1, 0, 0, 1>(PB, (int)blockIdx.x - gxa, (int)gridDim.x - gxa);
+}
+
 // register tiles a block keeps in flight: ~150 VGPRs of weight tiles per lane
 template <int QT, int NSB, int R>
 constexpr int flight_jmax() {
@@ -403,7 +447,9 @@ constexpr int flight_jmax() {
   return regs * 3 <= 150 ? 3 : regs * 2 <= 150 ? 2 : 1;
 }
 
-static size_t lds_bytes(int K, int BT) { return (size_t)BT * ((K + 255) / 256) * XPAD * 24 + 24 + 4 * GEMV_NW; }
+static size_t lds_bytes(int K, int BT, int JG = 1) {
+  return (size_t)BT * ((K + 255) / 256) * XPAD * 24 + 24 + 4 * GEMV_NW * JG;
+}
 // flight kernel with an in-block K split: activation slots + reduction slots + partial sums
 static size_t lds_bytes_ks(int K, int KS, int R) {
   return (size_t)((K + 255) / 256) * XPAD * 24 + 24 + 4 * GEMV_NW * KS + (size_t)4 * (KS - 1) * R * GEMV_NT;
@@ -460,7 +506,89 @@ static void launch_flight_ks_n(const GemvParams& P, int gx, hipStream_t s) {
       default: break;
     }
   }
-  hipLaunchKernelGGL((qgemv_flight_kernel<QT, NSB, 1, 1, NRM, 0, KS>), dim3(gx, 1, bz), dim3(GEMV_NT * KS), lds, s, P);
+  if (g_tune.xbar && !P.expert_ids)
+    hipLaunchKernelGGL((qgemv_flight_kernel<QT, NSB, 1, 1, NRM, 0, KS, 0, 1>), dim3(gx, 1, bz), dim3(GEMV_NT * KS), lds, s, P);
+  else
+    hipLaunchKernelGGL((qgemv_flight_kernel<QT, NSB, 1, 1, NRM, 0, KS>), dim3(gx, 1, bz), dim3(GEMV_NT * KS), lds, s, P);
+}
+
+static int cu_count() {
+  static int n = 0;
+  if (n <= 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+  }
+  return n;
+}
+
+// (JG, J) of an x-barrier launch: the smallest per-block capacity JG * J (tile groups x tiles per
+// group) that fits the tiles in one block per CU; J <= 2 keeps three 4-wave groups within the
+// 168-VGPR budget of 3 waves per SIMD. false: the matrix needs more (old launch shape).
+static bool xb_shape(int tiles, int jmax, int& JG, int& J, int& gx) {
+  const int ncu = cu_count();
+  const int cap = (tiles + ncu - 1) / ncu;
+  if (cap <= XB_MAX_JG) {
+    J = 1;
+    JG = cap;
+  } else {
+    J = 2;
+    JG = (cap + 1) / 2;
+  }
+  if (JG > XB_MAX_JG || J > jmax) return false;
+  gx = (tiles + JG * J - 1) / (JG * J);
+  return true;
+}
+
+// launches the variant if its register class admits JG groups; false otherwise
+template <int QT, int NSB, int J, int NRM, int MRG>
+static bool launch_xb_m(const GemvParams& P, int JG, int gx, hipStream_t s) {
+  if (JG > xb_maxjg<QT, NSB, J, NRM, MRG>()) return false;
+  hipLaunchKernelGGL((qgemv_flight_xb_kernel<QT, NSB, J, NRM, MRG>), dim3(gx), dim3(GEMV_NT * JG),
+                     lds_bytes(P.w.K, 1, JG), s, P);
+  return true;
+}
+
+template <int QT, int NSB, int J, int NRM>
+static bool launch_xb_n(const GemvParams& P, int JG, int gx, hipStream_t s) {
+  if constexpr (NSB == 1 && J == 1 && NRM == 0) {
+    switch (P.merge_S) {  // deferred flash-decode merge in the prologue (O projection)
+      case 0: break;
+      case 2: return launch_xb_m<QT, NSB, J, NRM, 2>(P, JG, gx, s);
+      case 4: return launch_xb_m<QT, NSB, J, NRM, 4>(P, JG, gx, s);
+      case 8: return launch_xb_m<QT, NSB, J, NRM, 8>(P, JG, gx, s);
+      default: return false;
+    }
+  }
+  return launch_xb_m<QT, NSB, J, NRM, 0>(P, JG, gx, s);
+}
+
+template <int QT, int NSB, int J>
+static bool launch_xb_j(const GemvParams& P, int JG, int gx, hipStream_t s) {
+  if (P.norm == NORM_NONE) return launch_xb_n<QT, NSB, J, 0>(P, JG, gx, s);
+  if (P.norm == NORM_LAYER && P.norm_b) return launch_xb_n<QT, NSB, J, 2>(P, JG, gx, s);
+  return launch_xb_n<QT, NSB, J, 1>(P, JG, gx, s);
+}
+
+// batch-1 decode GEMV as one x-barrier block per CU (see flight_body XB); false = not covered
+template <int QT>
+static bool launch_flight_xb(const GemvParams& P, int need, hipStream_t s) {
+  if constexpr (QT == QT_Q6_K8) {
+    return false;
+  } else {
+    if (!g_tune.xbar || P.expert_ids || g_tune.debug || need > 2) return false;
+    const int tiles = (P.w.N + 4 * GEMV_NW - 1) / (4 * GEMV_NW);
+    int JG, J, gx;
+    if (need == 1) {
+      if (!xb_shape(tiles, flight_jmax<QT, 1, 1>() >= 2 ? 2 : 1, JG, J, gx)) return false;
+      if (J == 1) return launch_xb_j<QT, 1, 1>(P, JG, gx, s);
+      if constexpr (flight_jmax<QT, 1, 1>() >= 2) return launch_xb_j<QT, 1, 2>(P, JG, gx, s);
+      return false;
+    }
+    if (P.merge_S || !xb_shape(tiles, 1, JG, J, gx)) return false;
+    return launch_xb_j<QT, 2, 1>(P, JG, gx, s);
+  }
 }
 
 template <int QT, int NSB, int R, int J>
@@ -553,6 +681,7 @@ static void launch_nsb(const GemvParams& P, hipStream_t s) {
 template <int QT>
 static void launch_q(const GemvParams& P, hipStream_t s) {
   if (P.merge_S > 0) {  // only the single-chunk B == 1 flight kernel merges (merge_supported())
+    if (launch_flight_xb<QT>(P, 1, s)) return;
     launch_flight<QT, 1, 1>(P, s);
     return;
   }
@@ -561,6 +690,7 @@ static void launch_q(const GemvParams& P, hipStream_t s) {
     if (P.B == 1 && need <= 4) {  // whole K in one chunk: all-in-flight kernel
       if (g_tune.rows == 2 && need == 1) { launch_flight<QT, 1, 2>(P, s); return; }
       if (launch_flight_split<QT>(P, need, s)) return;
+      if (launch_flight_xb<QT>(P, need, s)) return;
       switch (need) {
         case 1: launch_flight<QT, 1, 1>(P, s); return;
         case 2: launch_flight<QT, 2, 1>(P, s); return;
@@ -590,8 +720,38 @@ static void launch_dual_n(const GemvParams& A, const GemvParams& Bp, hipStream_t
                      s, A, Bp, ta);
 }
 
+// x-barrier dual launch for the Q4_K_M / Q5_K_M QKV (q,k rows Q4_K or Q5_K, v rows Q6_K): the group
+// count and per-side tiles per group that put the most blocks on distinct CUs
+template <int QA, int QB>
+static bool launch_dual_xb(const GemvParams& A, const GemvParams& Bp, int need, hipStream_t s) {
+  if constexpr (!((QA == QT_Q4_K || QA == QT_Q5_K) && QB == QT_Q6_K)) {
+    return false;
+  } else {
+    if (!g_tune.xbar || need != 1) return false;
+    const int ta = (A.w.N + 4 * GEMV_NW - 1) / (4 * GEMV_NW), tb = (Bp.w.N + 4 * GEMV_NW - 1) / (4 * GEMV_NW);
+    const int ncu = cu_count();
+    int best = -1, bJG = 0, bJA = 0, bJB = 0;
+    for (int JG = XB_MAX_JG; JG >= 1; --JG)
+      for (int JA = 1; JA <= 2; ++JA)
+        for (int JB = 1; JB <= 2; ++JB) {
+          const int blocks = (ta + JG * JA - 1) / (JG * JA) + (tb + JG * JB - 1) / (JG * JB);
+          if (blocks <= ncu && blocks > best) { best = blocks; bJG = JG; bJA = JA; bJB = JB; }
+        }
+    if (best < 0) return false;
+    const int gxa = (ta + bJG * bJA - 1) / (bJG * bJA);
+    const size_t lds = lds_bytes(A.w.K, 1, bJG);
+    const dim3 blk(GEMV_NT * bJG), grid(best);
+    if (bJA == 1 && bJB == 1) hipLaunchKernelGGL((qgemv_flight_dual_xb_kernel<QA, QB, 1, 1, 1, 1>), grid, blk, lds, s, A, Bp, gxa);
+    else if (bJA == 1) hipLaunchKernelGGL((qgemv_flight_dual_xb_kernel<QA, QB, 1, 1, 1, 2>), grid, blk, lds, s, A, Bp, gxa);
+    else if (bJB == 1) hipLaunchKernelGGL((qgemv_flight_dual_xb_kernel<QA, QB, 1, 1, 2, 1>), grid, blk, lds, s, A, Bp, gxa);
+    else hipLaunchKernelGGL((qgemv_flight_dual_xb_kernel<QA, QB, 1, 1, 2, 2>), grid, blk, lds, s, A, Bp, gxa);
+    return true;
+  }
+}
+
 template <int QA, int QB>
 static void launch_dual_q(const GemvParams& A, const GemvParams& Bp, int need, hipStream_t s) {
+  if (launch_dual_xb<QA, QB>(A, Bp, need, s)) return;
   if (need == 1) launch_dual_n<QA, QB, 1>(A, Bp, s);
   else launch_dual_n<QA, QB, 2>(A, Bp, s);
 }

@@ -107,6 +107,8 @@ class Runner:
             native()  # fail loudly: no silent torch fallback on a GPU box
             if os.environ.get("OMX_GEMV_XFIRST") in ("0", "1"):  # decode GEMV x-first knob (gemv.hip)
                 native().set_gemv_tuning(xfirst=int(os.environ["OMX_GEMV_XFIRST"]))
+            if os.environ.get("OMX_GEMV_XBAR") in ("0", "1"):  # x-barrier one-block-per-CU decode GEMVs
+                native().set_gemv_tuning(xbar=int(os.environ["OMX_GEMV_XBAR"]))
         self.tp_rank, self.tp_size, self.tp_group = tp_rank, tp_size, tp_group
         self._closed = False
         # TP serving (parallel/tp.py): rank 0 signals each decode step, followers mirror it
