@@ -134,6 +134,7 @@ PYBIND11_MODULE(_C, m) {
         }
         return out;
       })
+      .def("release", [](const GGUFMap& g, const std::string& name) { g.release(g.get(name)); })
       .def("data_ptr", [](const GGUFMap& g, const std::string& name) {
         return reinterpret_cast<uintptr_t>(g.data(g.get(name)));
       })

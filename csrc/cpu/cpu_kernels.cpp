@@ -105,9 +105,10 @@ static inline void kscales(const uint8_t* m, int* sc, int* mn, float& d, float& 
   }
 }
 
-static inline void unpack(const QMat& w, long long row, int sb, int SB, USB& u) {
+template <int QT>
+static inline __attribute__((always_inline)) void unpack(const QMat& w, long long row, int sb, int SB, USB& u) {
   const __m256i m4 = _mm256_set1_epi8(0x0F), x80 = _mm256_set1_epi8((char)0x80);
-  switch (w.qtype) {
+  switch (QT) {
     case QT_Q4_K: {
       const uint8_t* qs = w.s[0] + row * SB * 128;
       kscales(w.s[1] + row * SB * 16 + 16 * sb, u.sc, u.mn, u.d, u.dmin);
@@ -214,8 +215,9 @@ static inline float hsum_f32(__m256 v) {
 }
 
 // dot of one unpacked SB with one activation SB; returns the fp32 contribution
-static inline float dot_sb(const QMat& w, const USB& u, const int8_t* xq, float dx, const int16_t* bs) {
-  switch (w.qtype) {
+template <int QT>
+static inline __attribute__((always_inline)) float dot_sb(const USB& u, const int8_t* xq, float dx, const int16_t* bs) {
+  switch (QT) {
     case QT_Q4_K:
     case QT_Q5_K: {
       __m256i acc = _mm256_setzero_si256();
@@ -267,26 +269,39 @@ static inline float dot_sb(const QMat& w, const USB& u, const int8_t* xq, float 
   }
 }
 
-void gemm(const QMat& w, long long row_base, int N, const float* x, int ldx, int B, float* y, int ldy,
-          bool accumulate) {
-  static thread_local QAct act;
-  quantize_rows(x, ldx, B, w.K, act);
-  const int SB = act.SB;
-  const QAct& a = act;
-  // rows in chunks: each thread streams a contiguous slice of the matrix
+// streams of the next super-block a row step reads (prefetched ahead of the unpack)
+template <int QT>
+static inline void prefetch_sb(const QMat& w, long long row, int sb, int SB) {
+  if (sb >= SB) return;
+  if constexpr (QT == QT_Q8_0) {
+    const uint8_t* qs = w.s[0] + row * SB * 256;
+    for (int t = 0; t < 8; ++t) _mm_prefetch((const char*)(qs + (t * SB + sb) * 32), _MM_HINT_T0);
+  } else {
+    const uint8_t* qs = w.s[0] + row * SB * 128;
+    for (int t = 0; t < 8; ++t) _mm_prefetch((const char*)(qs + (t * SB + sb) * 16), _MM_HINT_T0);
+  }
+}
+
+template <int QT>
+static void gemm_t(const QMat& w, long long row_base, int N, const QAct& a, float* y, int ldy, bool accumulate) {
+  const int SB = a.SB, B = a.B;
+  // rows in contiguous slices: each thread streams its own part of the matrix
 #pragma omp parallel
   {
-    std::vector<float> acc(B);
+    float accs[64];
+    std::vector<float> accv(B > 64 ? B : 0);
+    float* acc = B > 64 ? accv.data() : accs;
 #pragma omp for schedule(static)
     for (int n = 0; n < N; ++n) {
       const long long row = row_base + n;
       for (int b = 0; b < B; ++b) acc[b] = 0.f;
       for (int sb = 0; sb < SB; ++sb) {
+        prefetch_sb<QT>(w, row, sb + 2, SB);
         USB u;
-        unpack(w, row, sb, SB, u);
+        unpack<QT>(w, row, sb, SB, u);
         for (int b = 0; b < B; ++b) {
           const size_t i = (size_t)b * SB + sb;
-          acc[b] += dot_sb(w, u, a.q.data() + i * 256, a.d[i], a.bsum.data() + i * 16);
+          acc[b] += dot_sb<QT>(u, a.q.data() + i * 256, a.d[i], a.bsum.data() + i * 16);
         }
       }
       for (int b = 0; b < B; ++b) {
@@ -297,18 +312,33 @@ void gemm(const QMat& w, long long row_base, int N, const float* x, int ldx, int
   }
 }
 
-void dequant_row(const QMat& w, long long row, float* out) {
+void gemm(const QMat& w, long long row_base, int N, const float* x, int ldx, int B, float* y, int ldy,
+          bool accumulate) {
+  static thread_local QAct act;
+  quantize_rows(x, ldx, B, w.K, act);
+  switch (w.qtype) {
+    case QT_Q4_0: gemm_t<QT_Q4_0>(w, row_base, N, act, y, ldy, accumulate); break;
+    case QT_Q8_0: gemm_t<QT_Q8_0>(w, row_base, N, act, y, ldy, accumulate); break;
+    case QT_Q4_K: gemm_t<QT_Q4_K>(w, row_base, N, act, y, ldy, accumulate); break;
+    case QT_Q5_K: gemm_t<QT_Q5_K>(w, row_base, N, act, y, ldy, accumulate); break;
+    case QT_Q6_K: gemm_t<QT_Q6_K>(w, row_base, N, act, y, ldy, accumulate); break;
+    default: break;
+  }
+}
+
+template <int QT>
+static void dequant_row_t(const QMat& w, long long row, float* out) {
   const int SB = (w.K + 255) / 256;
   for (int sb = 0; sb < SB; ++sb) {
     USB u;
-    unpack(w, row, sb, SB, u);
+    unpack<QT>(w, row, sb, SB, u);
     alignas(32) uint8_t c[256];
     for (int r = 0; r < 8; ++r) _mm256_store_si256((__m256i*)(c + 32 * r), u.c[r]);
     const int n = w.K - sb * 256 < 256 ? w.K - sb * 256 : 256;
     float* o = out + sb * 256;
     for (int j = 0; j < n; ++j) {
       const int s = j / 32;
-      switch (w.qtype) {
+      switch (QT) {
         case QT_Q4_K:
         case QT_Q5_K: o[j] = u.d * u.sc[s] * c[j] - u.dmin * u.mn[s]; break;
         case QT_Q6_K: o[j] = u.d * u.sc[j / 16] * ((int)c[j] - 32); break;
@@ -317,6 +347,17 @@ void dequant_row(const QMat& w, long long row, float* out) {
         default: o[j] = 0.f;
       }
     }
+  }
+}
+
+void dequant_row(const QMat& w, long long row, float* out) {
+  switch (w.qtype) {
+    case QT_Q4_0: dequant_row_t<QT_Q4_0>(w, row, out); break;
+    case QT_Q8_0: dequant_row_t<QT_Q8_0>(w, row, out); break;
+    case QT_Q4_K: dequant_row_t<QT_Q4_K>(w, row, out); break;
+    case QT_Q5_K: dequant_row_t<QT_Q5_K>(w, row, out); break;
+    case QT_Q6_K: dequant_row_t<QT_Q6_K>(w, row, out); break;
+    default: break;
   }
 }
 

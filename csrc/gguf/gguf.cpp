@@ -143,6 +143,13 @@ GGUFMap::~GGUFMap() {
   if (fd_ >= 0) ::close(fd_);
 }
 
+void GGUFMap::release(const TensorEntry& e) const {
+  const uintptr_t page = (uintptr_t)sysconf(_SC_PAGESIZE);
+  const uintptr_t lo = ((uintptr_t)(base_ + e.offset) + page - 1) / page * page;
+  const uintptr_t hi = (uintptr_t)(base_ + e.offset + e.nbytes) / page * page;
+  if (hi > lo) (void)madvise((void*)lo, hi - lo, MADV_DONTNEED);
+}
+
 const TensorEntry& GGUFMap::get(const std::string& name) const {
   auto it = index_.find(name);
   if (it == index_.end()) throw std::runtime_error("no tensor " + name);

@@ -28,6 +28,10 @@ class GGUFMap {
   const uint8_t* data(const TensorEntry& e) const { return base_ + e.offset; }
   size_t size() const { return size_; }
   uint32_t version() const { return version_; }
+  // drop this process's resident pages of a tensor's bytes (madvise MADV_DONTNEED on the read-only
+  // mapping; a later read faults them back in from the page cache): a loaded model does not keep the
+  // blob resident next to its repacked copy
+  void release(const TensorEntry& e) const;
 
  private:
   int fd_ = -1;

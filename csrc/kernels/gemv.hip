@@ -241,13 +241,33 @@ __device__ __forceinline__ void flight_body(const GemvParams& P, const int bx, c
   // they return only after most of the weight stream (profiles/r1_defer/gemv_timeline.log: prologue
   // p50 4.6-8.3 us on the down projections), so every tile waits on them.
   if (P.xfirst) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // diagnostic (DBG & 16): every block of the grid has its activations before ANY block requests a
+  // weight -- a bounded spin on a grid counter in the timeline buffer (scripts/gemv_timeline.py)
+  if constexpr ((DBG & 16) != 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0 && P.dbg_ts) {
+      unsigned long long* cnt = P.dbg_ts + 4 * 4096;
+      __hip_atomic_fetch_add(cnt, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned long long want = (unsigned long long)gridDim.x * gridDim.z;
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want &&
+             __builtin_amdgcn_s_memrealtime() - t0 < 10000)
+        __builtin_amdgcn_s_sleep(1);
+    }
+    __syncthreads();
+  }
   __builtin_amdgcn_sched_barrier(0);
   // 2. every weight tile of this block in flight (surplus slots re-read the last tile, unused)
   WTile<QT, NSB, R> T[J];
+  if constexpr ((DBG & 8) == 0) {
 #pragma unroll
-  for (int j = 0; j < J; ++j) {
-    const int t = min(vb + j * gv, n_tiles - 1);
-    load_wtile<QT, NSB, R>(w, row_base, t * ROWS_B + rbase, N, SB, sb0, s, T[j], se);
+    for (int j = 0; j < J; ++j) {
+      const int t = min(vb + j * gv, n_tiles - 1);
+      load_wtile<QT, NSB, R>(w, row_base, t * ROWS_B + rbase, N, SB, sb0, s, T[j], se);
+    }
+  } else {  // diagnostic: no weight traffic at all (activation latency alone)
+    for (int j = 0; j < J; ++j) T[j] = WTile<QT, NSB, R>{};
   }
   __builtin_amdgcn_sched_barrier(0);  // every load issued before the prologue's first wait
   if constexpr (MRG > 0) {  // flash-decode merge: splits without keys carry m = -inf, l = 0
@@ -487,6 +507,8 @@ static void launch_flight_n(const GemvParams& P, int gx, hipStream_t s) {
       case 2: hipLaunchKernelGGL((qgemv_flight_kernel<QT, NSB, R, J, NRM, 2>), dim3(gx, 1, bz), dim3(GEMV_NT), lds, s, P); return;
       case 3: hipLaunchKernelGGL((qgemv_flight_kernel<QT, NSB, R, J, NRM, 3>), dim3(gx, 1, bz), dim3(GEMV_NT), lds, s, P); return;
       case 4: hipLaunchKernelGGL((qgemv_flight_kernel<QT, NSB, R, J, NRM, 4>), dim3(gx, 1, bz), dim3(GEMV_NT), lds, s, P); return;
+      case 9: hipLaunchKernelGGL((qgemv_flight_kernel<QT, NSB, R, J, NRM, 9>), dim3(gx, 1, bz), dim3(GEMV_NT), lds, s, P); return;
+      case 16: hipLaunchKernelGGL((qgemv_flight_kernel<QT, NSB, R, J, NRM, 16>), dim3(gx, 1, bz), dim3(GEMV_NT), lds, s, P); return;
       default: break;
     }
   }
@@ -503,6 +525,8 @@ static void launch_flight_ks_n(const GemvParams& P, int gx, hipStream_t s) {
       case 2: hipLaunchKernelGGL((qgemv_flight_kernel<QT, NSB, 1, 1, NRM, 2, KS>), dim3(gx, 1, bz), dim3(GEMV_NT * KS), lds, s, P); return;
       case 3: hipLaunchKernelGGL((qgemv_flight_kernel<QT, NSB, 1, 1, NRM, 3, KS>), dim3(gx, 1, bz), dim3(GEMV_NT * KS), lds, s, P); return;
       case 4: hipLaunchKernelGGL((qgemv_flight_kernel<QT, NSB, 1, 1, NRM, 4, KS>), dim3(gx, 1, bz), dim3(GEMV_NT * KS), lds, s, P); return;
+      case 9: hipLaunchKernelGGL((qgemv_flight_kernel<QT, NSB, 1, 1, NRM, 9, KS>), dim3(gx, 1, bz), dim3(GEMV_NT * KS), lds, s, P); return;
+      case 16: hipLaunchKernelGGL((qgemv_flight_kernel<QT, NSB, 1, 1, NRM, 16, KS>), dim3(gx, 1, bz), dim3(GEMV_NT * KS), lds, s, P); return;
       default: break;
     }
   }

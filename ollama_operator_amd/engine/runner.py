@@ -34,10 +34,12 @@ GEMM_SPLIT_WS_FLOATS = 8 << 20  # 32 MiB of fp32 split-K slabs (prefill GEMMs at
 
 
 class NativeExec:
-    """Adapter: runner buffers -> `_C.Executor`."""
+    """Adapter: runner buffers -> a native executor: `_C.Executor` (gfx950 kernels, GPU runner) or
+    `_cpu.Executor` (the CPU serving backend, csrc/cpu; same call surface)."""
 
-    def __init__(self, runner: "Runner"):
-        C = native()
+    def __init__(self, runner: "Runner", module=None):
+        C = module if module is not None else native()
+        self.on_gpu = module is None
         r = runner
         w, loc, cfg = r.w, r.w.local, r.w.cfg
         self.r = r
@@ -62,7 +64,7 @@ class NativeExec:
                              attn_ws=p(r.attn_ws), attn_cnt=p(r.attn_cnt), x16=p(r.x16), gws=p(r.gws),
                              moe_rows=p(r.moe_rows) if cfg.n_expert else 0, moe_tiles=p(r.moe_tiles),
                              moe_ntiles=p(r.moe_ntiles),
-                             gws_elems=r.gws.numel(), max_B=r.max_batch,
+                             gws_elems=r.gws.numel(), max_B=r.max_batch, ld_logits=r.logits.shape[1],
                              n_splits=1))
         # step buffers bound once: every stage call below passes integers only
         e.set_inputs(dict(tokens=p(r.d_tokens), pos=p(r.d_pos), slot=p(r.d_slot), q_len=p(r.d_qlen),
@@ -81,7 +83,7 @@ class NativeExec:
             prefill: bool = False):
         S, defer = self.r.split_plan(B)
         self.exe.set_splits(S, defer)
-        self.exe.step(self.stages[stage], layer, B, n_logits, use_idx, prefill, stream_handle())
+        self.exe.step(self.stages[stage], layer, B, n_logits, use_idx, prefill, stream_handle() if self.on_gpu else 0)
 
 
 @dataclass
@@ -97,7 +99,10 @@ class Runner:
     def __init__(self, model_path: str, device: str | None = None, max_batch: int = 64, max_seqs: int = 4,
                  ctx: int | None = None, block_size: int = 16, tp_rank: int = 0, tp_size: int = 1,
                  tp_group=None, use_graphs: bool | None = None, weights: DeviceWeights | None = None,
-                 tp_ctrl=None):
+                 tp_ctrl=None, cpu_backend: str | None = None):
+        """cpu_backend (device "cpu" only): "native" = the quantised C++ backend (csrc/cpu, the serving
+        default), "torch" = the fp32 torch twin (test oracle). Default: $OMX_CPU_BACKEND, else native
+        when its module is built."""
         t0 = time.perf_counter()
         if device is None:
             device = f"cuda:{torch.cuda.current_device()}" if torch.cuda.is_available() else "cpu"
@@ -127,9 +132,13 @@ class Runner:
         i32 = dict(device=dev, dtype=torch.int32)
         E, Eq, Fl, Vl = loc["E"], loc["H"] * loc["D"], loc["F"], loc["V"]
         ksel = max(1, cfg.n_expert_used)
-        self.kc = [torch.zeros(n_blocks, loc["Hkv"], block_size, loc["D"], device=dev, dtype=torch.float16)
+        # CPU: the cache stays untouched (and out of RSS) until blocks are written -- every slot is
+        # written by its QKV step before any attention reads it
+        kv_alloc = torch.zeros if self.is_gpu else torch.empty
+        self.kc = [kv_alloc(n_blocks, loc["Hkv"], block_size, loc["D"], device=dev, dtype=torch.float16)
                    for _ in range(cfg.n_layer)]
-        self.vc = [torch.zeros_like(k) for k in self.kc]
+        self.vc = [kv_alloc(n_blocks, loc["Hkv"], block_size, loc["D"], device=dev, dtype=torch.float16)
+                   for _ in range(cfg.n_layer)]
         self.resid = torch.zeros(max_batch, E, **f32)
         self.qbuf = torch.zeros(max_batch, Eq, **f32)
         self.abuf = torch.zeros(max_batch, Eq, **f32)
@@ -190,7 +199,19 @@ class Runner:
             from ..parallel.custom_ar import CustomAllReduce
             rows = max(1, min(max_batch, max(max_seqs, 16), (1 << 18) // max(E, Vl)))
             self.ar = CustomAllReduce(tp_group, tp_rank, tp_size, rows * max(E, Vl))
-        self.exe = NativeExec(self) if self.is_gpu else TorchExecutor(self)
+        if self.is_gpu:
+            self.exe = NativeExec(self)
+        else:
+            from ..ops.cpu import cpu_module
+            choice = cpu_backend or os.environ.get("OMX_CPU_BACKEND") or ("native" if cpu_module() else "torch")
+            if choice == "native":
+                mod = cpu_module()
+                if mod is None:
+                    raise RuntimeError("CPU backend ollama_operator_amd._cpu is not built (python build_native.py)")
+                self.exe = NativeExec(self, mod)
+            else:
+                self.exe = TorchExecutor(self)
+        self.cpu_backend = None if self.is_gpu else ("native" if isinstance(self.exe, NativeExec) else "torch")
         if use_graphs is None:  # TP: graph-captured only through the custom all-reduce
             use_graphs = (self.is_gpu and (tp_size == 1 or self.ar is not None) and
                           os.environ.get("OMX_NO_GRAPH", "0") != "1")

@@ -74,6 +74,19 @@ def apply_penalties(logits: np.ndarray, history: list[int], o: SamplingOptions) 
             logits[t] = v
 
 
+def top_k_stable(lg: np.ndarray, k: int) -> np.ndarray:
+    """The first k of a stable descending argsort (ties by lower index), in O(V): partition, then
+    sort only the candidates (the CPU backend samples 51,200-entry Phi-2 logits per token)."""
+    if k >= lg.shape[0]:
+        return np.argsort(-lg, kind="stable")[:k]
+    part = np.argpartition(-lg, k - 1)[:k]
+    vk = lg[part].min()
+    greater = np.nonzero(lg > vk)[0]
+    equal = np.nonzero(lg == vk)[0][:k - len(greater)]
+    cand = np.concatenate([greater, equal])
+    return cand[np.lexsort((cand, -lg[cand]))]
+
+
 def sample_host(logits: np.ndarray, history: list[int], o: SamplingOptions, seed: int, step: int) -> int:
     lg = np.array(logits, dtype=np.float32, copy=True)
     apply_penalties(lg, history, o)
@@ -81,7 +94,7 @@ def sample_host(logits: np.ndarray, history: list[int], o: SamplingOptions, seed
         return int(np.argmax(lg))
     k = o.top_k if 0 < o.top_k <= 1024 else 1024
     k = min(k, lg.shape[0])
-    idx = np.argsort(-lg, kind="stable")[:k]
+    idx = top_k_stable(lg, k)
     vals = lg[idx].astype(np.float64)
     top = vals[0]
     p1 = np.exp(vals - top)

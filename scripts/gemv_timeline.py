@@ -37,7 +37,7 @@ def main():
         nw = torch.ones(K, device="cuda")
         y = torch.zeros(1, N // 2 if epi == 2 else N, device="cuda")
         norm = 1 if name in ("qkv", "gate_up") else 0
-        stamps = torch.zeros(4 * 4096, dtype=torch.int64, device="cuda")
+        stamps = torch.zeros(4 * 4096 + 64, dtype=torch.int64, device="cuda")  # + grid counter (DBG 16)
         res = []
         for rep in range(6):
             stamps.zero_()
@@ -47,7 +47,7 @@ def main():
             C.gemv(b, 1, x.data_ptr(), K, norm, nw.data_ptr(), 0, 1e-5, epi, y.data_ptr(), y.shape[1], 0, 0,
                    {"dbg_ts": stamps.data_ptr()}, s)
             torch.cuda.synchronize()
-            t = stamps.view(-1, 4).cpu().numpy()
+            t = stamps[:4 * 4096].view(-1, 4).cpu().numpy()
             t = t[t[:, 0] > 0].astype(np.float64)
             t0 = t[:, 0].min()
             t = t - t0

@@ -45,3 +45,8 @@ def tiny_models(tmp_path_factory):
         write_random_gguf(p, preset(base), ft, seed=zlib.crc32(name.encode()) % 1000, quantize_from_float=True)
         out[name] = p
     return out
+
+# CPU runners in the test suite default to the fp32 torch twin (the numerical oracle the GPU engine
+# is checked against); the native CPU backend has its own tests (tests/test_cpu_backend.py), which
+# ask for it explicitly.
+os.environ.setdefault("OMX_CPU_BACKEND", "torch")
