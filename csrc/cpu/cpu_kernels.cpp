@@ -79,8 +79,16 @@ struct USB {
   int sc[16];     // K-quants: integer scale per 32 (Q4_K/Q5_K: 8 used) or per 16 (Q6_K)
   int mn[8];      // Q4_K/Q5_K mins
   float d, dmin;  // super-block scales
-  float bd[8];    // Q4_0/Q8_0 per-32 block scales
+  __m256 bdv;     // Q4_0/Q8_0 per-32 block scales
 };
+
+// [sum of the 8 lanes of p[0]], ..., [sum of p[7]] -> one vector (block order)
+static inline __m256i hsum8(const __m256i* p) {
+  const __m256i t0 = _mm256_hadd_epi32(p[0], p[1]), t1 = _mm256_hadd_epi32(p[2], p[3]);
+  const __m256i t2 = _mm256_hadd_epi32(p[4], p[5]), t3 = _mm256_hadd_epi32(p[6], p[7]);
+  const __m256i u0 = _mm256_hadd_epi32(t0, t1), u1 = _mm256_hadd_epi32(t2, t3);
+  return _mm256_add_epi32(_mm256_permute2x128_si256(u0, u1, 0x20), _mm256_permute2x128_si256(u0, u1, 0x31));
+}
 
 static inline __m256i load2(const uint8_t* a, const uint8_t* b) {
   return _mm256_inserti128_si256(_mm256_castsi128_si256(_mm_loadu_si128((const __m128i*)a)),
@@ -174,27 +182,20 @@ static inline __attribute__((always_inline)) void unpack(const QMat& w, long lon
     }
     case QT_Q4_0: {
       const uint8_t* qs = w.s[0] + row * SB * 128;
-      const uint8_t* dd = w.s[1] + row * SB * 16 + 16 * sb;
-      for (int t = 0; t < 8; ++t) {
-        uint16_t h;
-        memcpy(&h, dd + 2 * t, 2);
-        u.bd[t] = h2f(h);
-        const __m128i p = _mm_xor_si128(_mm_loadu_si128((const __m128i*)(qs + (t * SB + sb) * 16)), _mm_set1_epi8((char)0x80));
-        const __m128i lo = _mm_and_si128(p, _mm_set1_epi8(0x0F));
-        const __m128i hi = _mm_and_si128(_mm_srli_epi16(p, 4), _mm_set1_epi8(0x0F));
-        u.c[t] = _mm256_inserti128_si256(_mm256_castsi128_si256(lo), hi, 1);
+      // 8 fp16 block scales in one conversion
+      u.bdv = _mm256_cvtph_ps(_mm_loadu_si128((const __m128i*)(w.s[1] + row * SB * 16 + 16 * sb)));
+      for (int t = 0; t < 8; t += 2) {  // blocks t, t+1 per 256-bit op: [lo_t | lo_t1], [hi_t | hi_t1]
+        const __m256i p = _mm256_xor_si256(load2(qs + (t * SB + sb) * 16, qs + ((t + 1) * SB + sb) * 16), x80);
+        const __m256i lo = _mm256_and_si256(p, m4), hi = _mm256_and_si256(_mm256_srli_epi16(p, 4), m4);
+        u.c[t] = _mm256_permute2x128_si256(lo, hi, 0x20);      // block t natural order
+        u.c[t + 1] = _mm256_permute2x128_si256(lo, hi, 0x31);  // block t + 1
       }
       break;
     }
     case QT_Q8_0: {
       const uint8_t* qs = w.s[0] + row * SB * 256;
-      const uint8_t* dd = w.s[1] + row * SB * 16 + 16 * sb;
-      for (int t = 0; t < 8; ++t) {
-        uint16_t h;
-        memcpy(&h, dd + 2 * t, 2);
-        u.bd[t] = h2f(h);
-        u.c[t] = _mm256_loadu_si256((const __m256i*)(qs + (t * SB + sb) * 32));
-      }
+      u.bdv = _mm256_cvtph_ps(_mm_loadu_si128((const __m128i*)(w.s[1] + row * SB * 16 + 16 * sb)));
+      for (int t = 0; t < 8; ++t) u.c[t] = _mm256_loadu_si256((const __m256i*)(qs + (t * SB + sb) * 32));
       break;
     }
     default: break;
@@ -241,32 +242,32 @@ static inline __attribute__((always_inline)) float dot_sb(const USB& u, const in
       for (int g = 0; g < 16; ++g) off += u.sc[g] * bs[g];
       return dx * u.d * (float)(hsum_i32(acc) - 32 * off);
     }
-    case QT_Q4_0: {
-      const __m256i ones = _mm256_set1_epi16(1);
-      __m256 acc = _mm256_setzero_ps();
-      float off = 0.f;
-      for (int t = 0; t < 8; ++t) {
-        const __m256i x = _mm256_loadu_si256((const __m256i*)(xq + 32 * t));
-        const __m256 p = _mm256_cvtepi32_ps(_mm256_madd_epi16(_mm256_maddubs_epi16(u.c[t], x), ones));
-        acc = _mm256_fmadd_ps(p, _mm256_set1_ps(u.bd[t]), acc);
-        off += u.bd[t] * (float)(bs[2 * t] + bs[2 * t + 1]);
-      }
-      return dx * (hsum_f32(acc) - 8.f * off);
-    }
-    case QT_Q8_0: {
-      const __m256i ones = _mm256_set1_epi16(1);
-      __m256 acc = _mm256_setzero_ps();
-      for (int t = 0; t < 8; ++t) {
-        const __m256i x = _mm256_loadu_si256((const __m256i*)(xq + 32 * t));
-        const __m256i aw = _mm256_sign_epi8(u.c[t], u.c[t]);  // |w| (u8), sign moved onto x
-        const __m256i sx = _mm256_sign_epi8(x, u.c[t]);
-        const __m256 p = _mm256_cvtepi32_ps(_mm256_madd_epi16(_mm256_maddubs_epi16(aw, sx), ones));
-        acc = _mm256_fmadd_ps(p, _mm256_set1_ps(u.bd[t]), acc);
-      }
-      return dx * hsum_f32(acc);
-    }
     default: return 0.f;
   }
+}
+
+// Q4_0 / Q8_0: per-block contributions of one SB as a vector (reduced once per row):
+// dx * d_t * (sum_i q_i x_i - 8 * sum_i x_i) for the 8 blocks t
+template <int QT>
+static inline __attribute__((always_inline)) __m256 dot_blocks(const USB& u, const int8_t* xq, float dx,
+                                                               const int16_t* bs) {
+  const __m256i ones = _mm256_set1_epi16(1);
+  __m256i p[8];
+  for (int t = 0; t < 8; ++t) {
+    const __m256i x = _mm256_loadu_si256((const __m256i*)(xq + 32 * t));
+    if constexpr (QT == QT_Q8_0) {
+      const __m256i aw = _mm256_sign_epi8(u.c[t], u.c[t]);  // |w| (u8), the sign moves onto x
+      p[t] = _mm256_madd_epi16(_mm256_maddubs_epi16(aw, _mm256_sign_epi8(x, u.c[t])), ones);
+    } else {
+      p[t] = _mm256_madd_epi16(_mm256_maddubs_epi16(u.c[t], x), ones);
+    }
+  }
+  __m256 v = _mm256_cvtepi32_ps(hsum8(p));
+  if constexpr (QT == QT_Q4_0) {  // zero point 8: subtract 8 * (sum of the block's activations)
+    const __m256i bs32 = _mm256_madd_epi16(_mm256_loadu_si256((const __m256i*)bs), ones);  // pairs of 16
+    v = _mm256_fnmadd_ps(_mm256_set1_ps(8.f), _mm256_cvtepi32_ps(bs32), v);
+  }
+  return _mm256_mul_ps(v, _mm256_mul_ps(u.bdv, _mm256_set1_ps(dx)));
 }
 
 // streams of the next super-block a row step reads (prefetched ahead of the unpack)
@@ -286,25 +287,38 @@ template <int QT>
 static void gemm_t(const QMat& w, long long row_base, int N, const QAct& a, float* y, int ldy, bool accumulate) {
   const int SB = a.SB, B = a.B;
   // rows in contiguous slices: each thread streams its own part of the matrix
+  constexpr bool BLK = QT == QT_Q4_0 || QT == QT_Q8_0;  // fp32 per-block scales: vector accumulators
 #pragma omp parallel
   {
-    float accs[64];
-    std::vector<float> accv(B > 64 ? B : 0);
-    float* acc = B > 64 ? accv.data() : accs;
+    // per-thread accumulators on the thread's own stack (small heap blocks of different threads
+    // share cache lines: written every super-block, that false sharing cost 4x at 8 threads)
+    alignas(64) float acc_s[64];
+    alignas(64) __m256 vacc_s[64];
+    std::vector<float> accv(B > 64 ? B + 16 : 0);
+    std::vector<__m256> vaccv(BLK && B > 64 ? B + 2 : 0);
+    float* acc = B > 64 ? accv.data() : acc_s;
+    __m256* vacc = B > 64 ? vaccv.data() : vacc_s;
 #pragma omp for schedule(static)
     for (int n = 0; n < N; ++n) {
       const long long row = row_base + n;
-      for (int b = 0; b < B; ++b) acc[b] = 0.f;
+      for (int b = 0; b < B; ++b) {
+        acc[b] = 0.f;
+        if constexpr (BLK) vacc[b] = _mm256_setzero_ps();
+      }
       for (int sb = 0; sb < SB; ++sb) {
         prefetch_sb<QT>(w, row, sb + 2, SB);
         USB u;
         unpack<QT>(w, row, sb, SB, u);
         for (int b = 0; b < B; ++b) {
           const size_t i = (size_t)b * SB + sb;
-          acc[b] += dot_sb<QT>(u, a.q.data() + i * 256, a.d[i], a.bsum.data() + i * 16);
+          if constexpr (BLK)
+            vacc[b] = _mm256_add_ps(vacc[b], dot_blocks<QT>(u, a.q.data() + i * 256, a.d[i], a.bsum.data() + i * 16));
+          else
+            acc[b] += dot_sb<QT>(u, a.q.data() + i * 256, a.d[i], a.bsum.data() + i * 16);
         }
       }
       for (int b = 0; b < B; ++b) {
+        if constexpr (BLK) acc[b] = hsum_f32(vacc[b]);
         float* o = y + (long long)b * ldy + n;
         *o = accumulate ? *o + acc[b] : acc[b];
       }
@@ -334,6 +348,8 @@ static void dequant_row_t(const QMat& w, long long row, float* out) {
     unpack<QT>(w, row, sb, SB, u);
     alignas(32) uint8_t c[256];
     for (int r = 0; r < 8; ++r) _mm256_store_si256((__m256i*)(c + 32 * r), u.c[r]);
+    alignas(32) float bd[8];
+    if constexpr (QT == QT_Q4_0 || QT == QT_Q8_0) _mm256_store_ps(bd, u.bdv);
     const int n = w.K - sb * 256 < 256 ? w.K - sb * 256 : 256;
     float* o = out + sb * 256;
     for (int j = 0; j < n; ++j) {
@@ -342,8 +358,8 @@ static void dequant_row_t(const QMat& w, long long row, float* out) {
         case QT_Q4_K:
         case QT_Q5_K: o[j] = u.d * u.sc[s] * c[j] - u.dmin * u.mn[s]; break;
         case QT_Q6_K: o[j] = u.d * u.sc[j / 16] * ((int)c[j] - 32); break;
-        case QT_Q4_0: o[j] = u.bd[s] * ((int)c[j] - 8); break;
-        case QT_Q8_0: o[j] = u.bd[s] * (int8_t)c[j]; break;
+        case QT_Q4_0: o[j] = bd[s] * ((int)c[j] - 8); break;
+        case QT_Q8_0: o[j] = bd[s] * (int8_t)c[j]; break;
         default: o[j] = 0.f;
       }
     }
