@@ -34,8 +34,11 @@ namespace omx {
 
 
 GemvTuning g_tune;
-void set_gemv_tuning(int blocks_per_cu, int rows, int debug, int ks, int xfirst, int xbar) {
+void set_gemv_tuning(int blocks_per_cu, int rows, int debug, int ks, int xfirst, int xbar, int stream,
+                     int stream_bpc) {
   g_tune.debug = debug > 0 ? debug : 0;
+  if (stream == 0 || stream == 1) g_tune.stream = stream;
+  if (stream_bpc >= 1 && stream_bpc <= 4) g_tune.stream_bpc = stream_bpc;
   if (xfirst == 0 || xfirst == 1) g_tune.xfirst = xfirst;
   if (xbar == 0 || xbar == 1) g_tune.xbar = xbar;
   if (ks >= 0 && ks <= 4) g_tune.ks = ks;
@@ -705,12 +708,14 @@ static void launch_nsb(const GemvParams& P, hipStream_t s) {
 template <int QT>
 static void launch_q(const GemvParams& P, hipStream_t s) {
   if (P.merge_S > 0) {  // only the single-chunk B == 1 flight kernel merges (merge_supported())
+    if (gemv_stream(P, s)) return;
     if (launch_flight_xb<QT>(P, 1, s)) return;
     launch_flight<QT, 1, 1>(P, s);
     return;
   }
   if (P.B == 1 || P.expert_ids != nullptr) {  // decode (and MoE: experts differ per batch row)
     const int need = ((P.w.K + 255) / 256 + 15) / 16;
+    if (P.B == 1 && gemv_stream(P, s)) return;  // bounded-depth streaming kernel (gemv_stream.hip)
     if (P.B == 1 && need <= 4) {  // whole K in one chunk: all-in-flight kernel
       if (g_tune.rows == 2 && need == 1) { launch_flight<QT, 1, 2>(P, s); return; }
       if (launch_flight_split<QT>(P, need, s)) return;
@@ -806,6 +811,7 @@ void gemv2(const GemvParams& A0, const GemvParams& B0, hipStream_t s) {
   const bool ok = A.B == 1 && Bp.B == 1 && A.w.K == Bp.w.K && need <= 2 && A.norm == NORM_RMS &&
                   Bp.norm == NORM_RMS && !A.expert_ids && !Bp.expert_ids && !A.merge_S && !Bp.merge_S &&
                   A.x == Bp.x && g_tune.debug == 0;
+  if (ok && gemv_stream2(A, Bp, s)) return;
   if (ok) {
     bool done = false;
     switch (eff_qtype(A)) {

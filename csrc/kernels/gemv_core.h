@@ -446,5 +446,8 @@ __device__ __forceinline__ void finish_rows(const GemvParams& P, float (&acc)[R]
 
 // small-batch decode (gemv_batch.hip): false = shape not covered, caller falls back
 bool gemv_batch(const GemvParams& P, hipStream_t s);
+// bounded-depth streaming batch-1 decode GEMV (gemv_stream.hip): false = not covered
+bool gemv_stream(const GemvParams& P, hipStream_t s);
+bool gemv_stream2(const GemvParams& A, const GemvParams& B, hipStream_t s);
 
 }  // namespace omx

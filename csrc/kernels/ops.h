@@ -82,10 +82,13 @@ struct GemvTuning {
   int debug = 0;          // microbenchmark-only kernel variants (gemv.hip DBG)
   int ks = 0;             // in-block K split of the flight kernel: 0 = auto, 1 = off, 2..4 = forced
   int xfirst = 0;         // 1: decode GEMVs wait for their activations before streaming weights
-  int xbar = 1;           // 1: batch-1 decode GEMVs as x-barrier launches, one block per CU (gemv.hip XB)
+  int xbar = 0;           // 1: batch-1 decode GEMVs as x-barrier launches, one block per CU (gemv.hip XB)
+  int stream = 1;         // 1: batch-1 decode GEMVs on the bounded-depth streaming kernel (gemv_stream.hip)
+  int stream_bpc = 1;     // its blocks per CU
 };
 extern GemvTuning g_tune;
-void set_gemv_tuning(int blocks_per_cu, int rows, int debug, int ks = -1, int xfirst = -1, int xbar = -1);
+void set_gemv_tuning(int blocks_per_cu, int rows, int debug, int ks = -1, int xfirst = -1, int xbar = -1,
+                     int stream = -1, int stream_bpc = -1);
 
 // Dequantize rows of a repacked matrix (embedding gather / fp16 copies)
 void embed_rows(const QMat& w, const int* rows, int n, float* out, int ldo, hipStream_t s);

@@ -114,6 +114,10 @@ class Runner:
                 native().set_gemv_tuning(xfirst=int(os.environ["OMX_GEMV_XFIRST"]))
             if os.environ.get("OMX_GEMV_XBAR") in ("0", "1"):  # x-barrier one-block-per-CU decode GEMVs
                 native().set_gemv_tuning(xbar=int(os.environ["OMX_GEMV_XBAR"]))
+            if os.environ.get("OMX_GEMV_STREAM") in ("0", "1"):  # bounded-depth streaming decode GEMV
+                native().set_gemv_tuning(stream=int(os.environ["OMX_GEMV_STREAM"]))
+            if os.environ.get("OMX_GEMV_STREAM_BPC"):
+                native().set_gemv_tuning(stream_bpc=int(os.environ["OMX_GEMV_STREAM_BPC"]))
         self.tp_rank, self.tp_size, self.tp_group = tp_rank, tp_size, tp_group
         self._closed = False
         # TP serving (parallel/tp.py): rank 0 signals each decode step, followers mirror it
