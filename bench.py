@@ -35,7 +35,8 @@ sys.path.insert(0, ROOT)
 
 
 MODEL_LABELS = {"llama2-7b": "Llama-2-7B", "llama2-13b": "Llama-2-13B", "llama2-70b": "Llama-2-70B",
-                "mistral-7b": "Mistral-7B", "mixtral-8x7b": "Mixtral-8x7B", "phi2": "Phi-2"}
+                "mistral-7b": "Mistral-7B", "mixtral-8x7b": "Mixtral-8x7B", "phi2": "Phi-2",
+                "gemma-2b": "Gemma-2B", "gemma-7b": "Gemma-7B"}
 
 
 def ensure_model(path: str, preset_name: str, ftype_name: str) -> str:

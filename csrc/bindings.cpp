@@ -45,7 +45,7 @@ static QMat qmat(py::object o) {
 static void check_attn(int H, int n_kv, int D) {
   if (n_kv <= 0 || H % n_kv) throw std::runtime_error("H must be a multiple of n_kv");
   // any group size: decode blocks take a divisor of G in {1, 2, 4, 8} (attention.hip heads_per_block)
-  if (D != 64 && D != 80 && D != 96 && D != 128) throw std::runtime_error("unsupported head dim");
+  if (D != 64 && D != 80 && D != 96 && D != 128 && D != 256) throw std::runtime_error("unsupported head dim");
 }
 
 static ARParams ar_params(py::dict d) {
@@ -339,6 +339,8 @@ PYBIND11_MODULE(_C, m) {
         k.n_expert_used = c["n_expert_used"].cast<int>();
         k.window = c["window"].cast<int>();
         k.tp = c["tp"].cast<int>();
+        k.embed_scale = c.contains("embed_scale") ? c["embed_scale"].cast<float>() : 1.f;
+        k.glu_act = c.contains("glu_act") ? c["glu_act"].cast<int>() : 0;
         check_attn(k.H, k.Hkv, k.D);
         e.layers.assign(k.n_layer, LayerW{});
       })
@@ -508,6 +510,7 @@ PYBIND11_MODULE(_C, m) {
   m.attr("EPI_STORE") = (int)EPI_STORE;
   m.attr("EPI_ADD") = (int)EPI_ADD;
   m.attr("EPI_GLU") = (int)EPI_GLU;
+  m.attr("EPI_GEGLU") = (int)EPI_GEGLU;
   m.attr("EPI_GELU") = (int)EPI_GELU;
   m.attr("EPI_QKV") = (int)EPI_QKV;
 }

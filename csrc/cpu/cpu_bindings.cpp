@@ -74,6 +74,8 @@ PYBIND11_MODULE(_cpu, m) {
         k.n_expert_used = c["n_expert_used"].cast<int>();
         k.window = c["window"].cast<int>();
         k.tp = c["tp"].cast<int>();
+        k.embed_scale = c.contains("embed_scale") ? c["embed_scale"].cast<float>() : 1.f;
+        k.glu_act = c.contains("glu_act") ? c["glu_act"].cast<int>() : 0;
         if (k.H <= 0 || k.Hkv <= 0 || k.H % k.Hkv || k.D <= 0 || k.n_rot > k.D) throw std::runtime_error("bad heads");
         e.layers.assign(k.n_layer, Layer{});
       })

@@ -48,7 +48,12 @@ float* Engine::dst(int B) { return cfg.tp > 1 ? buf.ypart : buf.resid; }
 
 void Engine::embed(int B) {
 #pragma omp parallel for schedule(static) if (B > 1)
-  for (int b = 0; b < B; ++b) dequant_row(tok_embd, buf.tokens[b], buf.resid + (long long)b * cfg.E);
+  for (int b = 0; b < B; ++b) {
+    float* r = buf.resid + (long long)b * cfg.E;
+    dequant_row(tok_embd, buf.tokens[b], r);
+    if (cfg.embed_scale != 1.f)
+      for (int j = 0; j < cfg.E; ++j) r[j] *= cfg.embed_scale;
+  }
 }
 
 void Engine::attn(int i, int B) {
@@ -194,7 +199,9 @@ void Engine::ffn(int i, int B) {
 #pragma omp parallel for schedule(static)
   for (int b = 0; b < B; ++b)
     for (int f = 0; f < F; ++f)
-      buf.hbuf[(long long)b * F + f] = silu(gu_[(long long)b * 2 * F + 2 * f]) * gu_[(long long)b * 2 * F + 2 * f + 1];
+      buf.hbuf[(long long)b * F + f] = (cfg.glu_act ? gelu(gu_[(long long)b * 2 * F + 2 * f])
+                                                   : silu(gu_[(long long)b * 2 * F + 2 * f])) *
+                                       gu_[(long long)b * 2 * F + 2 * f + 1];
   gemm(L.wdown, 0, E, buf.hbuf, F, B, y, E, add);
 }
 

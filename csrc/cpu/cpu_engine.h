@@ -29,6 +29,8 @@ struct Config {
   int E = 0, H = 0, Hkv = 0, D = 0, n_rot = 0, F = 0, n_layer = 0, V = 0;
   float eps = 1e-5f;
   int n_expert = 0, n_expert_used = 0, window = 0, tp = 1;
+  float embed_scale = 1.f;  // Gemma: sqrt(E)
+  int glu_act = 0;          // 0 SiLU-GLU, 1 GELU-GLU (Gemma)
 };
 
 struct Layer {

@@ -59,6 +59,13 @@ __device__ __forceinline__ void load_krow(const f16* p, KRow<DPL>& r) {
     const f16x8 t = __builtin_nontemporal_load((const f16x8*)p);
 #pragma unroll
     for (int j = 0; j < 8; ++j) r.v[j] = t[j];
+  } else if constexpr (DPL == 16) {  // head dim 256 (Gemma)
+    const f16x8 t0 = __builtin_nontemporal_load((const f16x8*)p), t1 = __builtin_nontemporal_load((const f16x8*)p + 1);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      r.v[j] = t0[j];
+      r.v[8 + j] = t1[j];
+    }
   } else if constexpr (DPL == 4) {
     const f16x4 t = *(const f16x4*)p;
 #pragma unroll
@@ -482,6 +489,7 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(AttnParams P) {
 static int heads_per_block(const AttnParams& P) {
   const int G = P.H / P.n_kv;
   int hpb = g_attn_hpb > 0 ? g_attn_hpb : (P.NQ * P.n_kv < 64 ? 1 : G);
+  if (P.D > 128 && hpb > 2) hpb = 2;  // head dim 256: the per-wave merge tile [8][G][D + 2] fits LDS for G <= 2
   while (hpb > 1 && (G % hpb || (hpb != 1 && hpb != 2 && hpb != 4 && hpb != 8))) --hpb;
   return hpb < 1 ? 1 : hpb;
 }
@@ -493,8 +501,8 @@ static void launch_d(const AttnParams& P, hipStream_t s) {
   switch (G) {
     case 1: hipLaunchKernelGGL((attn_decode_kernel<D, 1>), grid, dim3(ATT_NT), 0, s, P); break;
     case 2: hipLaunchKernelGGL((attn_decode_kernel<D, 2>), grid, dim3(ATT_NT), 0, s, P); break;
-    case 4: hipLaunchKernelGGL((attn_decode_kernel<D, 4>), grid, dim3(ATT_NT), 0, s, P); break;
-    case 8: hipLaunchKernelGGL((attn_decode_kernel<D, 8>), grid, dim3(ATT_NT), 0, s, P); break;
+    case 4: if constexpr (D <= 128) hipLaunchKernelGGL((attn_decode_kernel<D, 4>), grid, dim3(ATT_NT), 0, s, P); break;
+    case 8: if constexpr (D <= 128) hipLaunchKernelGGL((attn_decode_kernel<D, 8>), grid, dim3(ATT_NT), 0, s, P); break;
     default: break;
   }
 }
@@ -518,6 +526,7 @@ void attention_decode(const AttnParams& P0, hipStream_t s) {
     case 80: launch_d<80>(P, s); break;
     case 96: launch_d<96>(P, s); break;
     case 128: launch_d<128>(P, s); break;
+    case 256: launch_d<256>(P, s); break;  // Gemma (prefill too: the MFMA flash kernel covers D <= 128)
     default: break;
   }
 }

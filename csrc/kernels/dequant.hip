@@ -6,7 +6,7 @@
 namespace omx {
 
 // one block per gathered row; each thread dequantises 32-weight pieces
-__global__ __launch_bounds__(256) void embed_rows_kernel(QMat w, const int* rows, float* out, int ldo) {
+__global__ __launch_bounds__(256) void embed_rows_kernel(QMat w, const int* rows, float* out, int ldo, float scale) {
   const int b = blockIdx.x;
   const long long row = rows[b];
   const int P = w.K / 32;
@@ -17,15 +17,17 @@ __global__ __launch_bounds__(256) void embed_rows_kernel(QMat w, const int* rows
     dequant_piece(w, row, p, lo, hi, olo, ohi);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      *(f32x4*)(o + olo + 4 * j) = (f32x4){lo[4 * j], lo[4 * j + 1], lo[4 * j + 2], lo[4 * j + 3]};
-      *(f32x4*)(o + ohi + 4 * j) = (f32x4){hi[4 * j], hi[4 * j + 1], hi[4 * j + 2], hi[4 * j + 3]};
+      *(f32x4*)(o + olo + 4 * j) =
+          (f32x4){lo[4 * j], lo[4 * j + 1], lo[4 * j + 2], lo[4 * j + 3]} * scale;
+      *(f32x4*)(o + ohi + 4 * j) =
+          (f32x4){hi[4 * j], hi[4 * j + 1], hi[4 * j + 2], hi[4 * j + 3]} * scale;
     }
   }
 }
 
-void embed_rows(const QMat& w, const int* rows, int n, float* out, int ldo, hipStream_t s) {
+void embed_rows(const QMat& w, const int* rows, int n, float* out, int ldo, hipStream_t s, float scale) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(embed_rows_kernel, dim3(n), dim3(256), 0, s, w, rows, out, ldo);
+  hipLaunchKernelGGL(embed_rows_kernel, dim3(n), dim3(256), 0, s, w, rows, out, ldo, scale);
 }
 
 // grid-stride over (row, piece)

@@ -30,6 +30,10 @@ __device__ __forceinline__ void epi_apply(const GemvParams& P, int bb, int vn, f
       if ((vn & 1) == 0)  // even row = gate, odd row = up
         P.y[(long long)bb * P.ldy + (long long)zsel * P.y_sel_stride + vn / 2] = silu(v) * pv;
       break;
+    case EPI_GEGLU:  // Gemma: gelu(gate) * up
+      if ((vn & 1) == 0)
+        P.y[(long long)bb * P.ldy + (long long)zsel * P.y_sel_stride + vn / 2] = gelu_tanh(v) * pv;
+      break;
     case EPI_QKV: {
       const int Eq = P.Eq, Ekv = P.Ekv, D = P.D;
       int which, hh, d;

@@ -10,7 +10,7 @@
 namespace omx {
 
 enum { NORM_NONE = 0, NORM_RMS = 1, NORM_LAYER = 2 };
-enum { EPI_STORE = 0, EPI_ADD = 1, EPI_GLU = 2, EPI_GELU = 3, EPI_QKV = 4 };
+enum { EPI_STORE = 0, EPI_ADD = 1, EPI_GLU = 2, EPI_GELU = 3, EPI_QKV = 4, EPI_GEGLU = 5 };
 
 struct GemvParams {
   QMat w;
@@ -91,7 +91,7 @@ void set_gemv_tuning(int blocks_per_cu, int rows, int debug, int ks = -1, int xf
                      int stream = -1, int stream_bpc = -1);
 
 // Dequantize rows of a repacked matrix (embedding gather / fp16 copies)
-void embed_rows(const QMat& w, const int* rows, int n, float* out, int ldo, hipStream_t s);
+void embed_rows(const QMat& w, const int* rows, int n, float* out, int ldo, hipStream_t s, float scale = 1.f);
 void dequant_f16(const QMat& w, void* out_f16, hipStream_t s);
 
 struct AttnParams {

@@ -20,7 +20,7 @@ static GemvParams base_params(const QMat& w, int B, const float* x, int ldx, con
 }
 
 void Executor::embed(const StepInputs& in, hipStream_t s) {
-  embed_rows(tok_embd, in.tokens, in.B, ws.resid, cfg.E, s);
+  embed_rows(tok_embd, in.tokens, in.B, ws.resid, cfg.E, s, cfg.embed_scale);
 }
 
 void Executor::attn_block(int i, const StepInputs& in, hipStream_t s) {
@@ -203,7 +203,7 @@ void Executor::ffn_block(int i, const StepInputs& in, hipStream_t s) {
   G.norm = NORM_RMS;
   G.norm_w = L.ffn_norm;
   G.eps = cfg.eps;
-  G.epi = EPI_GLU;
+  G.epi = cfg.glu_act ? EPI_GEGLU : EPI_GLU;
   G.y = ws.hbuf;
   G.ldy = F;
   gemv(G, s);

@@ -19,6 +19,8 @@ struct ExecConfig {
   int n_expert = 0, n_expert_used = 0;
   int window = 0;
   int tp = 1;            // >1: O/down projections write partial sums to ypart (caller all-reduces)
+  float embed_scale = 1.f;  // token embeddings x this (Gemma: sqrt(E))
+  int glu_act = 0;          // 0 SiLU-GLU, 1 GELU-GLU (Gemma GeGLU)
 };
 
 struct LayerW {

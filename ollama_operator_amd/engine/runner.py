@@ -47,7 +47,7 @@ class NativeExec:
         e.configure(dict(arch=1 if cfg.arch == "phi2" else 0, E=loc["E"], H=loc["H"], Hkv=loc["Hkv"], D=loc["D"],
                          n_rot=cfg.n_rot, F=loc["F"], n_layer=cfg.n_layer, V=loc["V"], eps=float(cfg.norm_eps),
                          n_expert=cfg.n_expert, n_expert_used=cfg.n_expert_used, window=cfg.sliding_window,
-                         tp=r.tp_size))
+                         tp=r.tp_size, embed_scale=float(cfg.embed_scale), glu_act=int(cfg.gelu_glu)))
         p = lambda t: t.data_ptr() if t is not None else 0  # noqa: E731
         e.set_globals(w.tok_embd.tup, p(w.out_norm), p(w.out_norm_b), w.lm_head.tup, p(w.lm_bias), p(w.inv_freq))
         for i, L in enumerate(w.layers):

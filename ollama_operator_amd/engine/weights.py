@@ -263,8 +263,9 @@ class DeviceWeights:
                     L["wv"] = build_qmat(src, [(nv, rv, ar(Ekv))], Ekv, E, None, dev, widen=True)
                 L["attn_norm"] = t(src.f32(b + "attn_norm.weight"))
                 L["ffn_norm"] = t(src.f32(b + "ffn_norm.weight"))
-                L["wo"] = build_qmat(src, [(b + "attn_output.weight", ar(E), ar(E))], E, E,
-                                     kblocks(E, b + "attn_output.weight"), dev, widen=True)
+                Eq_full = cfg.n_embd_q  # O projection K = H * head_dim (Gemma: != E)
+                L["wo"] = build_qmat(src, [(b + "attn_output.weight", ar(E), ar(E))], E, Eq_full,
+                                     kblocks(Eq_full, b + "attn_output.weight"), dev, widen=True)
                 if cfg.n_expert:
                     X = cfg.n_expert
                     L["router"] = build_qmat(src, [(b + "ffn_gate_inp.weight", ar(X), ar(X))], X, E, None, dev)

@@ -49,7 +49,10 @@ def tensor_specs(cfg: ModelConfig, ftype: FileType) -> list[tuple[str, tuple[int
     Ekv = cfg.n_embd_kv
     f32 = GGMLType.F32
     mt = lambda role, i=0: _matrix_type(ftype, role, i, L)  # noqa: E731
-    specs: list[tuple[str, tuple[int, ...], GGMLType]] = [("token_embd.weight", (E, V), mt("token_embd"))]
+    # tied embeddings (Gemma) carry the output projection's type (llama.cpp quantises token_embd as
+    # output.weight when the latter is absent)
+    emb_role = "output" if cfg.arch == "gemma" else "token_embd"
+    specs: list[tuple[str, tuple[int, ...], GGMLType]] = [("token_embd.weight", (E, V), mt(emb_role))]
     if cfg.arch == "phi2":
         for i in range(L):
             b = f"blk.{i}."
@@ -64,14 +67,15 @@ def tensor_specs(cfg: ModelConfig, ftype: FileType) -> list[tuple[str, tuple[int
         specs += [("output_norm.weight", (E,), f32), ("output_norm.bias", (E,), f32),
                   ("output.weight", (E, V), mt("output")), ("output.bias", (V,), f32)]
         return specs
+    Eq = cfg.n_embd_q
     for i in range(L):
         b = f"blk.{i}."
         specs += [
             (b + "attn_norm.weight", (E,), f32),
-            (b + "attn_q.weight", (E, E), mt("attn_q", i)),
+            (b + "attn_q.weight", (E, Eq), mt("attn_q", i)),
             (b + "attn_k.weight", (E, Ekv), mt("attn_k", i)),
             (b + "attn_v.weight", (E, Ekv), mt("attn_v", i)),
-            (b + "attn_output.weight", (E, E), mt("attn_output", i)),
+            (b + "attn_output.weight", (Eq, E), mt("attn_output", i)),
             (b + "ffn_norm.weight", (E,), f32),
         ]
         if cfg.n_expert:
@@ -88,5 +92,7 @@ def tensor_specs(cfg: ModelConfig, ftype: FileType) -> list[tuple[str, tuple[int
                 (b + "ffn_up.weight", (E, F), mt("ffn_up", i)),
                 (b + "ffn_down.weight", (F, E), mt("ffn_down", i)),
             ]
-    specs += [("output_norm.weight", (E,), f32), ("output.weight", (E, V), mt("output"))]
+    specs += [("output_norm.weight", (E,), f32)]
+    if cfg.arch != "gemma":  # Gemma ties the output projection to token_embd
+        specs += [("output.weight", (E, V), mt("output"))]
     return specs

@@ -12,7 +12,7 @@ ROPE_NEOX = 2   # rotate halves (x[i], x[i + n_rot/2]) -- phi2 / gpt-neox
 
 # GGUF `general.architecture` values this engine runs, mapped to its internal arch. llama.cpp writes
 # "llama" for Llama 2 / Code Llama / Vicuna / Mistral / Mixtral (MoE via expert_count).
-SUPPORTED_ARCHS = {"llama": "llama", "phi2": "phi2"}
+SUPPORTED_ARCHS = {"llama": "llama", "phi2": "phi2", "gemma": "gemma"}
 
 
 class UnsupportedArchitecture(ValueError):
@@ -22,7 +22,7 @@ class UnsupportedArchitecture(ValueError):
 
 @dataclass
 class ModelConfig:
-    arch: str = "llama"            # "llama" (also Mistral / Mixtral / CodeLlama / Vicuna), "phi2"
+    arch: str = "llama"            # "llama" (also Mistral / Mixtral / CodeLlama / Vicuna), "phi2", "gemma"
     n_vocab: int = 32000
     n_embd: int = 4096
     n_layer: int = 32
@@ -37,6 +37,7 @@ class ModelConfig:
     n_expert: int = 0
     n_expert_used: int = 0
     sliding_window: int = 0
+    n_embd_head: int = 0           # head dim when not n_embd / n_head (Gemma: attention.key_length = 256)
     bos_id: int = 1
     eos_id: int = 2
     name: str = ""
@@ -44,7 +45,21 @@ class ModelConfig:
 
     @property
     def head_dim(self) -> int:
-        return self.n_embd // self.n_head
+        return self.n_embd_head or self.n_embd // self.n_head
+
+    @property
+    def n_embd_q(self) -> int:
+        return self.head_dim * self.n_head
+
+    @property
+    def gelu_glu(self) -> bool:
+        """GeGLU FFN (gelu(gate) * up) instead of SwiGLU (Gemma)."""
+        return self.arch == "gemma"
+
+    @property
+    def embed_scale(self) -> float:
+        """Token embeddings are multiplied by sqrt(n_embd) (Gemma; llama.cpp build_gemma)."""
+        return float(self.n_embd) ** 0.5 if self.arch == "gemma" else 1.0
 
     @property
     def n_embd_kv(self) -> int:
@@ -77,6 +92,9 @@ class ModelConfig:
         tokens = md.get("tokenizer.ggml.tokens")
         n_embd = int(g("embedding_length"))
         n_head = int(g("attention.head_count"))
+        head = int(g("attention.key_length", n_embd // n_head))
+        if int(g("attention.value_length", head)) != head:
+            raise UnsupportedArchitecture("attention.value_length != attention.key_length")
         cfg = cls(
             arch=SUPPORTED_ARCHS[arch],
             n_vocab=int(g("vocab_size", len(tokens) if tokens is not None else 32000)),
@@ -85,14 +103,15 @@ class ModelConfig:
             n_head=n_head,
             n_head_kv=int(g("attention.head_count_kv", n_head)),
             n_ff=int(g("feed_forward_length")),
-            n_rot=int(g("rope.dimension_count", n_embd // n_head)),
+            n_rot=int(g("rope.dimension_count", head)),
             rope_base=float(g("rope.freq_base", 10000.0)),
-            rope_mode=ROPE_NEOX if arch == "phi2" else ROPE_NORM,
+            rope_mode=ROPE_NEOX if arch in ("phi2", "gemma") else ROPE_NORM,  # llama.cpp llama_rope_type
             norm_eps=float(g("attention.layer_norm_rms_epsilon", g("attention.layer_norm_epsilon", 1e-5))),
             ctx_len=int(g("context_length", 4096)),
             n_expert=int(g("expert_count", 0)),
             n_expert_used=int(g("expert_used_count", 0)),
             sliding_window=int(g("attention.sliding_window", 0) or 0),
+            n_embd_head=head if head != n_embd // n_head else 0,
             bos_id=int(md.get("tokenizer.ggml.bos_token_id", 1)),
             eos_id=int(md.get("tokenizer.ggml.eos_token_id", 2)),
             name=str(md.get("general.name", "")),
@@ -100,7 +119,7 @@ class ModelConfig:
         return cfg
 
     def to_gguf_metadata(self) -> dict[str, Any]:
-        a = "phi2" if self.arch == "phi2" else "llama"
+        a = self.arch if self.arch in ("phi2", "gemma") else "llama"
         p = a + "."
         md: dict[str, Any] = {
             "general.architecture": a,
@@ -113,6 +132,9 @@ class ModelConfig:
             p + "attention.head_count": self.n_head,
             p + "attention.head_count_kv": self.n_head_kv,
         }
+        if self.n_embd_head or a == "gemma":
+            md[p + "attention.key_length"] = self.head_dim
+            md[p + "attention.value_length"] = self.head_dim
         if a == "phi2":
             md[p + "attention.layer_norm_epsilon"] = float(self.norm_eps)
         else:
@@ -138,7 +160,18 @@ PRESETS: dict[str, ModelConfig] = {
     "phi2": ModelConfig(name="phi2", arch="phi2", n_vocab=51200, n_embd=2560, n_layer=32, n_head=32,
                         n_head_kv=32, n_ff=10240, n_rot=32, rope_mode=ROPE_NEOX, norm_eps=1e-5,
                         ctx_len=2048, bos_id=50256, eos_id=50256),
+    # Gemma (reference README.md:58-59): GeGLU, sqrt(E) embedding scale, head dim 256, MQA (2B),
+    # NEOX RoPE, tied output. GGUF norm weights already carry Gemma's (1 + w) (llama.cpp converter)
+    "gemma-2b": ModelConfig(name="gemma-2b", arch="gemma", n_vocab=256000, n_embd=2048, n_layer=18, n_head=8,
+                            n_head_kv=1, n_ff=16384, n_rot=256, n_embd_head=256, rope_mode=ROPE_NEOX,
+                            norm_eps=1e-6, ctx_len=8192, bos_id=2, eos_id=1),
+    "gemma-7b": ModelConfig(name="gemma-7b", arch="gemma", n_vocab=256000, n_embd=3072, n_layer=28, n_head=16,
+                            n_head_kv=16, n_ff=24576, n_rot=256, n_embd_head=256, rope_mode=ROPE_NEOX,
+                            norm_eps=1e-6, ctx_len=8192, bos_id=2, eos_id=1),
     # small shapes of the same families for tests (K multiples of 256 so every quant type applies)
+    "tiny-gemma": ModelConfig(name="tiny-gemma", arch="gemma", n_vocab=512, n_embd=256, n_layer=2, n_head=2,
+                              n_head_kv=1, n_ff=512, n_rot=256, n_embd_head=256, rope_mode=ROPE_NEOX,
+                              norm_eps=1e-6, ctx_len=256, bos_id=2, eos_id=1),
     "tiny-llama": ModelConfig(name="tiny-llama", n_vocab=512, n_embd=256, n_layer=2, n_head=4,
                               n_head_kv=2, n_ff=512, n_rot=64, ctx_len=256),
     "tiny-mixtral": ModelConfig(name="tiny-mixtral", n_vocab=512, n_embd=256, n_layer=2, n_head=4,

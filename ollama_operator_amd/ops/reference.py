@@ -64,7 +64,7 @@ class TorchExecutor:
     def embed(self, B: int):
         r = self.r
         toks = r.d_tokens[:B].long()
-        r.resid[:B] = self.W(self.w.tok_embd)[toks]
+        r.resid[:B] = self.W(self.w.tok_embd)[toks] * self.w.cfg.embed_scale
 
     def attn(self, i: int, B: int):
         r, w = self.r, self.w
@@ -151,7 +151,8 @@ class TorchExecutor:
                         y[b] += tw[b, j] * (DN[e] @ h)
             else:
                 gu = xn @ self.W(L["wgu"]).T
-                h = F.silu(gu[:, 0::2]) * gu[:, 1::2]
+                act = self._gelu if cfg.gelu_glu else F.silu
+                h = act(gu[:, 0::2]) * gu[:, 1::2]
                 y = h @ self.W(L["wdown"]).T
         if r.tp_size > 1:
             r.ypart[:B] = y

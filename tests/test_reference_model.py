@@ -62,3 +62,25 @@ def test_unknown_architecture_fails_loudly(tmp_path):
     del md["general.architecture"]
     with _pt.raises(UnsupportedArchitecture):
         ModelConfig.from_gguf_metadata(md)
+
+
+def test_gemma_config_and_tensors(tmp_path):
+    """Gemma (reference README.md:58-59): head dim from attention.key_length (256 != E / H), NEOX
+    RoPE, GeGLU, sqrt(E) embedding scale, tied output (no output.weight)."""
+    import math
+
+    from ollama_operator_amd.gguf.constants import FileType
+    from ollama_operator_amd.gguf.reader import read_gguf
+    from ollama_operator_amd.models.config import ROPE_NEOX, ModelConfig, preset
+    from ollama_operator_amd.models.random_init import write_random_gguf
+    path = str(tmp_path / "g.gguf")
+    write_random_gguf(path, preset("tiny-gemma"), FileType.MOSTLY_Q4_K_M, seed=0)
+    g = read_gguf(path)
+    cfg = ModelConfig.from_gguf_metadata(g.metadata)
+    assert cfg.arch == "gemma" and cfg.head_dim == 256 and cfg.n_embd_q == 512 and cfg.rope_mode == ROPE_NEOX
+    assert cfg.gelu_glu and math.isclose(cfg.embed_scale, 16.0)
+    assert "output.weight" not in g.tensors and "token_embd.weight" in g.tensors
+    assert tuple(g.tensors["blk.0.attn_output.weight"].shape) == (512, 256)
+    for name in ("gemma-2b", "gemma-7b"):
+        c = preset(name)
+        assert c.head_dim == 256 and c.n_vocab == 256000
