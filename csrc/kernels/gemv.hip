@@ -529,7 +529,9 @@ static void launch_flight_ks_n(const GemvParams& P, int gx, hipStream_t s) {
       case 3: hipLaunchKernelGGL((qgemv_flight_kernel<QT, NSB, 1, 1, NRM, 3, KS>), dim3(gx, 1, bz), dim3(GEMV_NT * KS), lds, s, P); return;
       case 4: hipLaunchKernelGGL((qgemv_flight_kernel<QT, NSB, 1, 1, NRM, 4, KS>), dim3(gx, 1, bz), dim3(GEMV_NT * KS), lds, s, P); return;
       case 9: hipLaunchKernelGGL((qgemv_flight_kernel<QT, NSB, 1, 1, NRM, 9, KS>), dim3(gx, 1, bz), dim3(GEMV_NT * KS), lds, s, P); return;
-      case 16: hipLaunchKernelGGL((qgemv_flight_kernel<QT, NSB, 1, 1, NRM, 16, KS>), dim3(gx, 1, bz), dim3(GEMV_NT * KS), lds, s, P); return;
+      case 16:
+        hipLaunchKernelGGL((qgemv_flight_kernel<QT, NSB, 1, 1, NRM, 16, KS>), dim3(gx, 1, bz), dim3(GEMV_NT * KS), lds, s, P);
+        return;
       default: break;
     }
   }

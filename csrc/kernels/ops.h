@@ -83,7 +83,7 @@ struct GemvTuning {
   int ks = 0;             // in-block K split of the flight kernel: 0 = auto, 1 = off, 2..4 = forced
   int xfirst = 0;         // 1: decode GEMVs wait for their activations before streaming weights
   int xbar = 0;           // 1: batch-1 decode GEMVs as x-barrier launches, one block per CU (gemv.hip XB)
-  int stream = 1;         // 1: batch-1 decode GEMVs on the bounded-depth streaming kernel (gemv_stream.hip)
+  int stream = 0;         // 1: batch-1 decode GEMVs on the bounded-depth streaming kernel (gemv_stream.hip)
   int stream_bpc = 1;     // its blocks per CU
 };
 extern GemvTuning g_tune;
