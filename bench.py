@@ -341,7 +341,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=16)
     ap.add_argument("--prompt", type=int, default=128)
     ap.add_argument("--model", default="llama2-7b")
-    ap.add_argument("--ftype", default="Q4_K_M")
+    ap.add_argument("--ftype", default="Q4_K_M", type=str.upper)
     ap.add_argument("--dir", default=os.environ.get("OMX_BENCH_DIR", "/tmp/omx_bench"))
     ap.add_argument("--batch-extra", type=int, default=0,
                     help="also measure continuous-batching throughput with this many concurrent sequences per "
