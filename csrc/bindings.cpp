@@ -250,7 +250,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemv_merge_supported", &gemv_merge_supported);
   m.def("set_gemv_tuning", &set_gemv_tuning, py::arg("blocks_per_cu") = 0, py::arg("rows") = 0,
         py::arg("debug") = 0, py::arg("ks") = -1, py::arg("xfirst") = -1, py::arg("xbar") = -1,
-        py::arg("stream") = -1, py::arg("stream_bpc") = -1);
+        py::arg("stream") = -1, py::arg("stream_bpc") = -1, py::arg("pf") = -1, py::arg("ws") = -1);
   m.def("embed_rows", [](py::object w, uintptr_t rows, int n, uintptr_t out, int ldo, uintptr_t stream) {
     embed_rows(qmat(w), Pp<const int>(rows), n, Pp<float>(out), ldo, S(stream));
   });

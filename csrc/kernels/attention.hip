@@ -88,8 +88,9 @@ struct KVStep {
   KRow<DPL> k[U], v[U];
 };
 
-// U key slots per lane group per step: 4, or 2 when 8 query heads share a KV head (registers)
-template <int D, int G, int U = (G >= 8 ? 2 : 4)>
+// U key slots per lane group per step: 4, or 2 when 8 query heads share a KV head or the head dim is
+// 256 (registers: 4 slots of D = 256 spilled 188 B per lane)
+template <int D, int G, int U = (G >= 8 || D > 128 ? 2 : 4)>
 __global__ __launch_bounds__(ATT_NT) void attn_decode_kernel(AttnParams P) {
   constexpr int DPL = D / 16;
   constexpr int ATT_U = U, ATT_STEP = ATT_NG * U;

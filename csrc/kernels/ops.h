@@ -63,6 +63,11 @@ struct GemvParams {
   // prologue done, first tile computed, exit; null in production
   unsigned long long* dbg_ts;
   int xfirst;                  // activations waited for before any weight load (GemvTuning::xfirst)
+  // cross-launch prefetch (B == 1 decode): the matrix the NEXT GEMV of the step streams. Block b
+  // pulls a prefix of that launch's row tile b (16 rows, every stream) into its XCD's L2 behind its
+  // own weight loads, so the bytes move while this launch computes its tail and the next one ramps
+  // (pf.s0 null: off). Block b of both grids sits on XCD b % 8.
+  QMat pf;
 };
 
 // y = epi(W x): the quantised GEMV for small B (decode), the MFMA dequant GEMM for B >= GEMM_MIN_B
@@ -85,10 +90,12 @@ struct GemvTuning {
   int xbar = 0;           // 1: batch-1 decode GEMVs as x-barrier launches, one block per CU (gemv.hip XB)
   int stream = 0;         // 1: batch-1 decode GEMVs on the bounded-depth streaming kernel (gemv_stream.hip)
   int stream_bpc = 1;     // its blocks per CU
+  int pf = 0;             // 1: batch-1 GEMVs prefetch the next GEMV's first row tiles into L2 (GemvParams::pf)
+  int ws = 0;             // 1: batch-1 GEMVs on the wave-specialised LDS-DMA kernel (gemv_ws.hip)
 };
 extern GemvTuning g_tune;
 void set_gemv_tuning(int blocks_per_cu, int rows, int debug, int ks = -1, int xfirst = -1, int xbar = -1,
-                     int stream = -1, int stream_bpc = -1);
+                     int stream = -1, int stream_bpc = -1, int pf = -1, int ws = -1);
 
 // Dequantize rows of a repacked matrix (embedding gather / fp16 copies)
 void embed_rows(const QMat& w, const int* rows, int n, float* out, int ldo, hipStream_t s, float scale = 1.f);

@@ -48,10 +48,12 @@ void Executor::attn_block(int i, const StepInputs& in, hipStream_t s) {
   P.n_rot = cfg.n_rot;
   P.n_kv = cfg.Hkv;
   P.bs = in.bs;
+  P.pf = phi ? L.wgu : L.wo;  // the next GEMV of the step (gemv.hip cross-launch prefetch)
   if (!L.qkv_fused) {  // q,k and v rows of different quant types: one dual launch at B == 1
     GemvParams V = P;
     V.w = L.wv;
     V.row_offset = Eq + Ekv;
+    V.pf = QMat{};
     gemv2(P, V, s);
   } else {
     gemv(P, s);
@@ -66,6 +68,7 @@ void Executor::attn_block(int i, const StepInputs& in, hipStream_t s) {
     U.bias = L.bup;
     U.y = ws.hbuf;
     U.ldy = cfg.F;
+    U.pf = L.wo;
     gemv(U, s);
   }
   // --- attention over the paged cache
@@ -105,6 +108,7 @@ void Executor::attn_block(int i, const StepInputs& in, hipStream_t s) {
     O.merge_D = cfg.D;
   }
   O.bias = L.bo;
+  O.pf = phi ? L.wdown : cfg.n_expert > 0 ? L.router : L.wgu;
   if (cfg.tp > 1) {
     O.epi = EPI_STORE;
     O.y = tp_dst(0, B);
@@ -127,6 +131,7 @@ void Executor::ffn_block(int i, const StepInputs& in, hipStream_t s) {
     Dn.bias = L.bdown;
     Dn.y = dst;
     Dn.ldy = E;
+    Dn.pf = next_qkv(i);
     gemv(Dn, s);
     return;
   }
@@ -196,7 +201,7 @@ void Executor::ffn_block(int i, const StepInputs& in, hipStream_t s) {
     Dn.n_sel = k;
     Dn.x_per_sel = 1;
     Dn.x_sel_stride = F;
-    gemv(Dn, s);
+    gemv(Dn, s);  // expert launches take no prefetch (their rows depend on the routing)
     return;
   }
   GemvParams G = base_params(L.wgu, B, ws.resid, E, ws);
@@ -206,11 +211,13 @@ void Executor::ffn_block(int i, const StepInputs& in, hipStream_t s) {
   G.epi = cfg.glu_act ? EPI_GEGLU : EPI_GLU;
   G.y = ws.hbuf;
   G.ldy = F;
+  G.pf = L.wdown;
   gemv(G, s);
   GemvParams Dn = base_params(L.wdown, B, ws.hbuf, F, ws);
   Dn.epi = dst_epi;
   Dn.y = dst;
   Dn.ldy = E;
+  Dn.pf = next_qkv(i);
   gemv(Dn, s);
 }
 
@@ -232,6 +239,11 @@ void Executor::head(const StepInputs& in, hipStream_t s) {
   P.y = in.logits;
   P.ldy = lm_head.N;
   gemv(P, s);
+}
+
+// the first GEMV after layer i's FFN: layer i+1's QKV, or the LM head
+QMat Executor::next_qkv(int i) const {
+  return i + 1 < (int)layers.size() ? layers[i + 1].wqk : lm_head;
 }
 
 float* Executor::tp_dst(int slab, int B) const {

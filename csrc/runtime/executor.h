@@ -112,6 +112,7 @@ class Executor {
 
  private:
   float* tp_dst(int slab, int B) const;  // where a row-parallel projection leaves its partial sums
+  QMat next_qkv(int i) const;          // the matrix the GEMV after layer i's FFN streams (prefetch target)
   int ar_active_ = 0;
 };
 

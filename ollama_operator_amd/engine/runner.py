@@ -116,6 +116,10 @@ class Runner:
                 native().set_gemv_tuning(xbar=int(os.environ["OMX_GEMV_XBAR"]))
             if os.environ.get("OMX_GEMV_STREAM") in ("0", "1"):  # bounded-depth streaming decode GEMV
                 native().set_gemv_tuning(stream=int(os.environ["OMX_GEMV_STREAM"]))
+            if os.environ.get("OMX_GEMV_PF") in ("0", "1"):  # cross-launch L2 prefetch of the next GEMV
+                native().set_gemv_tuning(pf=int(os.environ["OMX_GEMV_PF"]))
+            if os.environ.get("OMX_GEMV_WS") in ("0", "1"):  # wave-specialised LDS-DMA decode GEMV
+                native().set_gemv_tuning(ws=int(os.environ["OMX_GEMV_WS"]))
             if os.environ.get("OMX_GEMV_STREAM_BPC"):
                 native().set_gemv_tuning(stream_bpc=int(os.environ["OMX_GEMV_STREAM_BPC"]))
         self.tp_rank, self.tp_size, self.tp_group = tp_rank, tp_size, tp_group

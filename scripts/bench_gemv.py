@@ -63,12 +63,14 @@ def main():
     if os.environ.get("OMX_BENCH_SHAPES"):
         keep = os.environ["OMX_BENCH_SHAPES"].split(",")
         shapes = [s for s in SHAPES if s[0] in keep]
-    # knob tuple: (blocks/CU, rows, debug, ks, xfirst, xbar, stream, stream_bpc); missing -> defaults
-    knobs = [tuple(k) + (0, 0, 0, 0, 0, 0, 1, 1)[len(k):] for k in knobs]
+    # knob tuple: (blocks/CU, rows, debug, ks, xfirst, xbar, stream, stream_bpc, ws); missing -> defaults
+    knobs = [tuple(k) + (0, 0, 0, 0, 0, 0, 0, 1, 0)[len(k):] for k in knobs]
     if os.environ.get("OMX_BENCH_XBAR_AB"):  # A/B of the x-barrier launch on every knob
         knobs = [k[:5] + (xb,) + k[6:] for k in knobs for xb in (0, 1)]
     if os.environ.get("OMX_BENCH_STREAM_AB"):  # flight vs streaming kernel (1 and 2 blocks per CU)
-        knobs = [k[:6] + (0, 1) for k in knobs] + [k[:6] + (1, b) for k in knobs for b in (1, 2)]
+        knobs = [k[:6] + (0, 1) + k[8:] for k in knobs] + [k[:6] + (1, b) + k[8:] for k in knobs for b in (1, 2)]
+    if os.environ.get("OMX_BENCH_WS_AB"):  # flight vs the wave-specialised LDS-DMA kernel (gemv_ws.hip)
+        knobs = [k[:8] + (w,) for k in knobs for w in (0, 1)]
     # clock warm-up: the first shape measured on an idle GPU otherwise reads up to 2x slow
     big = torch.empty(256 << 20, dtype=torch.uint8, device="cuda")
     t0 = time.time()
@@ -76,8 +78,8 @@ def main():
         big.add_(1)
     torch.cuda.synchronize()
     del big
-    for (name, qt, N, K, epi), (bpc, rpw, r1, ks, xf, xb, st, sbpc) in itertools.product(shapes, knobs):
-        C.set_gemv_tuning(bpc, rpw, r1, ks, xf, xb, st, sbpc)
+    for (name, qt, N, K, epi), (bpc, rpw, r1, ks, xf, xb, st, sbpc, ws) in itertools.product(shapes, knobs):
+        C.set_gemv_tuning(bpc, rpw, r1, ks, xf, xb, st, sbpc, ws=ws)
         tups, ts, nbytes = mats[name]
         x = torch.randn(1, K, device="cuda")
         nw = torch.ones(K, device="cuda")
@@ -96,9 +98,10 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) * 1e3 / n
-        res.append((name, f"blocks/CU={bpc} rows={rpw} dbg={r1} ks={ks} xfirst={xf} xbar={xb} stream={st}x{sbpc}", us, nbytes / us / 1e3))
+        res.append((name, f"blocks/CU={bpc} rows={rpw} dbg={r1} ks={ks} xfirst={xf} xbar={xb} stream={st}x{sbpc} ws={ws}",
+                    us, nbytes / us / 1e3))
         print(f"{name:10s} {res[-1][1]} {us:8.2f} us  {nbytes/us/1e3:7.1f} GB/s", flush=True)
-    C.set_gemv_tuning(4, 1, 0, 0, 0, 0, 1, 1)
+    C.set_gemv_tuning(4, 1, 0, 0, 0, 0, 0, 1, ws=0)
     print("best per shape:")
     for name in mats:
         b = min((r for r in res if r[0] == name), key=lambda r: ("dbg=0" not in r[1], r[2]))
