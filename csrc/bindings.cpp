@@ -25,7 +25,7 @@ static QMat qmat(py::object o) {
   QMat m{};
   if (o.is_none()) return m;
   auto t = o.cast<py::tuple>();
-  if (t.size() != 7 && t.size() != 8) throw std::runtime_error("qmat tuple must be (s0, s1, s2, s3, N, K, qtype[, s4])");
+  if (t.size() < 7 || t.size() > 9) throw std::runtime_error("qmat tuple must be (s0, s1, s2, s3, N, K, qtype[, s4[, mt]])");
   m.s0 = Pp<const uint8_t>(t[0].cast<uintptr_t>());
   m.s1 = Pp<const uint8_t>(t[1].cast<uintptr_t>());
   m.s2 = Pp<const uint8_t>(t[2].cast<uintptr_t>());
@@ -33,7 +33,8 @@ static QMat qmat(py::object o) {
   m.N = t[4].cast<int>();
   m.K = t[5].cast<int>();
   m.qtype = t[6].cast<int>();
-  m.s4 = t.size() == 8 ? Pp<const uint8_t>(t[7].cast<uintptr_t>()) : nullptr;
+  m.s4 = t.size() >= 8 ? Pp<const uint8_t>(t[7].cast<uintptr_t>()) : nullptr;
+  m.mt = t.size() == 9 ? Pp<const uint8_t>(t[8].cast<uintptr_t>()) : nullptr;
   if (m.s4 && m.qtype != QT_Q6_K) throw std::runtime_error("widened codes are for Q6_K only");
   if (m.qtype != QT_Q4_0 && m.qtype != QT_Q8_0 && m.qtype != QT_Q4_K && m.qtype != QT_Q5_K && m.qtype != QT_Q6_K)
     throw std::runtime_error("unsupported device quant type " + std::to_string(m.qtype));
@@ -201,6 +202,22 @@ PYBIND11_MODULE(_C, m) {
       P.n_kv = qkv["n_kv"].cast<int>();
       P.bs = qkv["bs"].cast<int>();
     }
+    // batched matrix-core decode chain (gemv_mfma.hip): fp16 activations in, RMS partials, emission
+    auto ip = [&](const char* k) -> uintptr_t { return qkv.contains(k) ? qkv[k].cast<uintptr_t>() : 0; };
+    auto ii = [&](const char* k) -> int { return qkv.contains(k) ? qkv[k].cast<int>() : 0; };
+    P.x16 = Pp<const void>(ip("x16"));
+    P.ld16 = ii("ld16");
+    P.zrow16 = ii("zrow16");
+    P.xstat = Pp<const float>(ip("xstat"));
+    P.xstat_n = ii("xstat_n");
+    P.emit16 = Pp<void>(ip("emit16"));
+    P.ld_emit = ii("ld_emit");
+    P.emit_nw = Pp<const float>(ip("emit_nw"));
+    P.emit_stat = Pp<float>(ip("emit_stat"));
+    P.y16 = Pp<void>(ip("y16"));
+    P.ld16y = ii("ld16y");
+    if ((P.x16 || P.emit16 || P.y16) && !gemv_mb_supported(P))
+      throw std::runtime_error("gemv: fp16 chain operands given for a shape the matrix-core GEMV does not take");
     if (qkv.contains("expert_ids")) {
       P.expert_ids = Pp<const int>(qkv["expert_ids"].cast<uintptr_t>());
       P.expert_w = Pp<const float>(qkv.contains("expert_w") ? qkv["expert_w"].cast<uintptr_t>() : 0);
@@ -273,6 +290,14 @@ PYBIND11_MODULE(_C, m) {
     decode_feedback(Pp<int>(step), ld, Pp<const int>(sampled), B, advance, Pp<const int>(block_table), max_blocks,
                     bs, Pp<int>(host_ring), ring, S(stream));
   });
+  m.def("mfma_layout_bytes", &mfma_layout_bytes);
+  m.def("repack_m", [](py::object w, uintptr_t out, uintptr_t stream) {
+    QMat q = qmat(w);
+    if (!out || !mfma_layout_bytes(q.qtype, q.N, q.K)) throw std::runtime_error("repack_m: no layout M for this matrix");
+    repack_m(q, Pp<void>(out), S(stream));
+  });
+  m.def("set_mb_enable", &set_mb_enable);
+  m.def("set_mb_tuning", &set_mb_tuning, py::arg("dbg") = -1, py::arg("bpc") = 0);
   m.def("widen_q6k", [](py::object w, uintptr_t out, uintptr_t stream) {
     QMat q = qmat(w);
     if (q.qtype != QT_Q6_K || !out) throw std::runtime_error("widen_q6k: Q6_K matrix and output required");
@@ -397,6 +422,15 @@ PYBIND11_MODULE(_C, m) {
         w.moe_rows = Pp<int>(ptr("moe_rows"));
         w.moe_tiles = Pp<int>(ptr("moe_tiles"));
         w.moe_ntiles = Pp<int>(ptr("moe_ntiles"));
+        w.mb_ok = (d.contains("mb_ok") ? d["mb_ok"].cast<int>() : 0) && e.chain_capable() ? 1 : 0;
+        w.xa16 = Pp<void>(ptr("xa16"));
+        w.h16 = Pp<void>(ptr("h16"));
+        w.a16 = Pp<void>(ptr("a16"));
+        w.st[0] = Pp<float>(ptr("st0"));
+        w.st[1] = Pp<float>(ptr("st1"));
+        w.ld_e = d.contains("ld_e") ? d["ld_e"].cast<int>() : 0;
+        w.ld_f = d.contains("ld_f") ? d["ld_f"].cast<int>() : 0;
+        w.ld_q = d.contains("ld_q") ? d["ld_q"].cast<int>() : 0;
         w.max_B = d["max_B"].cast<int>();
         w.n_splits = d["n_splits"].cast<int>();
       })
@@ -427,7 +461,8 @@ PYBIND11_MODULE(_C, m) {
         e.ws.ar_on = 1;
       })
       .def("clear_ar", [](Executor& e) { e.ws.ar_on = 0; })
-      .def("ar_fits", &Executor::ar_fits);
+      .def("ar_fits", &Executor::ar_fits)
+      .def_property_readonly("mb_chain", [](const Executor& e) { return e.ws.mb_ok != 0; });
   m.attr("ST_FORWARD") = (int)ST_FORWARD;
   m.attr("ST_EMBED") = (int)ST_EMBED;
   m.attr("ST_ATTN") = (int)ST_ATTN;

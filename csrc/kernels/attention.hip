@@ -253,7 +253,9 @@ __global__ __launch_bounds__(ATT_NT) void attn_decode_kernel(AttnParams P) {
       P.ws[row * P.H * D + h * D + d] = A;
       if (d == 0) *(f32x2*)(P.ws + (long long)P.NQ * S * P.H * D + (row * P.H + h) * 2) = (f32x2){M, L};
     } else if (S == 1) {
-      P.out[(long long)qi * P.ldo + h * D + d] = L > 0.f ? A / L : 0.f;
+      const float o = L > 0.f ? A / L : 0.f;
+      P.out[(long long)qi * P.ldo + h * D + d] = o;
+      if (P.out16) ((f16*)P.out16)[(long long)qi * P.ldo + h * D + d] = (f16)o;
     } else {  // write-through (sc1) stores: the hand-off below then needs no release fence
       float* ws = P.ws + (((long long)qi * P.H + h) * gridDim.z + split) * (D + 2);
       __hip_atomic_store(ws + d, A, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -306,7 +308,9 @@ __global__ __launch_bounds__(ATT_NT) void attn_decode_kernel(AttnParams P) {
 #pragma unroll 8
     for (int s = 0; s < S; ++s) A += sw[g][s] * ld1(ws + s * (D + 2) + d);
     const float L = sL[g];
-    P.out[(long long)qi * P.ldo + (h0 + g) * D + d] = L > 0.f ? A / L : 0.f;
+    const float o = L > 0.f ? A / L : 0.f;
+    P.out[(long long)qi * P.ldo + (h0 + g) * D + d] = o;
+    if (P.out16) ((f16*)P.out16)[(long long)qi * P.ldo + (h0 + g) * D + d] = (f16)o;
   }
 }
 

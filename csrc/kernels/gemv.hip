@@ -860,6 +860,7 @@ void gemv(const GemvParams& P0, hipStream_t s) {
     // flight grid for K <= 4096 is one chunk, R = 1, no K split: the merge variant covers exactly it
     if (!gemv_merge_supported(P.B, P.w.K, P.merge_D, P.merge_S) || P.norm != NORM_NONE || P.expert_ids) return;
   }
+  if (P.B > 1 && gemv_mb(P, s)) return;  // continuous-batching rows on the matrix cores (layout M)
   if (gemm_eligible(P)) {
     gemm(P, s);
     return;

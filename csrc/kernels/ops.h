@@ -68,6 +68,18 @@ struct GemvParams {
   // own weight loads, so the bytes move while this launch computes its tail and the next one ramps
   // (pf.s0 null: off). Block b of both grids sits on XCD b % 8.
   QMat pf;
+  // batched matrix-core decode chain (gemv_mfma.hip, 2 <= B <= 16; null = unused):
+  const void* x16;             // consumer: activations already in fp16 [B][ld16] (times norm_w when norm = RMS)
+  int ld16;
+  int zrow16;                  //   index of an all-zero row of x16 (>= B): the A-operand lanes of rows >= B
+  const float* xstat;          // consumer: per-row sum-of-squares partials [xstat_n][16] of the un-normed x
+  int xstat_n;                 //   (RMSNorm scale rsqrt(sum / K + eps) applied to the outputs)
+  void* emit16;                // producer (EPI_ADD): also writes fp16(new_resid * emit_nw) [B][ld_emit]
+  int ld_emit;
+  const float* emit_nw;
+  float* emit_stat;            //   and its per-16-row-tile sum-of-squares partials [tiles][16]
+  void* y16;                   // EPI_GLU / EPI_GEGLU: fp16 output [B][ld16y] instead of y
+  int ld16y;
 };
 
 // y = epi(W x): the quantised GEMV for small B (decode), the MFMA dequant GEMM for B >= GEMM_MIN_B
@@ -77,6 +89,15 @@ bool gemv_merge_supported(int B, int K, int D, int S);
 // two GEMVs over the same x (same K, RMS norm prologue) in one launch when B == 1, else two launches
 void gemv2(const GemvParams& A, const GemvParams& B, hipStream_t s);
 constexpr int GEMM_MIN_B = 16;
+// batched decode GEMV on the matrix cores (gemv_mfma.hip): 2 <= B <= 16 rows, needs the layout M
+// copy (QMat::mt) built by repack_m; false = shape not covered (the caller takes the int8 GEMV)
+bool gemv_mb(const GemvParams& P, hipStream_t s);
+bool gemv_mb_supported(const GemvParams& P);
+void set_mb_enable(int on);
+void set_mb_tuning(int dbg, int bpc);  // microbenchmark variants (gemv_mfma.hip DBG), blocks per CU
+bool mb_enabled();
+size_t mfma_layout_bytes(int qtype, int N, int K);  // 0 = no layout M for this quant type
+void repack_m(const QMat& w, void* out, hipStream_t s);
 bool gemm_eligible(const GemvParams& P);
 void gemm(const GemvParams& P, hipStream_t s);
 
@@ -115,6 +136,7 @@ struct AttnParams {
   int window;                  // sliding window (0 = none)
   float* out;                  // [NQ][ldo] fp32
   int ldo;
+  void* out16;                 // optional fp16 copy [NQ][ldo] (the batched matrix-core O projection reads it)
   float* ws;                   // split workspace: [NQ][H][S][D + 2] fp32
   int n_splits;                // <= 64
   int* counters;               // [NQ][H] arrival tickets (one per block row), zero before first use (self re-arming)

@@ -25,4 +25,5 @@ struct QMat {
   const uint8_t* s3;
   int N, K, qtype;
   const uint8_t* s4;  // optional widened Q6_K codes (QT_Q6_K8), null otherwise
+  const uint8_t* mt;  // optional layout M copy for the batched MFMA decode GEMV (gemv_mfma.hip), or null
 };

@@ -19,6 +19,56 @@ static GemvParams base_params(const QMat& w, int B, const float* x, int ldx, con
   return P;
 }
 
+// Batched decode chain (gemv_mfma.hip): each residual-adding projection (O, down) also emits the
+// next RMSNorm'd GEMV's activations as fp16(resid * norm_w) plus per-tile sum-of-squares partials;
+// the consumer (gate_up, next QKV, LM head) reads them straight from global memory and applies
+// rsqrt(mean + eps) to its outputs -- no per-block activation staging, no separate norm launch.
+bool Executor::chain(const StepInputs& in) const {
+  return ws.mb_ok && mb_enabled() && in.B >= 2 && in.B <= MB_CHAIN_MAX && !in.prefill && cfg.tp == 1 && cfg.arch == 0 &&
+         cfg.n_expert == 0 && ws.xa16 && ws.h16 && ws.a16 && ws.st[0] && ws.st[1];
+}
+
+static void chain_in(GemvParams& P, const void* x16, int ld16, const float* xstat, int n_stat) {
+  P.x16 = x16;
+  P.ld16 = ld16;
+  P.zrow16 = MB_CHAIN_MAX;
+  P.xstat = xstat;
+  P.xstat_n = n_stat;
+}
+
+static void chain_emit(GemvParams& P, void* e16, int ld, const float* nw, float* st) {
+  P.emit16 = e16;
+  P.ld_emit = ld;
+  P.emit_nw = nw;
+  P.emit_stat = st;
+}
+
+// every projection of the chain takes the matrix-core kernel (a fallback kernel would neither emit nor
+// read the fp16 activations): checked once when the workspace is bound
+bool Executor::chain_capable() const {
+  if (cfg.tp != 1 || cfg.arch != 0 || cfg.n_expert != 0 || layers.empty()) return false;
+  static const float dummy[4] = {0.f, 0.f, 0.f, 0.f};
+  auto ok = [&](const QMat& w, int epi, int norm, bool x16, bool emit) {
+    GemvParams P{};
+    P.w = w;
+    P.B = 2;
+    P.epi = epi;
+    P.norm = norm;
+    P.n_sel = 1;
+    if (x16) chain_in(P, dummy, 256, norm == NORM_RMS ? dummy : nullptr, (cfg.E + 15) / 16);
+    if (emit) chain_emit(P, (void*)dummy, 256, dummy, (float*)dummy);
+    return gemv_mb_supported(P);
+  };
+  for (const LayerW& L : layers) {
+    if (!ok(L.wqk, EPI_QKV, NORM_RMS, true, false) || !ok(L.wo, EPI_ADD, NORM_NONE, true, true) ||
+        !ok(L.wgu, EPI_GLU, NORM_RMS, true, false) || !ok(L.wdown, EPI_ADD, NORM_NONE, true, true))
+      return false;
+    if (!L.qkv_fused && !ok(L.wv, EPI_QKV, NORM_RMS, true, false)) return false;
+    if (!ok(L.wqk, EPI_QKV, NORM_RMS, false, false)) return false;  // layer 0 reads fp32 resid
+  }
+  return ok(lm_head, EPI_STORE, NORM_RMS, true, false);
+}
+
 void Executor::embed(const StepInputs& in, hipStream_t s) {
   embed_rows(tok_embd, in.tokens, in.B, ws.resid, cfg.E, s, cfg.embed_scale);
 }
@@ -49,6 +99,8 @@ void Executor::attn_block(int i, const StepInputs& in, hipStream_t s) {
   P.n_kv = cfg.Hkv;
   P.bs = in.bs;
   P.pf = phi ? L.wgu : L.wo;  // the next GEMV of the step (gemv.hip cross-launch prefetch)
+  const bool ch = chain(in);
+  if (ch && i > 0) chain_in(P, ws.xa16, ws.ld_e, ws.st[1], (E + 15) / 16);  // emitted by layer i-1's down
   if (!L.qkv_fused) {  // q,k and v rows of different quant types: one dual launch at B == 1
     GemvParams V = P;
     V.w = L.wv;
@@ -99,6 +151,7 @@ void Executor::attn_block(int i, const StepInputs& in, hipStream_t s) {
   if (defer && !gemv_merge_supported(B, Eq, cfg.D, ws.n_splits))
     throw std::runtime_error("deferred attention merge: unsupported (K, D, splits)");
   A.defer = defer;
+  if (ch) A.out16 = ws.a16;
   attention_decode(A, s);
   // --- output projection (+ residual, or partial sum under TP)
   GemvParams O = base_params(L.wo, B, defer ? ws.attn_ws : ws.abuf, Eq, ws);
@@ -117,6 +170,10 @@ void Executor::attn_block(int i, const StepInputs& in, hipStream_t s) {
     O.y = ws.resid;
   }
   O.ldy = E;
+  if (ch) {
+    chain_in(O, ws.a16, ws.ld_q, nullptr, 0);
+    chain_emit(O, ws.xa16, ws.ld_e, L.ffn_norm, ws.st[0]);  // gate_up's RMSNorm input
+  }
   gemv(O, s);
 }
 
@@ -204,6 +261,7 @@ void Executor::ffn_block(int i, const StepInputs& in, hipStream_t s) {
     gemv(Dn, s);  // expert launches take no prefetch (their rows depend on the routing)
     return;
   }
+  const bool ch = chain(in);
   GemvParams G = base_params(L.wgu, B, ws.resid, E, ws);
   G.norm = NORM_RMS;
   G.norm_w = L.ffn_norm;
@@ -212,12 +270,21 @@ void Executor::ffn_block(int i, const StepInputs& in, hipStream_t s) {
   G.y = ws.hbuf;
   G.ldy = F;
   G.pf = L.wdown;
+  if (ch) {
+    chain_in(G, ws.xa16, ws.ld_e, ws.st[0], (E + 15) / 16);
+    G.y16 = ws.h16;
+    G.ld16y = ws.ld_f;
+  }
   gemv(G, s);
   GemvParams Dn = base_params(L.wdown, B, ws.hbuf, F, ws);
   Dn.epi = dst_epi;
   Dn.y = dst;
   Dn.ldy = E;
   Dn.pf = next_qkv(i);
+  if (ch) {  // the next RMSNorm'd GEMV: layer i+1's QKV, or the LM head
+    chain_in(Dn, ws.h16, ws.ld_f, nullptr, 0);
+    chain_emit(Dn, ws.xa16, ws.ld_e, i + 1 < (int)layers.size() ? layers[i + 1].attn_norm : out_norm, ws.st[1]);
+  }
   gemv(Dn, s);
 }
 
@@ -238,6 +305,8 @@ void Executor::head(const StepInputs& in, hipStream_t s) {
   P.bias = lm_bias;
   P.y = in.logits;
   P.ldy = lm_head.N;
+  if (chain(in) && x == ws.resid && in.n_logits == in.B && cfg.n_layer > 0)
+    chain_in(P, ws.xa16, ws.ld_e, ws.st[1], (E + 15) / 16);
   gemv(P, s);
 }
 

@@ -69,7 +69,16 @@ struct Workspace {
   // write their partial sums into this rank's slab 0 / 1, the vocab-sharded LM head into slab 2.
   ARParams ar{};
   int ar_on = 0;
+  // batched decode chain on the matrix cores (gemv_mfma.hip, 2 <= B <= MB_CHAIN_MAX, tp == 1): fp16
+  // activation rows [MB_CHAIN_MAX + 1][ld] (row MB_CHAIN_MAX all zero) and RMS partial slabs
+  int mb_ok = 0;             // every dense projection has its layout M copy
+  void* xa16 = nullptr;      // fp16(resid * next norm weight) [17][ld_e]
+  void* h16 = nullptr;       // fp16 GLU output [17][ld_f]
+  void* a16 = nullptr;       // fp16 attention output [17][ld_q]
+  float* st[2] = {nullptr, nullptr};  // sum-of-squares partials [E / 16][16] (after O / after down)
+  int ld_e = 0, ld_f = 0, ld_q = 0;
 };
+constexpr int MB_CHAIN_MAX = 16;
 
 struct StepInputs {
   int B = 0;
@@ -108,10 +117,12 @@ class Executor {
   void forward(const StepInputs& in, hipStream_t s);     // tp == 1 only
   void forward_tp(const StepInputs& in, hipStream_t s);  // tp > 1, custom all-reduce (graph-capturable)
   bool ar_fits(int B) const;                             // decode batch B fits the AR slabs
+  bool chain_capable() const;                            // every projection takes the fp16 matrix-core chain
   StepInputs bound{};                                    // pre-bound step inputs (set_inputs)
 
  private:
   float* tp_dst(int slab, int B) const;  // where a row-parallel projection leaves its partial sums
+  bool chain(const StepInputs& in) const;  // this step runs the fp16 matrix-core decode chain
   QMat next_qkv(int i) const;          // the matrix the GEMV after layer i's FFN streams (prefetch target)
   int ar_active_ = 0;
 };

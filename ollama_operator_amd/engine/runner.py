@@ -65,7 +65,7 @@ class NativeExec:
                              moe_rows=p(r.moe_rows) if cfg.n_expert else 0, moe_tiles=p(r.moe_tiles),
                              moe_ntiles=p(r.moe_ntiles),
                              gws_elems=r.gws.numel(), max_B=r.max_batch, ld_logits=r.logits.shape[1],
-                             n_splits=1))
+                             n_splits=1, **self._chain_ws(r)))
         # step buffers bound once: every stage call below passes integers only
         e.set_inputs(dict(tokens=p(r.d_tokens), pos=p(r.d_pos), slot=p(r.d_slot), q_len=p(r.d_qlen),
                           q_seq=p(r.d_qseq), block_table=p(r.d_block_table), max_blocks=r.max_blocks,
@@ -75,6 +75,17 @@ class NativeExec:
             e.set_ar(r.ar.params)
         self.stages = dict(forward=C.ST_FORWARD, embed=C.ST_EMBED, attn=C.ST_ATTN, ffn=C.ST_FFN, head=C.ST_HEAD,
                            forward_tp=C.ST_FORWARD_TP)
+
+    @staticmethod
+    def _chain_ws(r) -> dict:
+        """The fp16 matrix-core decode chain buffers (the executor enables the chain only when every
+        projection takes the matrix-core kernel: Executor::chain_capable)."""
+        mb = getattr(r, "mb_bufs", None)
+        if not mb:
+            return {}
+        d = {k: v.data_ptr() for k, v in mb.items()}
+        d.update(mb_ok=1, ld_e=mb["xa16"].shape[1], ld_f=mb["h16"].shape[1], ld_q=mb["a16"].shape[1])
+        return d
 
     def ar_fits(self, B: int) -> bool:
         return self.exe.ar_fits(B)
@@ -127,6 +138,11 @@ class Runner:
         # TP serving (parallel/tp.py): rank 0 signals each decode step, followers mirror it
         self.tp_ctrl = tp_ctrl
         self.w = weights or DeviceWeights(model_path, self.device, tp_rank, tp_size)
+        # continuous batching on the matrix cores (gemv_mfma.hip): layout M weight copies, built on the
+        # device, whenever this runner can batch sequences (OMX_MFMA_BATCH=0 keeps the int8 GEMV only)
+        self.mfma_bytes = 0
+        if self.is_gpu and max_seqs > 1 and os.environ.get("OMX_MFMA_BATCH", "1") != "0":
+            self.mfma_bytes = self.w.build_mfma_layouts()
         cfg = self.cfg = self.w.cfg
         loc = self.w.local
         self.max_batch = max_batch
@@ -158,6 +174,15 @@ class Runner:
         self.ew = torch.zeros(max_batch, ksel, **f32)
         # fp16 activations for the prefill MFMA GEMM (any GEMM input: E, H*D, F, k*F wide)
         self.x16 = torch.zeros(max_batch * max(E, Eq, ksel * Fl, ksel * E), device=dev, dtype=torch.float16)
+        # batched decode chain on the matrix cores (executor.cpp chain(): 2 <= B <= 16): fp16 activation
+        # rows [17][ld] (row 16 stays zero) + RMS sum-of-squares partial slabs
+        self.mb_bufs = None
+        if self.mfma_bytes:
+            r256 = lambda n: (n + 255) // 256 * 256  # noqa: E731
+            h16 = dict(device=dev, dtype=torch.float16)
+            self.mb_bufs = dict(xa16=torch.zeros(17, r256(E), **h16), h16=torch.zeros(17, r256(Fl), **h16),
+                                a16=torch.zeros(17, r256(Eq), **h16), st0=torch.zeros((E + 15) // 16 * 16, **f32),
+                                st1=torch.zeros((E + 15) // 16 * 16, **f32))
         # MoE prefill grouping (csrc/kernels/moe.hip moe_sort -> grouped MFMA GEMM)
         n_pairs = max_batch * ksel
         self.moe_rows = torch.zeros(n_pairs, **i32)

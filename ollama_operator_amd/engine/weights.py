@@ -41,12 +41,28 @@ class DevQMat:
     streams: list[torch.Tensor] = field(default_factory=list)
     # Q6_K only, GPU: codes widened to signed int8 at load for the batch-1 GEMV (qmat.h QT_Q6_K8)
     wide: torch.Tensor | None = None
+    # GPU, continuous batching: layout M copy for the matrix-core batched decode GEMV (gemv_mfma.hip)
+    mt: torch.Tensor | None = None
 
     @property
     def tup(self) -> tuple:
         p = [s.data_ptr() for s in self.streams] + [0] * (4 - len(self.streams))
         t = (p[0], p[1], p[2], p[3], self.N, self.K, int(self.qtype))
+        if self.mt is not None:
+            return t + (self.wide.data_ptr() if self.wide is not None else 0, self.mt.data_ptr())
         return t + (self.wide.data_ptr(),) if self.wide is not None else t
+
+    def build_mfma_layout(self) -> int:
+        """Layout M copy (gemv_mfma.hip `repack_m`, built on the device from the v2 streams) for the
+        batched decode GEMV; returns its bytes (0: this quant type has no layout M)."""
+        from ..ops import native, stream_handle
+        if self.mt is not None:
+            return self.mt.numel()
+        n = native().mfma_layout_bytes(int(self.qtype), self.N, self.K)
+        if n:
+            self.mt = torch.empty(n, dtype=torch.uint8, device=self.streams[0].device)
+            native().repack_m(self.tup, self.mt.data_ptr(), stream_handle())
+        return n
 
     @property
     def nbytes(self) -> int:
@@ -293,6 +309,16 @@ class DeviceWeights:
         # the GGUF mapping (and any requantised copies) is no longer needed: dropping it releases the
         # file's resident pages (a CPU server would otherwise hold the blob twice in RSS)
         self.src = None
+
+    def build_mfma_layouts(self) -> int:
+        """Layout M copies of every dense projection (+ LM head) for continuous-batching decode steps
+        on the matrix cores; MoE expert stacks keep the routed int8 GEMV. Returns the bytes added."""
+        n = self.lm_head.build_mfma_layout()
+        for L in self.layers:
+            for k, v in L.items():
+                if isinstance(v, DevQMat) and k not in ("gu_exps", "down_exps"):
+                    n += v.build_mfma_layout()
+        return n
 
     @property
     def nbytes(self) -> int:
