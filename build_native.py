@@ -57,24 +57,36 @@ def _needs(obj: str, src: str, hdr_mtime: float) -> bool:
     return m < os.path.getmtime(src) or m < hdr_mtime
 
 
-def build(jobs: int | None = None, clean: bool = False, verbose: bool = False) -> str:
+DEBUG_BUILD = os.path.join(ROOT, "build", "debug")
+DEBUG_FLAGS = ["-O1", "-g", "-DOMX_DEBUG_KERNELS"]
+
+
+def build(jobs: int | None = None, clean: bool = False, verbose: bool = False, debug: bool = False,
+          sources: list[str] | None = None) -> str:
+    """debug: the in-kernel bounds assertions (OMX_KASSERT) and -O1 -g, objects in build/debug and the
+    module in build/debug/ollama_operator_amd (put that directory first on sys.path to load it).
+    sources: compile only these csrc-relative translation units (no link), e.g. for a build check."""
     import pybind11
-    os.makedirs(BUILD, exist_ok=True)
+    build_dir = DEBUG_BUILD if debug else BUILD
+    os.makedirs(build_dir, exist_ok=True)
     if clean:
-        for f in glob.glob(os.path.join(BUILD, "*.o")):
+        for f in glob.glob(os.path.join(build_dir, "*.o")):
             os.remove(f)
     srcs = sorted(s for s in glob.glob(os.path.join(CSRC, "**", "*.hip"), recursive=True) +
                   glob.glob(os.path.join(CSRC, "**", "*.cpp"), recursive=True)
                   if not s.startswith(CPU_SRC + os.sep))  # the CPU backend is its own module (build_cpu)
     hdr_mtime = max((os.path.getmtime(h) for h in _headers()), default=0.0)
     py_inc = sysconfig.get_paths()["include"]
-    common = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", CSRC,
+    if sources is not None:
+        srcs = [os.path.join(CSRC, x) for x in sources]
+    opt = DEBUG_FLAGS if debug else ["-O3"]
+    common = [*opt, "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", CSRC,
               "-I", pybind11.get_include(), "-I", py_inc, "-Wno-unused-result"]
     jobs_list = []
     objs = []
     for s in srcs:
         rel = os.path.relpath(s, CSRC).replace(os.sep, "_")
-        obj = os.path.join(BUILD, rel + ".o")
+        obj = os.path.join(build_dir, rel + ".o")
         objs.append(obj)
         if _needs(obj, s, hdr_mtime):
             if s.endswith(".hip"):
@@ -102,7 +114,12 @@ def build(jobs: int | None = None, clean: bool = False, verbose: bool = False) -
         for s, out, cmd in failed:
             sys.stderr.write(f"--- {s}\n{cmd}\n{out}\n")
         raise RuntimeError(f"native build failed ({len(failed)} translation units)")
+    if sources is not None:
+        return build_dir
     out = target_path()
+    if debug:
+        os.makedirs(os.path.join(build_dir, "ollama_operator_amd"), exist_ok=True)
+        out = os.path.join(build_dir, "ollama_operator_amd", os.path.basename(out))
     if not os.path.exists(out) or jobs_list or any(os.path.getmtime(o) > os.path.getmtime(out) for o in objs):
         link = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", out, *objs, "-lpthread"]
         tl = _torch_lib()
@@ -145,7 +162,10 @@ if __name__ == "__main__":
     ap.add_argument("--clean", action="store_true")
     ap.add_argument("--jobs", type=int, default=None)
     ap.add_argument("--cpu-only", action="store_true", help="build only the CPU backend module")
+    ap.add_argument("--debug", action="store_true",
+                    help="kernels with in-kernel bounds assertions (OMX_KASSERT), -O1 -g, into build/debug")
     a = ap.parse_args()
-    print(build_cpu(verbose=True))
+    if not a.debug:
+        print(build_cpu(verbose=True))
     if not a.cpu_only:
-        print(build(a.jobs, a.clean, verbose=True))
+        print(build(a.jobs, a.clean, verbose=True, debug=a.debug))

@@ -277,6 +277,19 @@ PYBIND11_MODULE(_C, m) {
   m.def("argmax", [](uintptr_t logits, int B, int V, int ld, uintptr_t out, uintptr_t stream) {
     argmax(Pp<const float>(logits), B, V, ld, Pp<int>(out), S(stream));
   });
+  m.def("moe_router", [](py::object wq, int B, uintptr_t x, int ldx, uintptr_t norm_w, float eps, int k, uintptr_t ids,
+                         uintptr_t w, uintptr_t stream) {
+    GemvParams P{};
+    P.w = qmat(wq);
+    if (P.w.N > 64 || k < 1 || k > P.w.N) throw std::runtime_error("moe_router: X <= 64 experts, 1 <= k <= X");
+    P.B = B;
+    P.x = Pp<const float>(x);
+    P.ldx = ldx;
+    P.norm = norm_w ? NORM_RMS : NORM_NONE;
+    P.norm_w = Pp<const float>(norm_w);
+    P.eps = eps;
+    moe_router(P, k, Pp<int>(ids), Pp<float>(w), S(stream));
+  });
   m.def("moe_route", [](uintptr_t logits, int B, int X, int k, uintptr_t ids, uintptr_t w, uintptr_t stream) {
     moe_route(Pp<const float>(logits), B, X, k, Pp<int>(ids), Pp<float>(w), S(stream));
   });

@@ -138,6 +138,7 @@ __global__ __launch_bounds__(ATT_NT) void attn_decode_kernel(AttnParams P) {
     const int w1 = min(t1, w0 + ATT_BTW * bs);
     const int b0 = w0 / bs, nb = (w1 - 1) / bs - b0 + 1;
     __syncthreads();  // previous window's readers are done with sbt
+    OMX_KASSERT(nb <= ATT_BTW && b0 + nb <= P.max_blocks);
     for (int i = threadIdx.x; i < nb; i += ATT_NT) sbt[i] = bt[b0 + i];
     __syncthreads();
 
@@ -146,6 +147,7 @@ __global__ __launch_bounds__(ATT_NT) void attn_decode_kernel(AttnParams P) {
       for (int u = 0; u < ATT_U; ++u) {
         const int t = min(ts + u * ATT_NG + grp, w1 - 1);  // clamped; masked at use
         const long long blk = sbt[t / bs - b0];
+        OMX_KASSERT(t >= 0 && t / bs - b0 < nb && blk >= 0);
         const long long base = ((blk * P.n_kv + kvh) * bs + (t % bs)) * D + li * DPL;
         load_krow<DPL>(kc + base, st.k[u]);
         load_krow<DPL>(vc + base, st.v[u]);

@@ -6,6 +6,16 @@
 
 #define OMX_WAVE 64
 
+// In-kernel bounds assertions: compiled in only by the debug build
+// (`python build_native.py --debug`: -DOMX_DEBUG_KERNELS -O1 -g, a separate in-tree build directory);
+// a failing check prints the condition with the block / thread and aborts the kernel (device assert).
+#ifdef OMX_DEBUG_KERNELS
+#include <cassert>
+#define OMX_KASSERT(c) assert(c)
+#else
+#define OMX_KASSERT(c) ((void)0)
+#endif
+
 typedef _Float16 f16;
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));

@@ -821,6 +821,7 @@ static void pf_filter(GemvParams& P) {
 }
 
 void gemv2(const GemvParams& A0, const GemvParams& B0, hipStream_t s) {
+  if (A0.B > 1 && gemv_mb2(A0, B0, s)) return;  // batched decode chain: q,k + v on the matrix cores
   GemvParams A = A0, Bp = B0;
   A.xfirst = Bp.xfirst = g_tune.xfirst;
   pf_filter(A);

@@ -66,6 +66,7 @@ __device__ __forceinline__ void load_wtile(const QMat& w, long long row_base, in
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     const long long row = row_base + min(row0 + r, N - 1);
+    OMX_KASSERT(row >= 0 && sb0 + s < SB + 16 * NSB);
 #pragma unroll
     for (int i = 0; i < NSB; ++i) {
       const long long sb = min(sb0 + s + 16 * i, se - 1);  // clamped: padding lanes re-read, never use

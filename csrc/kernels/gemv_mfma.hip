@@ -46,6 +46,7 @@ typedef _Float16 mh2 __attribute__((ext_vector_type(2)));
 constexpr int MB_NW = 8;         // waves per block
 constexpr int MB_NT = 64 * MB_NW;
 constexpr int MB_BMAX = 16;      // batch rows per MFMA (A-operand rows)
+constexpr int MB_BMIN = 3;       // smallest batch taken (profiles/r3_batch)
 constexpr unsigned MB_MAGIC = 0x64006400u;  // fp16 1024.0 in both halves
 constexpr int MB_SPL = 12;       // RMS partials per lane: producers of up to 64 * 12 row tiles (E <= 12288)
 
@@ -286,6 +287,7 @@ __device__ __forceinline__ void mb_load_rec(const QMat& w, int tile, int SB, int
                                             MUnit<QT, NR, CA>& U) {
   constexpr int REC = mb_rec_bytes(QT), CODE = mb_code_bytes(QT);
   const int j = lane & 15, q = lane >> 4;
+  OMX_KASSERT(tile >= 0 && tile < (w.N + 15) / 16 && sb >= 0 && sb < SB);
   const uint8_t* R = w.mt + ((long long)tile * SB + sb) * REC;
 #pragma unroll
   for (int c = 0; c < MUnit<QT, NR, CA>::NC; ++c)
@@ -303,6 +305,13 @@ __device__ __forceinline__ void mb_load_rec(const QMat& w, int tile, int SB, int
 __device__ __forceinline__ void mb_load_a(const f16* xg, int sb, f16x8 (&a)[8]) {
 #pragma unroll
   for (int s = 0; s < 8; ++s) a[s] = *(const f16x8*)(xg + sb * 256 + 32 * s);
+}
+
+// (a & m) | o in one VALU op (hipcc emits v_and + v_or for the C expression)
+__device__ __forceinline__ unsigned and_or(unsigned a, unsigned m, unsigned o) {
+  unsigned r;
+  asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(m), "v"(o));
+  return r;
 }
 
 __device__ __forceinline__ unsigned sel4(const u32x4& v, int i) {
@@ -328,17 +337,17 @@ __device__ __forceinline__ f16x8 mb_deq(const u32x4* c, mh2 sc, mh2 mn) {
     r.w = asu2((ash2(__builtin_amdgcn_perm(0x64646464u, f1, 0x04030402u)) - off) * sc);
   } else {
     const unsigned wd = sel4(c[S >> 2], S & 3);
-    unsigned u0 = (wd & 0x000F000Fu) | MB_MAGIC;
-    unsigned u1 = ((wd >> 8) & 0x000F000Fu) | MB_MAGIC;
-    unsigned u2 = ((wd >> 4) & 0x000F000Fu) | MB_MAGIC;
-    unsigned u3 = ((wd >> 12) & 0x000F000Fu) | MB_MAGIC;
+    unsigned u0 = and_or(wd, 0x000F000Fu, MB_MAGIC);
+    unsigned u1 = and_or(wd >> 8, 0x000F000Fu, MB_MAGIC);
+    unsigned u2 = and_or(wd >> 4, 0x000F000Fu, MB_MAGIC);
+    unsigned u3 = and_or(wd >> 12, 0x000F000Fu, MB_MAGIC);
     if constexpr (QT == QT_Q6_K) {  // high bits of pair k at bits 2i / 16 + 2i of H, i = 4 (S & 1) + k
       const unsigned H = sel4(c[2], S >> 1);
       constexpr int I = 4 * (S & 1);
-      u0 |= shr<2 * I - 4>(H) & 0x00300030u;
-      u1 |= shr<2 * I - 2>(H) & 0x00300030u;
-      u2 |= shr<2 * I>(H) & 0x00300030u;
-      u3 |= shr<2 * I + 2>(H) & 0x00300030u;
+      u0 = and_or(shr<2 * I - 4>(H), 0x00300030u, u0);
+      u1 = and_or(shr<2 * I - 2>(H), 0x00300030u, u1);
+      u2 = and_or(shr<2 * I>(H), 0x00300030u, u2);
+      u3 = and_or(shr<2 * I + 2>(H), 0x00300030u, u3);
       const mh2 off = {(f16)1056.f, (f16)1056.f};  // 1024 + 32 (Q6_K codes are q - 32)
       r.x = asu2((ash2(u0) - off) * sc);
       r.y = asu2((ash2(u1) - off) * sc);
@@ -464,7 +473,7 @@ static size_t mb_lds_bytes(int B, int K, int am) {
 // across the barrier), meets the block, and waves 0..3 sum the 8 partials in wave order (deterministic)
 // and run the fused epilogue, one output per lane each.
 template <int QT, int NSBW, int RD, int AM, int DBG = 0>
-__global__ __launch_bounds__(MB_NT) void gemv_mb_kernel(GemvParams P) {
+__device__ __forceinline__ void mb_body(const GemvParams& P, const int bx, const int gxn) {
   constexpr bool TU = NSBW <= 2;
   constexpr int NR = TU ? NSBW : 1;
   constexpr bool G16 = AM == AM_G16;
@@ -482,7 +491,7 @@ __global__ __launch_bounds__(MB_NT) void gemv_mb_kernel(GemvParams P) {
   const int sb0 = wave * SB / MB_NW, sb1 = (wave + 1) * SB / MB_NW, nsb = sb1 - sb0;
   const int last_sb = nsb > 0 ? sb1 - 1 : min(sb0, SB - 1);  // surplus loads re-read it (cache hits)
   const int n_tiles = (N + 15) >> 4;
-  const int my_tiles = (int)blockIdx.x < n_tiles ? (n_tiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+  const int my_tiles = bx < n_tiles ? (n_tiles - 1 - bx) / gxn + 1 : 0;
   const int upt = TU ? 1 : nsb;  // units per tile
   const int n_units = my_tiles * upt;
   const bool av = j < B;         // A-operand lane: batch row j
@@ -571,17 +580,20 @@ __global__ __launch_bounds__(MB_NT) void gemv_mb_kernel(GemvParams P) {
   }
 
   // 3. the first RD units in flight (epilogue operands first: they are needed only after the weights)
-  auto unit_tile = [&](int u) { return (int)blockIdx.x + (TU ? u : u / (nsb > 0 ? nsb : 1)) * (int)gridDim.x; };
+  auto unit_tile = [&](int u) { return bx + (TU ? u : u / (nsb > 0 ? nsb : 1)) * gxn; };
   auto load_unit = [&](MUnit<QT, NR, CA>& U, int u) {
-    u = min(u, n_units - 1);  // surplus refills re-read the last unit (cache hits, never computed)
+    // surplus slots (past the wave's last unit) re-read one line of the last unit: every lane the same
+    // address, so a surplus load instruction costs one cache line (never computed)
+    const int ln = u < n_units ? lane : 0;
+    u = min(u, n_units - 1);
     const int t = unit_tile(u);
     mb_epi_load(P, t, U.eo);
     if constexpr (TU) {
 #pragma unroll
-      for (int r = 0; r < NR; ++r) mb_load_rec<QT, NR, CA>(w, t, SB, min(sb0 + r, last_sb), r, lane, U);
+      for (int r = 0; r < NR; ++r) mb_load_rec<QT, NR, CA>(w, t, SB, min(sb0 + r, last_sb), r, ln, U);
     } else {
       const int sb = sb0 + u % nsb;
-      mb_load_rec<QT, NR, CA>(w, t, SB, sb, 0, lane, U);
+      mb_load_rec<QT, NR, CA>(w, t, SB, sb, 0, ln, U);
       if constexpr (CA) mb_load_a(xg, sb, U.a);
     }
     __builtin_amdgcn_sched_barrier(0);  // issue order = consumption order (vmcnt retires in order)
@@ -615,6 +627,7 @@ __global__ __launch_bounds__(MB_NT) void gemv_mb_kernel(GemvParams P) {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     if (wave >= 4 || (DBG & 4)) return;  // wave-uniform
     const int r = wave, b = 4 * q + r;  // this lane's output: row j, batch row 4 q + r
+    OMX_KASSERT(tile >= 0 && tile < n_tiles && B <= MB_BMAX);
     float x = 0.f;
 #pragma unroll
     for (int i = 0; i < MB_NW; ++i) x += rb[(i * 64 + lane) * 4 + r];
@@ -642,8 +655,8 @@ __global__ __launch_bounds__(MB_NT) void gemv_mb_kernel(GemvParams P) {
   if (!TU && nsb == 0) {  // no super-blocks in this wave (K < 2048): zero partials
     for (int t = 0; t < my_tiles; ++t) {
       float eo[MB_EO];
-      mb_epi_load(P, (int)blockIdx.x + t * (int)gridDim.x, eo);
-      finish((f32x4){0.f, 0.f, 0.f, 0.f}, (int)blockIdx.x + t * (int)gridDim.x, eo);
+      mb_epi_load(P, bx + t * gxn, eo);
+      finish((f32x4){0.f, 0.f, 0.f, 0.f}, bx + t * gxn, eo);
     }
     return;
   }
@@ -697,6 +710,19 @@ __global__ __launch_bounds__(MB_NT) void gemv_mb_kernel(GemvParams P) {
 #pragma unroll
   for (int r = 0; r < RD; ++r)
     if (u + r < n_units) step(U[r], u + r);  // wave-uniform
+}
+
+template <int QT, int NSBW, int RD, int AM, int DBG = 0>
+__global__ __launch_bounds__(MB_NT) void gemv_mb_kernel(GemvParams P) {
+  mb_body<QT, NSBW, RD, AM, DBG>(P, blockIdx.x, gridDim.x);
+}
+
+// two matrices over the same activations in ONE launch (the Q4_K_M QKV: q,k rows Q4_K + v rows
+// Q6_K): blocks [0, ga) run A, the rest B -- one launch ramp / drain instead of two
+template <int QA, int QB, int NSBW, int RD, int AM>
+__global__ __launch_bounds__(MB_NT) void gemv_mb2_kernel(GemvParams PA, GemvParams PB, int ga) {
+  if ((int)blockIdx.x < ga) mb_body<QA, NSBW, RD, AM>(PA, blockIdx.x, ga);
+  else mb_body<QB, NSBW, RD, AM>(PB, (int)blockIdx.x - ga, (int)gridDim.x - ga);
 }
 
 static int mb_cu_count() {
@@ -761,7 +787,8 @@ static bool mb_q(const GemvParams& P, size_t lds, hipStream_t s) {
 static int mb_am(const GemvParams& P) { return P.x16 ? AM_G16 : AM_LDS; }
 
 bool gemv_mb_supported(const GemvParams& P) {
-  if (!g_mb_enable || !P.w.mt || P.B < 2 || P.B > MB_BMAX || P.expert_ids || P.merge_S) return false;
+  // B = 2 stays on the int8 GEMV (gemv_batch.hip): measured 2.08 vs 2.15 ms per Llama-2-7B step
+  if (!g_mb_enable || !P.w.mt || P.B < MB_BMIN || P.B > MB_BMAX || P.expert_ids || P.merge_S) return false;
   if (g_tune.debug) return false;
   const int q = P.w.qtype;
   if (q != QT_Q4_K && q != QT_Q6_K && q != QT_Q4_0 && q != QT_Q8_0) return false;
@@ -775,6 +802,33 @@ bool gemv_mb_supported(const GemvParams& P) {
     return false;
   }
   return mb_lds_bytes(P.B, P.w.K, am) <= 160 * 1024;
+}
+
+// the QKV pair of a K-quant mix in one launch (gemv2 at B > 1): blocks split in proportion to bytes
+bool gemv_mb2(const GemvParams& A, const GemvParams& Bp, hipStream_t s) {
+  if (!gemv_mb_supported(A) || !gemv_mb_supported(Bp) || A.w.K != Bp.w.K || A.B != Bp.B) return false;
+  if (mb_am(A) != AM_G16 || mb_am(Bp) != AM_G16 || g_mb_dbg) return false;
+  if (A.w.qtype != QT_Q4_K || Bp.w.qtype != QT_Q6_K) return false;
+  const int SB = n_sb_host(A.w.K), nsbw = (SB + MB_NW - 1) / MB_NW;
+  if (nsbw > 2) return false;
+  const int ta = (A.w.N + 15) / 16, tb = (Bp.w.N + 15) / 16, ncu = mb_cu_count();
+  const double ba = (double)ta * mb_rec_bytes(QT_Q4_K), bb = (double)tb * mb_rec_bytes(QT_Q6_K);
+  int ga = (int)(ncu * ba / (ba + bb) + 0.5);
+  ga = ga < 1 ? 1 : ga > ta ? ta : ga;
+  int gb = ncu - ga;
+  gb = gb < 1 ? 1 : gb > tb ? tb : gb;
+  const size_t lds = mb_lds_bytes(A.B, A.w.K, AM_G16);
+  auto go = [&](auto kern) {
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      attr = true;
+    }
+    hipLaunchKernelGGL(kern, dim3(ga + gb), dim3(MB_NT), lds, s, A, Bp, ga);
+  };
+  if (nsbw == 1) go(gemv_mb2_kernel<QT_Q4_K, QT_Q6_K, 1, 4, AM_G16>);
+  else go(gemv_mb2_kernel<QT_Q4_K, QT_Q6_K, 2, 3, AM_G16>);
+  return true;
 }
 
 bool gemv_mb(const GemvParams& P, hipStream_t s) {

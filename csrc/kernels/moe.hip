@@ -32,6 +32,71 @@ void moe_route(const float* logits, int B, int X, int k, int* ids, float* w, hip
   hipLaunchKernelGGL(moe_route_kernel, dim3((B + 63) / 64), dim3(64), 0, s, logits, B, X, k, ids, w);
 }
 
+// Fused router (decode and prefill): RMSNorm + router logits + softmax top-k + renormalised weights in
+// ONE launch, one 256-thread block per token. Replaces the router GEMV + moe_route pair (two launches,
+// the logits' round trip through memory: 5.5 + 4.8 us per layer on Mixtral, profiles/r2_models). The
+// X <= 64 logits are exact fp32 dots of the dequantised router rows with the fp32 normalised token
+// (dequant_piece), the experts one wave each in turn; wave 0 then holds logit e in lane e and draws the
+// k largest by wave argmax (lowest index among equals, as moe_route_kernel).
+constexpr int ROUTER_NT = 256;
+__global__ __launch_bounds__(ROUTER_NT) void moe_router_kernel(GemvParams P, int k, int* ids, float* wout) {
+  __shared__ float red[ROUTER_NT / 64];
+  __shared__ float lg[64];
+  const int b = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const QMat& W = P.w;
+  const int K = W.K, X = W.N, SB = n_sb(K);
+  const float* x = P.x + (long long)b * P.ldx;
+  float ss = 0.f;
+  for (int i = tid; i < K / 4; i += ROUTER_NT) {
+    const f32x4 v = *(const f32x4*)(x + 4 * i);
+    ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+  }
+  ss = block_sum<ROUTER_NT>(ss, red);
+  const float rstd = P.norm == NORM_RMS ? rsqrtf(ss / K + P.eps) : 1.f;
+  const int n_pieces = SB * 8;  // 32-weight pieces per row (K padded to whole super-blocks)
+  for (int e = wave; e < X; e += ROUTER_NT / 64) {
+    float acc = 0.f;
+    for (int p = lane; p < n_pieces; p += 64) {
+      float lo[16], hi[16];
+      int olo, ohi;
+      dequant_piece(W, e, p, lo, hi, olo, ohi);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        if (olo + i < K) acc += lo[i] * x[olo + i] * (P.norm_w ? P.norm_w[olo + i] : 1.f);
+        if (ohi + i < K) acc += hi[i] * x[ohi + i] * (P.norm_w ? P.norm_w[ohi + i] : 1.f);
+      }
+    }
+    acc = wave_sum(acc);
+    if (lane == 0) lg[e] = acc * rstd;
+  }
+  __syncthreads();
+  if (wave != 0) return;
+  float v = lane < X ? lg[lane] : -INFINITY;
+  const float mx = wave_max(v);
+  float tot = 0.f, mine = 0.f;
+  int rank = -1;
+  for (int j = 0; j < k; ++j) {
+    const float bv = wave_max(v);
+    const unsigned long long hit = __ballot(v == bv && lane < X);
+    const int best = hit ? __ffsll((long long)hit) - 1 : 0;
+    const float pr = __expf(bv - mx);
+    tot += pr;
+    if (lane == best) {
+      rank = j;
+      mine = pr;
+      v = -INFINITY;  // drawn
+    }
+  }
+  if (rank >= 0) {
+    ids[b * k + rank] = lane;
+    wout[b * k + rank] = mine / tot;
+  }
+}
+
+void moe_router(const GemvParams& P, int k, int* ids, float* w, hipStream_t s) {
+  hipLaunchKernelGGL(moe_router_kernel, dim3(P.B), dim3(ROUTER_NT), 0, s, P, k, ids, w);
+}
+
 __global__ void gather_rows_kernel(const float* x, int ld, const int* idx, int n, float* out) {
   const long long r = blockIdx.x;
   const float* src = x + (long long)idx[r] * ld;

@@ -92,6 +92,7 @@ constexpr int GEMM_MIN_B = 16;
 // batched decode GEMV on the matrix cores (gemv_mfma.hip): 2 <= B <= 16 rows, needs the layout M
 // copy (QMat::mt) built by repack_m; false = shape not covered (the caller takes the int8 GEMV)
 bool gemv_mb(const GemvParams& P, hipStream_t s);
+bool gemv_mb2(const GemvParams& A, const GemvParams& B, hipStream_t s);  // two matrices, one launch
 bool gemv_mb_supported(const GemvParams& P);
 void set_mb_enable(int on);
 void set_mb_tuning(int dbg, int bpc);  // microbenchmark variants (gemv_mfma.hip DBG), blocks per CU
@@ -178,6 +179,8 @@ void sample(const SampleParams& P, hipStream_t s);
 void argmax(const float* logits, int B, int V, int ld, int* out, hipStream_t s);
 
 void moe_route(const float* logits, int B, int X, int k, int* ids, float* w, hipStream_t s);
+// fused RMSNorm + router logits + top-k softmax (P.w = router [X <= 64][K], P.x = resid, P.norm_w)
+void moe_router(const GemvParams& P, int k, int* ids, float* w, hipStream_t s);
 void gather_rows(const float* x, int ld, const int* idx, int rows, int n, float* out, hipStream_t s);
 void moe_sort(const int* eids, int n_pairs, int X, int* rows, int* tiles, int* n_tiles, int tile_m, hipStream_t s);
 // grouped dequant GEMM over expert-homogeneous row tiles (P.moe_* set; P.B = number of pairs)

@@ -24,7 +24,7 @@ static GemvParams base_params(const QMat& w, int B, const float* x, int ldx, con
 // the consumer (gate_up, next QKV, LM head) reads them straight from global memory and applies
 // rsqrt(mean + eps) to its outputs -- no per-block activation staging, no separate norm launch.
 bool Executor::chain(const StepInputs& in) const {
-  return ws.mb_ok && mb_enabled() && in.B >= 2 && in.B <= MB_CHAIN_MAX && !in.prefill && cfg.tp == 1 && cfg.arch == 0 &&
+  return ws.mb_ok && mb_enabled() && in.B >= 3 && in.B <= MB_CHAIN_MAX && !in.prefill && cfg.tp == 1 && cfg.arch == 0 &&
          cfg.n_expert == 0 && ws.xa16 && ws.h16 && ws.a16 && ws.st[0] && ws.st[1];
 }
 
@@ -51,7 +51,7 @@ bool Executor::chain_capable() const {
   auto ok = [&](const QMat& w, int epi, int norm, bool x16, bool emit) {
     GemvParams P{};
     P.w = w;
-    P.B = 2;
+    P.B = 4;
     P.epi = epi;
     P.norm = norm;
     P.n_sel = 1;
@@ -198,11 +198,15 @@ void Executor::ffn_block(int i, const StepInputs& in, hipStream_t s) {
     R.norm = NORM_RMS;
     R.norm_w = L.ffn_norm;
     R.eps = cfg.eps;
-    R.epi = EPI_STORE;
-    R.y = ws.rlogits;
-    R.ldy = X;
-    gemv(R, s);
-    moe_route(ws.rlogits, B, X, k, ws.eids, ws.ew, s);
+    if (X <= 64) {  // one fused launch: norm + router logits + top-k (moe.hip moe_router)
+      moe_router(R, k, ws.eids, ws.ew, s);
+    } else {
+      R.epi = EPI_STORE;
+      R.y = ws.rlogits;
+      R.ldy = X;
+      gemv(R, s);
+      moe_route(ws.rlogits, B, X, k, ws.eids, ws.ew, s);
+    }
     if (B >= GEMM_MIN_B && ws.x16 && ws.moe_rows) {
       // prefill: grouped MFMA GEMM over expert-homogeneous tiles of the sorted (token, expert)
       // pairs -- each expert's weights stream once per 128 routed rows, not once per pair

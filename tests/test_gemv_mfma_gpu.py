@@ -29,7 +29,7 @@ class QMM(QM):
 
 
 @pytest.mark.parametrize("qt", MB_TYPES)
-@pytest.mark.parametrize("B", [2, 4, 7, 16])
+@pytest.mark.parametrize("B", [3, 4, 7, 16])
 @pytest.mark.parametrize("K", [256, 2080, 4096, 11008])
 def test_mb_store(qt, B, K):
     if K == 2080 and qt in (GGMLType.Q4_K, GGMLType.Q6_K):
@@ -133,7 +133,7 @@ def test_mb_layout_bytes():
     assert C().mfma_layout_bytes(int(GGMLType.Q5_K), 4096, 4096) == 0
 
 
-@pytest.mark.parametrize("B", [2, 4, 8, 16])
+@pytest.mark.parametrize("B", [3, 4, 8, 16])
 def test_mb_engine_batched_decode(tiny_models, B):
     """Engine level: a continuous-batching step with layout M equals the int8-GEMV step."""
     from ollama_operator_amd.engine.runner import Runner
@@ -170,7 +170,7 @@ def f16_rows(x, ld, zero_rows=1):
 
 
 @pytest.mark.parametrize("qt", MB_TYPES)
-@pytest.mark.parametrize("B,K", [(2, 4096), (5, 4096), (16, 2048), (4, 11008), (9, 11008)])
+@pytest.mark.parametrize("B,K", [(3, 4096), (5, 4096), (16, 2048), (4, 11008), (9, 11008)])
 def test_mb_fp16_input_with_rms_partials(qt, B, K):
     """Consumer side of the chain: activations fp16(x * norm_w) from global memory, the RMSNorm scale
     from per-16-row sum-of-squares partials (as a producer's epilogue leaves them)."""
@@ -180,8 +180,8 @@ def test_mb_fp16_input_with_rms_partials(qt, B, K):
     nw = torch.rand(K, device="cuda") + 0.5
     ld = (K + 255) // 256 * 256
     x16 = f16_rows(x * nw, ld)
-    parts = torch.zeros(K // 16, 16, device="cuda")
-    parts[:, :B] = x.pow(2).reshape(B, K // 16, 16).sum(-1).T
+    parts = torch.zeros(16, K // 16, device="cuda")  # [batch row][16-row tile] as producers write them
+    parts[:B] = x.pow(2).reshape(B, K // 16, 16).sum(-1)
     y = torch.zeros(B, N, device="cuda")
     gemv(m, x, norm=1, nw=nw, y=y, extra=dict(x16=x16.data_ptr(), ld16=ld, zrow16=B, xstat=parts.data_ptr(),
                                               xstat_n=K // 16))
@@ -200,16 +200,16 @@ def test_mb_residual_emission(B):
     resid = resid0.clone()
     nw_next = torch.rand(N, device="cuda") + 0.5
     e16 = torch.zeros(B + 1, N, device="cuda", dtype=torch.float16)
-    st = torch.full((N // 16, 16), -1.0, device="cuda")
+    st = torch.full((16, N // 16), -1.0, device="cuda")
     gemv(m, x, epi=1, y=resid, extra=dict(emit16=e16.data_ptr(), ld_emit=N, emit_nw=nw_next.data_ptr(),
                                           emit_stat=st.data_ptr()))
     ref = resid0 + x @ m.w.T
     assert rel(resid, ref) < 4e-3
     assert rel(e16[:B].float(), (resid * nw_next)) < 1e-3
     assert float(e16[B].abs().max()) == 0.0
-    got = st[:, :B].sum(0)
+    got = st[:B].sum(1)
     assert torch.allclose(got, resid.pow(2).sum(-1), rtol=1e-4)
-    assert float((st[:, B:] + 1).abs().max()) == 0.0  # rows >= B untouched
+    assert float((st[B:] + 1).abs().max()) == 0.0  # rows >= B untouched
 
 
 def test_mb_chain_matches_fused_norm():
@@ -222,7 +222,7 @@ def test_mb_chain_matches_fused_norm():
     resid = torch.randn(B, E, device="cuda") * 3
     nw = torch.rand(E, device="cuda") + 0.5
     e16 = torch.zeros(B + 1, E, device="cuda", dtype=torch.float16)
-    st = torch.zeros(E // 16, 16, device="cuda")
+    st = torch.zeros(16, E // 16, device="cuda")
     gemv(mo, a, epi=1, y=resid, extra=dict(emit16=e16.data_ptr(), ld_emit=E, emit_nw=nw.data_ptr(),
                                            emit_stat=st.data_ptr()))
     y_chain = torch.zeros(B, F, device="cuda")

@@ -386,3 +386,22 @@ def test_gemv_q6k_widened(K, B):
     gemv(m, x, epi=1, y=y2)
     torch.cuda.synchronize()
     assert rel(y2, res + x @ m.w.T) < 1e-2
+
+
+@pytest.mark.parametrize("qt", [GGMLType.Q8_0, GGMLType.Q4_K, GGMLType.Q6_K])
+@pytest.mark.parametrize("B,X,k", [(1, 8, 2), (5, 8, 2), (3, 16, 4), (2, 60, 6)])
+def test_moe_router_fused(qt, B, X, k):
+    """Fused RMSNorm + router logits + top-k softmax (moe.hip moe_router) against fp32 torch."""
+    K = 1024
+    m = QM(qt, X, K, seed=X + k)
+    x = torch.randn(B, K, device="cuda")
+    nw = torch.rand(K, device="cuda") + 0.5
+    ids = torch.full((B, k), -1, device="cuda", dtype=torch.int32)
+    w = torch.zeros(B, k, device="cuda")
+    C().moe_router(m.tup, B, x.data_ptr(), K, nw.data_ptr(), 1e-5, k, ids.data_ptr(), w.data_ptr(), S())
+    xn = x * torch.rsqrt(x.pow(2).mean(-1, keepdim=True) + 1e-5) * nw
+    logits = xn @ m.w.T
+    top, idx = torch.topk(logits, k, dim=-1)
+    ref_w = torch.softmax(top, dim=-1)
+    assert torch.equal(ids.long(), idx), (ids, idx)
+    assert torch.allclose(w, ref_w, atol=1e-5)
