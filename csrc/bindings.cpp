@@ -288,7 +288,7 @@ PYBIND11_MODULE(_C, m) {
     P.norm = norm_w ? NORM_RMS : NORM_NONE;
     P.norm_w = Pp<const float>(norm_w);
     P.eps = eps;
-    moe_router(P, k, Pp<int>(ids), Pp<float>(w), S(stream));
+    if (!moe_router(P, k, Pp<int>(ids), Pp<float>(w), S(stream))) throw std::runtime_error("moe_router: shape not covered");
   });
   m.def("moe_route", [](uintptr_t logits, int B, int X, int k, uintptr_t ids, uintptr_t w, uintptr_t stream) {
     moe_route(Pp<const float>(logits), B, X, k, Pp<int>(ids), Pp<float>(w), S(stream));

@@ -778,8 +778,9 @@ static bool mb_q(const GemvParams& P, size_t lds, hipStream_t s) {
   const int SB = n_sb_host(P.w.K), nsbw = (SB + MB_NW - 1) / MB_NW;
   switch (nsbw) {
     case 1: mb_launch<QT, 1, 4, AM>(P, lds, s); return true;
-    case 2: mb_launch<QT, 2, 3, AM>(P, lds, s); return true;
-    case 3: case 4: case 5: case 6: case 7: case 8: mb_launch<QT, 8, 3, AM>(P, lds, s); return true;
+    // Q8_0 records are twice the Q4 size: a 3-deep ring spills at these widths, keep 2 units in flight
+    case 2: mb_launch<QT, 2, QT == QT_Q8_0 ? 2 : 3, AM>(P, lds, s); return true;
+    case 3: case 4: case 5: case 6: case 7: case 8: mb_launch<QT, 8, QT == QT_Q8_0 ? 2 : 3, AM>(P, lds, s); return true;
     default: return false;
   }
 }

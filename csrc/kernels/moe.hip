@@ -38,40 +38,90 @@ void moe_route(const float* logits, int B, int X, int k, int* ids, float* w, hip
 // X <= 64 logits are exact fp32 dots of the dequantised router rows with the fp32 normalised token
 // (dequant_piece), the experts one wave each in turn; wave 0 then holds logit e in lane e and draws the
 // k largest by wave argmax (lowest index among equals, as moe_route_kernel).
-constexpr int ROUTER_NT = 256;
+constexpr int ROUTER_NT = 1024;
+constexpr int ROUTER_KMAX = 16384;  // normalised token staged in LDS (72 KiB with the padding below)
+// LDS index of token element o: 4 pad floats after every 32 so that lanes reading consecutive pieces
+// (32 floats apart) spread over the banks instead of all hitting one (a 64-way conflict per ds_read)
+__device__ __forceinline__ int rpad(int o) { return o + (o >> 5) * 4; }
+constexpr int ROUTER_PPT = 2;       // 32-weight pieces per thread: X * K / 32 <= 2048 (X = 8 at K <= 8192)
+// one 1024-thread block per token; thread t owns pieces t, t + 1024 of the flattened (expert, piece)
+// list, all requested before the token's statistics are waited for (a single block is latency-bound:
+// one round trip for x and one for the router rows, not one per expert)
 __global__ __launch_bounds__(ROUTER_NT) void moe_router_kernel(GemvParams P, int k, int* ids, float* wout) {
+  extern __shared__ __attribute__((aligned(16))) float xs[];  // [K padded to whole super-blocks]
   __shared__ float red[ROUTER_NT / 64];
   __shared__ float lg[64];
   const int b = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const QMat& W = P.w;
-  const int K = W.K, X = W.N, SB = n_sb(K);
+  const int K = W.K, X = W.N, SB = n_sb(K), np = SB * 8, total = X * np;
   const float* x = P.x + (long long)b * P.ldx;
-  float ss = 0.f;
-  for (int i = tid; i < K / 4; i += ROUTER_NT) {
+  if (tid < 64) lg[tid] = 0.f;
+  // 1. this thread's token slice and router pieces in flight together
+  f32x4 xv = {0.f, 0.f, 0.f, 0.f};
+  f32x4 nv = {1.f, 1.f, 1.f, 1.f};
+  if (4 * tid < K) {
+    xv = *(const f32x4*)(x + 4 * tid);
+    if (P.norm_w) nv = *(const f32x4*)(P.norm_w + 4 * tid);
+  }
+  float lo[ROUTER_PPT][16], hi[ROUTER_PPT][16];
+  int olo[ROUTER_PPT], ohi[ROUTER_PPT];
+#pragma unroll
+  for (int j = 0; j < ROUTER_PPT; ++j) {
+    const int i = min(tid + j * ROUTER_NT, total - 1);
+    dequant_piece(W, i / np, i % np, lo[j], hi[j], olo[j], ohi[j]);
+  }
+  // 2. RMS statistics (K <= 4 * ROUTER_NT in one pass; larger K: strided remainder), normalised copy
+  float ss = xv.x * xv.x + xv.y * xv.y + xv.z * xv.z + xv.w * xv.w;
+  for (int i = tid + ROUTER_NT; i < K / 4; i += ROUTER_NT) {
     const f32x4 v = *(const f32x4*)(x + 4 * i);
     ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
   }
   ss = block_sum<ROUTER_NT>(ss, red);
   const float rstd = P.norm == NORM_RMS ? rsqrtf(ss / K + P.eps) : 1.f;
-  const int n_pieces = SB * 8;  // 32-weight pieces per row (K padded to whole super-blocks)
-  for (int e = wave; e < X; e += ROUTER_NT / 64) {
-    float acc = 0.f;
-    for (int p = lane; p < n_pieces; p += 64) {
-      float lo[16], hi[16];
-      int olo, ohi;
-      dequant_piece(W, e, p, lo, hi, olo, ohi);
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        if (olo + i < K) acc += lo[i] * x[olo + i] * (P.norm_w ? P.norm_w[olo + i] : 1.f);
-        if (ohi + i < K) acc += hi[i] * x[ohi + i] * (P.norm_w ? P.norm_w[ohi + i] : 1.f);
+  for (int i = tid; i < SB * 64; i += ROUTER_NT) {
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (4 * i < K) {
+      if (i == tid) {
+        v = xv * rstd * nv;
+      } else {
+        v = *(const f32x4*)(x + 4 * i) * rstd;
+        if (P.norm_w) v *= *(const f32x4*)(P.norm_w + 4 * i);
       }
     }
-    acc = wave_sum(acc);
-    if (lane == 0) lg[e] = acc * rstd;
+    *(f32x4*)(xs + rpad(4 * i)) = v;
+  }
+  __syncthreads();
+  // 3. piece dots, summed per expert (pieces of one expert are consecutive in the flat list)
+  float part[ROUTER_PPT];
+#pragma unroll
+  for (int j = 0; j < ROUTER_PPT; ++j) {
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; i += 4) {
+      const f32x4 a = *(const f32x4*)(xs + rpad(olo[j]) + i), c = *(const f32x4*)(xs + rpad(ohi[j]) + i);
+      acc += lo[j][i] * a.x + lo[j][i + 1] * a.y + lo[j][i + 2] * a.z + lo[j][i + 3] * a.w;
+      acc += hi[j][i] * c.x + hi[j][i + 1] * c.y + hi[j][i + 2] * c.z + hi[j][i + 3] * c.w;
+    }
+    part[j] = tid + j * ROUTER_NT < total ? acc : 0.f;
+  }
+  // np is a multiple of 8: an expert's pieces span whole 8-lane groups; reduce within groups of 8,
+  // then one LDS add per group (deterministic order is not needed for a top-k over distinct logits,
+  // but the sum order is fixed anyway: groups are added by one wave in order below)
+  __shared__ float gsum[ROUTER_PPT * ROUTER_NT / 8];
+#pragma unroll
+  for (int j = 0; j < ROUTER_PPT; ++j) {
+    float v = group_sum<8>(part[j]);
+    if ((lane & 7) == 0) gsum[(tid + j * ROUTER_NT) / 8] = v;
   }
   __syncthreads();
   if (wave != 0) return;
-  float v = lane < X ? lg[lane] : -INFINITY;
+  // 4. wave 0: logit of expert e (lane e) = sum of its np / 8 group sums, top-k, softmax
+  float v = -INFINITY;
+  if (lane < X) {
+    float t = 0.f;
+    for (int g = lane * (np / 8); g < (lane + 1) * (np / 8); ++g) t += gsum[g];
+    v = t;
+  }
   const float mx = wave_max(v);
   float tot = 0.f, mine = 0.f;
   int rank = -1;
@@ -93,8 +143,18 @@ __global__ __launch_bounds__(ROUTER_NT) void moe_router_kernel(GemvParams P, int
   }
 }
 
-void moe_router(const GemvParams& P, int k, int* ids, float* w, hipStream_t s) {
-  hipLaunchKernelGGL(moe_router_kernel, dim3(P.B), dim3(ROUTER_NT), 0, s, P, k, ids, w);
+bool moe_router(const GemvParams& P, int k, int* ids, float* w, hipStream_t s) {
+  const int np = (P.w.K + 255) / 256 * 8;
+  if (P.w.N > 64 || P.w.K > ROUTER_KMAX || P.w.K % 4 || P.w.N * np > ROUTER_PPT * ROUTER_NT) return false;
+  static bool attr = false;  // 64 KiB of dynamic LDS: one attribute call, before any graph capture
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)moe_router_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              ROUTER_KMAX * 9 / 8 * (int)sizeof(float));
+    attr = true;
+  }
+  const size_t lds = (size_t)((P.w.K + 255) / 256) * 288 * sizeof(float);
+  hipLaunchKernelGGL(moe_router_kernel, dim3(P.B), dim3(ROUTER_NT), lds, s, P, k, ids, w);
+  return true;
 }
 
 __global__ void gather_rows_kernel(const float* x, int ld, const int* idx, int n, float* out) {

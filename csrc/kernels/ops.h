@@ -180,7 +180,7 @@ void argmax(const float* logits, int B, int V, int ld, int* out, hipStream_t s);
 
 void moe_route(const float* logits, int B, int X, int k, int* ids, float* w, hipStream_t s);
 // fused RMSNorm + router logits + top-k softmax (P.w = router [X <= 64][K], P.x = resid, P.norm_w)
-void moe_router(const GemvParams& P, int k, int* ids, float* w, hipStream_t s);
+bool moe_router(const GemvParams& P, int k, int* ids, float* w, hipStream_t s);  // false: shape not covered
 void gather_rows(const float* x, int ld, const int* idx, int rows, int n, float* out, hipStream_t s);
 void moe_sort(const int* eids, int n_pairs, int X, int* rows, int* tiles, int* n_tiles, int tile_m, hipStream_t s);
 // grouped dequant GEMM over expert-homogeneous row tiles (P.moe_* set; P.B = number of pairs)

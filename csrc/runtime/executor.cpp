@@ -198,9 +198,7 @@ void Executor::ffn_block(int i, const StepInputs& in, hipStream_t s) {
     R.norm = NORM_RMS;
     R.norm_w = L.ffn_norm;
     R.eps = cfg.eps;
-    if (X <= 64) {  // one fused launch: norm + router logits + top-k (moe.hip moe_router)
-      moe_router(R, k, ws.eids, ws.ew, s);
-    } else {
+    if (!moe_router(R, k, ws.eids, ws.ew, s)) {  // one fused launch: norm + logits + top-k (moe.hip)
       R.epi = EPI_STORE;
       R.y = ws.rlogits;
       R.ldy = X;

@@ -550,6 +550,27 @@ class Runner:
         """Host -> d_tokens[:len(tokens)] (batch recomposition: rows' next inputs)."""
         self._upload(np.zeros((5, 0), np.int32), np.asarray(tokens, np.int32))
 
+    # -- continuous-batching operations (engine/scheduler.py); TPRunnerProxy mirrors each one to the
+    # -- follower ranks, so every KV / sampler decision of the leader is replayed, never re-derived
+    def admit(self, sid: int, keep: int, tokens: list[int], opts: SamplingOptions, history: list[int],
+              seed: int) -> None:
+        """Start row 0 of a new request: keep `keep` cached tokens of `sid`, prefill `tokens`, seed the
+        sampler and sample the first token into s_out[0]."""
+        self.kv.truncate(sid, keep)
+        self.prefill(sid, tokens)
+        self._set_sampler(0, opts, history, seed, 0)
+        self._sample(1)
+
+    def recompose(self, rows: list[tuple], tokens: list[int]) -> None:
+        """New batch composition: rows[b] = (opts, history, seed, n_sampled) and the rows' next inputs."""
+        for b, (o, hist, seed, n) in enumerate(rows):
+            self._set_sampler(b, o, hist, seed, n)
+        self.set_tokens(tokens)
+
+    def evict(self, sid: int) -> None:
+        """Drop a cached (idle) sequence's KV row."""
+        self.kv.free_seq(sid)
+
     def capture_batch_graphs(self, max_B: int) -> None:
         """Load-time capture of the B = 2..max_B decode graphs (continuous batching)."""
         if self.use_graphs:
@@ -557,13 +578,19 @@ class Runner:
                 self._graph(B)
             torch.cuda.synchronize()
 
-    def _generate_pipelined(self, sid: int, st, first: int, max_tokens: int, stop, times, t1) -> Iterator[int]:
+    def _generate_pipelined(self, sid: int, st, first: int, max_tokens: int, stop, times, t1,
+                            ctrl=None) -> Iterator[int]:
         """Two decode steps in flight: step i consumes token i+1 straight from device memory (written
         by step i-1's sampler), so the host never has to see a token before issuing the step after
         it. When token n is handed out, steps producing tokens n+1 and n+2 are already queued; the
         host's detokenise / stop checks / Python overhead hide behind ~2 steps of GPU work instead of
         leaving the GPU idle between steps (was ~130 us per step, profiles/r1_attn). A step issued
-        past a stop is wasted work whose KV position is never recorded in `tokens`."""
+        past a stop is wasted work whose KV position is never recorded in `tokens`.
+
+        Tensor parallel (`ctrl`): every rank runs this same loop. The leader decides each handed-out
+        token (its server applies stop strings on text) and broadcasts go / stop on the gloo control
+        group; followers take that decision instead of their own, so all ranks issue exactly the same
+        steps, two in flight, and read their own (identical) sampled tokens from their host rings."""
         base = st.length  # position of `first`
         ring = self._host_ring  # host-mapped: step at input position p stores its token at p % R
         R = self._ring_n
@@ -580,11 +607,18 @@ class Runner:
 
         n = 0
         tok = first
+        leader = ctrl is not None and ctrl.leader
+        follower = ctrl is not None and not ctrl.leader
         try:
             while True:
                 n += 1  # handing out token n (1-based; token 1 came from the prompt)
-                done = n >= max_tokens or (stop is not None and stop(tok))
+                if follower:
+                    done = not ctrl.wait()
+                else:
+                    done = n >= max_tokens or (stop is not None and stop(tok))
                 if not done:
+                    if leader:
+                        ctrl.signal(True)
                     target = min(n + 1, max_tokens - 1)  # steps 0..n: tokens up to n+2
                     while issued < target:
                         issue()
@@ -596,6 +630,10 @@ class Runner:
                 evs[slot].synchronize()
                 tok = int(ring[slot])
         finally:
+            if leader:
+                ctrl.signal(False)  # generation over (also when the consumer closed us early)
+            if ctrl is not None and self.ar is not None:
+                self.ar.check()  # a peer that missed a barrier timed the step out: fail loudly
             if times is not None:
                 times.gen_tokens = n
                 times.gen_s = time.perf_counter() - t1
@@ -627,8 +665,8 @@ class Runner:
             times.prompt_s = time.perf_counter() - t0
         t1 = time.perf_counter()
         max_tokens = min(max_tokens, self.ctx - st.length)
-        if self.is_gpu and self.tp_ctrl is None:
-            yield from self._generate_pipelined(sid, st, first, max_tokens, stop, times, t1)
+        if self.is_gpu:
+            yield from self._generate_pipelined(sid, st, first, max_tokens, stop, times, t1, ctrl=self.tp_ctrl)
             return
         n = 0
         tok = first

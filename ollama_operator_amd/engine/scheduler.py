@@ -68,8 +68,8 @@ class BatchScheduler:
     """Per-model continuous-batching loop (see module docstring)."""
 
     def __init__(self, runner: Runner, max_parallel: int = 4, depth: int = 2):
-        if runner.tp_size > 1:
-            raise ValueError("continuous batching runs on single-rank runners (TP serving is serialised)")
+        # tensor parallel: `runner` is the leader's TPRunnerProxy; every runner call below is mirrored to
+        # the follower ranks (parallel/tp.py), which replay the leader's decisions step for step
         self.r = runner
         # one KV row stays reserved for exclusive jobs (embeddings) even when every row decodes
         self.max_parallel = max(1, min(max_parallel, runner.max_batch, runner.max_seqs - 1))
@@ -217,7 +217,7 @@ class BatchScheduler:
             self.idle.remove(best)
             return best, keep
         if not kv.rows_free and self.idle:
-            kv.free_seq(self.idle.pop(0))
+            self.r.evict(self.idle.pop(0))
         return self.r.new_sequence(), 0
 
     def _admit(self) -> None:
@@ -233,12 +233,9 @@ class BatchScheduler:
             try:
                 sid, keep = self._take_sequence(req.prompt)
                 keep = min(keep, len(req.prompt) - 1)
-                r.kv.truncate(sid, keep)
                 req.sid = sid
                 t0 = time.perf_counter()
-                r.prefill(sid, req.prompt[keep:])
-                r._set_sampler(0, req.opts, req.prompt, req.seed, 0)
-                r._sample(1)
+                r.admit(sid, keep, req.prompt[keep:], req.opts, req.prompt, req.seed)
                 first = int(r.s_out[0].item())
             except BaseException as e:  # noqa: BLE001 -- this request fails, the batch goes on
                 if req.sid is not None and req.sid in r.kv.seqs:
@@ -273,10 +270,8 @@ class BatchScheduler:
 
     def _recompose(self) -> None:
         """Rows changed: upload every row's next input token and sampler state (history, RNG step)."""
-        r = self.r
-        for b, req in enumerate(self.active):
-            r._set_sampler(b, req.opts, req.history, req.seed, req.n_sampled)
-        r.set_tokens([req.last_input for req in self.active])
+        self.r.recompose([(req.opts, req.history, req.seed, req.n_sampled) for req in self.active],
+                         [req.last_input for req in self.active])
 
     def _must_drain(self, rows: list[_Req]) -> bool:
         """Stop issuing (drain in-flight steps, then recompose) only when the composition must change:

@@ -204,6 +204,28 @@ class TPRunnerProxy:
         self._mirror("generate", sid=sid, prompt=list(prompt), options=o, max_tokens=max_tokens)
         return self.r.generate(sid, prompt, o, max_tokens=max_tokens, stop=stop, times=times)
 
+    # continuous batching (engine/scheduler.py drives the leader's runner through these)
+    def admit(self, sid: int, keep: int, tokens: list[int], opts, history: list[int], seed: int) -> None:
+        self._mirror("admit", sid=sid, keep=keep, tokens=list(tokens), opts=opts, history=list(history), seed=seed)
+        self.r.admit(sid, keep, tokens, opts, history, seed)
+
+    def recompose(self, rows: list[tuple], tokens: list[int]) -> None:
+        rows = [(o, list(h), sd, n) for o, h, sd, n in rows]
+        self._mirror("recompose", rows=rows, tokens=list(tokens))
+        self.r.recompose(rows, tokens)
+
+    def decode_batch(self, sids: list[int], poss: list[int]) -> None:
+        self._mirror("decode_batch", sids=list(sids), poss=list(poss))
+        self.r.decode_batch(sids, poss)
+
+    def evict(self, sid: int) -> None:
+        self._mirror("evict", sid=sid)
+        self.r.evict(sid)
+
+    def capture_batch_graphs(self, max_B: int) -> None:
+        self._mirror("capture_batch_graphs", max_B=max_B)
+        self.r.capture_batch_graphs(max_B)
+
     def close(self) -> None:
         self.world.ar_probe = None
         self._mirror("unload")
@@ -256,6 +278,16 @@ def worker_main() -> None:
         elif op == "generate":
             for _ in runner.generate(cmd["sid"], cmd["prompt"], cmd["options"], max_tokens=cmd["max_tokens"]):
                 pass
+        elif op == "admit":
+            runner.admit(cmd["sid"], cmd["keep"], cmd["tokens"], cmd["opts"], cmd["history"], cmd["seed"])
+        elif op == "recompose":
+            runner.recompose(cmd["rows"], cmd["tokens"])
+        elif op == "decode_batch":
+            runner.decode_batch(cmd["sids"], cmd["poss"])
+        elif op == "evict":
+            runner.evict(cmd["sid"])
+        elif op == "capture_batch_graphs":
+            runner.capture_batch_graphs(cmd["max_B"])
         else:
             raise RuntimeError(f"unknown TP command {op}")
     dist.barrier(group=ctrl_group)

@@ -150,23 +150,23 @@ class ModelManager:
         # prefill chunk = MFMA GEMM M dimension (weights cross HBM once per chunk)
         chunk = int(os.environ.get("OMX_PREFILL_CHUNK", "2048"))  # 2048-token TTFT 117 -> 94 ms vs 512
         scheduler = None
+        # continuous batching (Ollama OLLAMA_NUM_PARALLEL): parallel rows + as many idle sequences
+        # kept for prefix reuse; KV is sized for all of them at full context (288 GB HBM)
+        # default 4 as Ollama; the batched path is covered on MI355X by
+        # tests/test_engine_gpu.py::test_batched_decode_matches_single / test_scheduler_concurrent_gpu
+        par = max(1, int(os.environ.get("OLLAMA_NUM_PARALLEL", "4")))
+        # rows: par decoding + par idle prefix-cache sequences + 1 kept free for embeddings
+        max_seqs = max(2, 2 * par + 1)
         if self.tp_world is not None:  # tensor parallel: every rank loads its shard (parallel/tp.py)
             from ..parallel.tp import load_tp_runner
-            runner = load_tp_runner(self.tp_world, path, max_batch=chunk, max_seqs=2, ctx=ctx)
-            runner.warmup()
+            runner = load_tp_runner(self.tp_world, path, max_batch=chunk, max_seqs=max_seqs, ctx=ctx)
         else:
-            # continuous batching (Ollama OLLAMA_NUM_PARALLEL): parallel rows + as many idle sequences
-            # kept for prefix reuse; KV is sized for all of them at full context (288 GB HBM)
-            # default 4 as Ollama; the batched path is covered on MI355X by
-            # tests/test_engine_gpu.py::test_batched_decode_matches_single / test_scheduler_concurrent_gpu
-            par = max(1, int(os.environ.get("OLLAMA_NUM_PARALLEL", "4")))
-            # rows: par decoding + par idle prefix-cache sequences + 1 kept free for embeddings
-            runner = Runner(path, device=self.device, max_batch=chunk, max_seqs=max(2, 2 * par + 1), ctx=ctx)
-            runner.warmup()
-            if par > 1:
-                from ..engine.scheduler import BatchScheduler
-                runner.capture_batch_graphs(par)
-                scheduler = BatchScheduler(runner, max_parallel=par)
+            runner = Runner(path, device=self.device, max_batch=chunk, max_seqs=max_seqs, ctx=ctx)
+        runner.warmup()
+        if par > 1:  # under TP the scheduler drives the leader's proxy; followers replay every call
+            from ..engine.scheduler import BatchScheduler
+            runner.capture_batch_graphs(par)
+            scheduler = BatchScheduler(runner, max_parallel=par)
         return LoadedModel(name=name, digest=m.digest, path=path, runner=runner, tokenizer=tok, scheduler=scheduler,
                            template=self.store.text_layer(m, MT_TEMPLATE), system=self.store.text_layer(m, MT_SYSTEM),
                            params=self.store.params(m), num_ctx=runner.ctx, size=os.path.getsize(path),

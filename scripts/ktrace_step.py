@@ -20,7 +20,12 @@ def main():
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     idx = [i for i, r in enumerate(rows) if re.search(r"sample(_fast)?_kernel", r["Kernel_Name"])]
     # steady-state decode steps: between consecutive sampler launches, skip the first few
-    steps = list(zip(idx[4:-1], idx[5:]))[-16:]
+    steps = list(zip(idx[4:-1], idx[5:]))
+    # drop steps that contain a prefill (bench runs a ttft probe after the decode loop)
+    spans = sorted(int(rows[b]["Start_Timestamp"]) - int(rows[a]["Start_Timestamp"]) for a, b in steps)
+    med = spans[len(spans) // 2] if spans else 0
+    steps = [(a, b) for a, b in steps
+             if int(rows[b]["Start_Timestamp"]) - int(rows[a]["Start_Timestamp"]) <= 1.5 * med][-16:]
     busy = collections.Counter()
     calls = collections.Counter()
     gap_after = collections.Counter()
