@@ -125,6 +125,9 @@ def build(jobs: int | None = None, clean: bool = False, verbose: bool = False, d
         tl = _torch_lib()
         if tl:
             link += [f"-L{tl}", f"-Wl,-rpath,{tl}"]
+        # hipBLASLt for the large-M prefill GEMM (csrc/runtime/blas.cpp): torch's copy when present
+        # (one instance per process), else the ROCm one
+        link += ["-lhipblaslt"] + ([] if tl and os.path.exists(os.path.join(tl, "libhipblaslt.so")) else ["-L/opt/rocm/lib"])
         r = subprocess.run(link, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError("link failed:\n" + " ".join(link) + "\n" + r.stdout + r.stderr)

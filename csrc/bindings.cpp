@@ -189,6 +189,12 @@ PYBIND11_MODULE(_C, m) {
       P.gws = Pp<float>(qkv["gws"].cast<uintptr_t>());
       P.gws_elems = qkv["gws_elems"].cast<long long>();
     }
+    if (qkv.contains("w16ws")) {  // large-M library GEMM scratch (gemm.hip gemm_lib)
+      P.w16ws = Pp<void>(qkv["w16ws"].cast<uintptr_t>());
+      P.w16_elems = qkv["w16_elems"].cast<long long>();
+      P.yws = Pp<float>(qkv["yws"].cast<uintptr_t>());
+      P.yws_elems = qkv["yws_elems"].cast<long long>();
+    }
     if (epi == EPI_QKV) {
       P.pos = Pp<const int>(qkv["pos"].cast<uintptr_t>());
       P.slot = Pp<const int>(qkv["slot"].cast<uintptr_t>());
@@ -271,9 +277,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("embed_rows", [](py::object w, uintptr_t rows, int n, uintptr_t out, int ldo, uintptr_t stream) {
     embed_rows(qmat(w), Pp<const int>(rows), n, Pp<float>(out), ldo, S(stream));
   });
-  m.def("dequant_f16", [](py::object w, uintptr_t out, uintptr_t stream) {
-    dequant_f16(qmat(w), Pp<void>(out), S(stream));
-  });
+  m.def("set_gemm_lib_min_m", &set_gemm_lib_min_m, "prefill rows from which the hipBLASLt path runs (0 = off)");
+  m.def("gemm_lib_min_m", &gemm_lib_min_m);
+  m.def("dequant_f16", [](py::object w, uintptr_t out, uintptr_t stream, int perm) {
+    dequant_f16(qmat(w), Pp<void>(out), S(stream), perm);
+  }, py::arg("w"), py::arg("out"), py::arg("stream"), py::arg("perm") = 0);
   m.def("argmax", [](uintptr_t logits, int B, int V, int ld, uintptr_t out, uintptr_t stream) {
     argmax(Pp<const float>(logits), B, V, ld, Pp<int>(out), S(stream));
   });
@@ -432,6 +440,10 @@ PYBIND11_MODULE(_C, m) {
         w.x16 = Pp<void>(ptr("x16"));
         w.gws = Pp<float>(ptr("gws"));
         w.gws_elems = d.contains("gws_elems") ? d["gws_elems"].cast<long long>() : 0;
+        w.w16 = Pp<void>(ptr("w16"));
+        w.w16_elems = d.contains("w16_elems") ? d["w16_elems"].cast<long long>() : 0;
+        w.yws = Pp<float>(ptr("yws"));
+        w.yws_elems = d.contains("yws_elems") ? d["yws_elems"].cast<long long>() : 0;
         w.moe_rows = Pp<int>(ptr("moe_rows"));
         w.moe_tiles = Pp<int>(ptr("moe_tiles"));
         w.moe_ntiles = Pp<int>(ptr("moe_ntiles"));

@@ -30,7 +30,9 @@ void embed_rows(const QMat& w, const int* rows, int n, float* out, int ldo, hipS
   hipLaunchKernelGGL(embed_rows_kernel, dim3(n), dim3(256), 0, s, w, rows, out, ldo, scale);
 }
 
-// grid-stride over (row, piece)
+// grid-stride over (row, piece); PERM: K order (0, 2, 1, 3) inside every 4, the order prep_x16 writes the
+// prefill activations in (gemm.hip), so the library GEMM can consume both as they are
+template <bool PERM>
 __global__ __launch_bounds__(256) void dequant_f16_kernel(QMat w, f16* out) {
   const int P = w.K / 32;
   const long long total = (long long)w.N * P;
@@ -45,8 +47,9 @@ __global__ __launch_bounds__(256) void dequant_f16_kernel(QMat w, f16* out) {
     f16x8 a, b, c, d;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      a[j] = (f16)lo[j]; b[j] = (f16)lo[8 + j];
-      c[j] = (f16)hi[j]; d[j] = (f16)hi[8 + j];
+      const int k = PERM ? (j & ~3) | ((j & 1) << 1) | ((j >> 1) & 1) : j;  // 0 2 1 3
+      a[j] = (f16)lo[k]; b[j] = (f16)lo[8 + k];
+      c[j] = (f16)hi[k]; d[j] = (f16)hi[8 + k];
     }
     *(f16x8*)(o + olo) = a;
     *(f16x8*)(o + olo + 8) = b;
@@ -55,10 +58,13 @@ __global__ __launch_bounds__(256) void dequant_f16_kernel(QMat w, f16* out) {
   }
 }
 
-void dequant_f16(const QMat& w, void* out, hipStream_t s) {
+void dequant_f16(const QMat& w, void* out, hipStream_t s, int perm) {
   const long long total = (long long)w.N * (w.K / 32);
-  const int blocks = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
-  hipLaunchKernelGGL(dequant_f16_kernel, dim3(blocks), dim3(256), 0, s, w, (f16*)out);
+  const int blocks = (int)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192);
+  if (perm)
+    hipLaunchKernelGGL(dequant_f16_kernel<true>, dim3(blocks), dim3(256), 0, s, w, (f16*)out);
+  else
+    hipLaunchKernelGGL(dequant_f16_kernel<false>, dim3(blocks), dim3(256), 0, s, w, (f16*)out);
 }
 
 // Q6_K -> QT_Q6_K8 widening at load (qmat.h): one thread per (row, super-block, piece) writes the

@@ -459,9 +459,39 @@ bool gemm_eligible(const GemvParams& P) {
   return P.xws != nullptr && P.B >= GEMM_MIN_B && P.expert_ids == nullptr && (P.w.K % 32) == 0;
 }
 
+// Large-M library path (blas.cpp): dequantise W once into fp16 (in prep_x16's K order), one hipBLASLt
+// GEMM into the fp32 slab yws, then the fused epilogue as for split-K (finalize, one slab)
+static int g_lib_min_m = -1;  // -1: OMX_GEMM_LIB_MIN_M (default 256), read once
+
+int gemm_lib_min_m() {
+  if (g_lib_min_m < 0) {
+    const char* e = getenv("OMX_GEMM_LIB_MIN_M");
+    g_lib_min_m = e ? atoi(e) : 256;
+  }
+  return g_lib_min_m;
+}
+
+void set_gemm_lib_min_m(int m) { g_lib_min_m = m; }
+
+static bool gemm_lib(const GemvParams& P, const f16* x16, hipStream_t s) {
+  const int lm = gemm_lib_min_m();
+  const long long M = P.B, N = P.w.N, K = P.w.K;
+  if (lm <= 0 || M < lm || !P.w16ws || !P.yws || N * K > P.w16_elems || M * N > P.yws_elems) return false;
+  dequant_f16(P.w, P.w16ws, s, 1);
+  if (!blas_gemm_tn(P.w16ws, x16, P.yws, (int)M, (int)N, (int)K, P.gws, P.gws ? (size_t)P.gws_elems * 4 : 0, s))
+    return false;
+  GemvParams F = P;
+  F.gws = P.yws;
+  const long long pairs = M * ((N + 1) / 2);
+  const int blocks = (int)((pairs + 255) / 256 < 4096 ? (pairs + 255) / 256 : 4096);
+  hipLaunchKernelGGL(gemm_finalize_kernel, dim3(blocks), dim3(256), 0, s, F, 1);
+  return true;
+}
+
 void gemm(const GemvParams& P, hipStream_t s) {
   f16* x16 = (f16*)P.xws;
   hipLaunchKernelGGL(prep_x16_kernel, dim3(P.B), dim3(256), 0, s, P, x16);
+  if (gemm_lib(P, x16, s)) return;
   switch (P.w.qtype) {
     case QT_Q4_K: launch_gemm<QT_Q4_K>(P, x16, s); break;
     case QT_Q6_K: launch_gemm<QT_Q6_K>(P, x16, s); break;

@@ -45,6 +45,13 @@ struct GemvParams {
   // split-K partial slabs for small-M GEMMs: fp32 [splits][B][N], capacity gws_elems (0 -> no split)
   float* gws;
   long long gws_elems;
+  // library GEMM path for large M (gemm.hip gemm_lib, blas.cpp): the weight dequantised once per call
+  // into fp16 scratch [N][K], one hipBLASLt fp16 x fp16 -> fp32 GEMM into yws [M][N], then the fused
+  // epilogue; null / too small -> the fused dequant MFMA GEMM
+  void* w16ws;
+  long long w16_elems;
+  float* yws;
+  long long yws_elems;
   // MoE prefill grouped GEMM (gemm.hip GROUPED): rows are the B*k (token, expert) pairs sorted by
   // expert (moe_sort); x / y rows are in sorted order except that moe_scatter writes output row
   // pair = moe_rows[pos] to token pair / n_sel with routing weight expert_w[pair]
@@ -89,6 +96,13 @@ bool gemv_merge_supported(int B, int K, int D, int S);
 // two GEMVs over the same x (same K, RMS norm prologue) in one launch when B == 1, else two launches
 void gemv2(const GemvParams& A, const GemvParams& B, hipStream_t s);
 constexpr int GEMM_MIN_B = 16;
+// prefill rows from which the library GEMM path is taken (0 = never); OMX_GEMM_LIB_MIN_M overrides
+void set_gemm_lib_min_m(int m);
+int gemm_lib_min_m();
+// D[M][N] (fp32, row-major) = X[M][K] . W[N][K]^T, X and W fp16 row-major, on hipBLASLt; false when
+// no algorithm fits (the caller falls back)
+bool blas_gemm_tn(const void* w16, const void* x16, float* d, int M, int N, int K, void* ws, size_t ws_bytes,
+                  hipStream_t s);
 // batched decode GEMV on the matrix cores (gemv_mfma.hip): 2 <= B <= 16 rows, needs the layout M
 // copy (QMat::mt) built by repack_m; false = shape not covered (the caller takes the int8 GEMV)
 bool gemv_mb(const GemvParams& P, hipStream_t s);
@@ -121,7 +135,7 @@ void set_gemv_tuning(int blocks_per_cu, int rows, int debug, int ks = -1, int xf
 
 // Dequantize rows of a repacked matrix (embedding gather / fp16 copies)
 void embed_rows(const QMat& w, const int* rows, int n, float* out, int ldo, hipStream_t s, float scale = 1.f);
-void dequant_f16(const QMat& w, void* out_f16, hipStream_t s);
+void dequant_f16(const QMat& w, void* out_f16, hipStream_t s, int perm = 0);  // perm: prep_x16 K order
 
 struct AttnParams {
   const float* q;              // [NQ][ldq] fp32 (roped)

@@ -1,0 +1,108 @@
+// hipBLASLt fp16 x fp16 -> fp32 GEMM for the large-M prefill path (gemm.hip gemm_lib).
+//
+// Why a library GEMM here: at M >= a few hundred prompt tokens the prefill projections are compute
+// bound, and hipBLASLt's gfx950 MFMA kernels run 0.85-1.2 PFLOP/s on the Llama-2-7B shapes at
+// M = 2048 (profiles/r3_gemm/blas_probe.log) against 0.33 for the fused dequant GEMM, whose
+// in-loop dequantisation is VALU/LDS-bound. The weight is dequantised once per call into an fp16
+// scratch (dequant.hip, memory-bound: ~2 bytes written per weight), so the quantised weights stay the
+// only resident copy. Plain library GEMM, nothing fused: the epilogue runs afterwards.
+//
+// Layout: hipBLASLt is column-major. Row-major D[M][N] is column-major N x M (ld N); row-major
+// W[N][K] is column-major K x N (ld K) used transposed; row-major X[M][K] is column-major K x M.
+// So D = op_T(W) * X, a "TN" GEMM. Plans (descriptors + heuristic algorithm) are cached per shape
+// and device.
+#include <hipblaslt/hipblaslt.h>
+
+#include <cstdio>
+#include <map>
+#include <mutex>
+#include <tuple>
+
+#include "kernels/ops.h"
+
+namespace omx {
+
+namespace {
+
+struct Plan {
+  hipblasLtMatmulDesc_t op = nullptr;
+  hipblasLtMatrixLayout_t a = nullptr, b = nullptr, d = nullptr;
+  hipblasLtMatmulAlgo_t algo{};
+  size_t ws = 0;
+  bool ok = false;
+};
+
+std::mutex g_mu;
+std::map<int, hipblasLtHandle_t> g_handles;
+std::map<std::tuple<int, int, int, int, size_t>, Plan> g_plans;
+
+hipblasLtHandle_t handle(int dev) {
+  auto it = g_handles.find(dev);
+  if (it != g_handles.end()) return it->second;
+  hipblasLtHandle_t h = nullptr;
+  if (hipblasLtCreate(&h) != HIPBLAS_STATUS_SUCCESS) h = nullptr;
+  g_handles[dev] = h;
+  return h;
+}
+
+Plan make_plan(hipblasLtHandle_t h, int M, int N, int K, size_t ws_bytes) {
+  Plan p;
+  if (hipblasLtMatmulDescCreate(&p.op, HIPBLAS_COMPUTE_32F, HIP_R_32F) != HIPBLAS_STATUS_SUCCESS) return p;
+  const hipblasOperation_t ta = HIPBLAS_OP_T, tb = HIPBLAS_OP_N;
+  hipblasLtMatmulDescSetAttribute(p.op, HIPBLASLT_MATMUL_DESC_TRANSA, &ta, sizeof(ta));
+  hipblasLtMatmulDescSetAttribute(p.op, HIPBLASLT_MATMUL_DESC_TRANSB, &tb, sizeof(tb));
+  if (hipblasLtMatrixLayoutCreate(&p.a, HIP_R_16F, K, N, K) != HIPBLAS_STATUS_SUCCESS ||
+      hipblasLtMatrixLayoutCreate(&p.b, HIP_R_16F, K, M, K) != HIPBLAS_STATUS_SUCCESS ||
+      hipblasLtMatrixLayoutCreate(&p.d, HIP_R_32F, N, M, N) != HIPBLAS_STATUS_SUCCESS)
+    return p;
+  hipblasLtMatmulPreference_t pref = nullptr;
+  if (hipblasLtMatmulPreferenceCreate(&pref) != HIPBLAS_STATUS_SUCCESS) return p;
+  const uint64_t wsb = ws_bytes;
+  hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsb, sizeof(wsb));
+  hipblasLtMatmulHeuristicResult_t res[8];
+  int n = 0;
+  const hipblasStatus_t st = hipblasLtMatmulAlgoGetHeuristic(h, p.op, p.a, p.b, p.d, p.d, pref, 8, res, &n);
+  hipblasLtMatmulPreferenceDestroy(pref);
+  for (int i = 0; st == HIPBLAS_STATUS_SUCCESS && i < n && !p.ok; ++i) {
+    if (res[i].state != HIPBLAS_STATUS_SUCCESS || res[i].workspaceSize > ws_bytes) continue;
+    p.algo = res[i].algo;
+    p.ws = res[i].workspaceSize;
+    p.ok = true;
+  }
+  if (!p.ok)
+    fprintf(stderr, "[omx] hipBLASLt: no algorithm for M=%d N=%d K=%d (status %d, %d candidates, %zu B workspace); "
+            "fused dequant GEMM used\n", M, N, K, (int)st, n, ws_bytes);
+  return p;
+}
+
+}  // namespace
+
+bool blas_gemm_tn(const void* w16, const void* x16, float* d, int M, int N, int K, void* ws, size_t ws_bytes,
+                  hipStream_t s) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return false;
+  Plan p;
+  hipblasLtHandle_t h;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    h = handle(dev);
+    if (!h) return false;
+    const auto key = std::make_tuple(dev, M, N, K, ws_bytes);
+    auto it = g_plans.find(key);
+    if (it == g_plans.end()) it = g_plans.emplace(key, make_plan(h, M, N, K, ws_bytes)).first;
+    p = it->second;
+  }
+  if (!p.ok) return false;
+  const float alpha = 1.f, beta = 0.f;
+  const hipblasStatus_t st = hipblasLtMatmul(h, p.op, &alpha, w16, p.a, x16, p.b, &beta, d, p.d, d, p.d, &p.algo,
+                                             p.ws ? ws : nullptr, p.ws, s);
+  if (st != HIPBLAS_STATUS_SUCCESS) {
+    static bool warned = false;
+    if (!warned) fprintf(stderr, "[omx] hipBLASLt matmul failed (status %d, M=%d N=%d K=%d)\n", (int)st, M, N, K);
+    warned = true;
+    return false;
+  }
+  return true;
+}
+
+}  // namespace omx

@@ -10,6 +10,10 @@ static GemvParams base_params(const QMat& w, int B, const float* x, int ldx, con
   P.xws = ws.x16;
   P.gws = ws.gws;
   P.gws_elems = ws.gws_elems;
+  P.w16ws = ws.w16;
+  P.w16_elems = ws.w16_elems;
+  P.yws = ws.yws;
+  P.yws_elems = ws.yws_elems;
   P.w = w;
   P.B = B;
   P.x = x;

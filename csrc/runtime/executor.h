@@ -62,6 +62,10 @@ struct Workspace {
   int* moe_tiles = nullptr;  // [(maxB*k/128 + X + 1)*3] expert row tiles
   int* moe_ntiles = nullptr; // [1]
   long long gws_elems = 0;
+  void* w16 = nullptr;       // large-M prefill library GEMM: fp16 dequantised weight [N][K] scratch
+  long long w16_elems = 0;
+  float* yws = nullptr;      //   and its fp32 output slab [M][N]
+  long long yws_elems = 0;
   int max_B = 0;
   int n_splits = 1;
   int defer = 0;             // B == 1: attention leaves n_splits partials, the O GEMV merges them

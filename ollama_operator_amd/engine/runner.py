@@ -27,7 +27,7 @@ from ..ops.reference import TorchExecutor
 from ..utils.trace import trace_range
 from .kv_cache import PagedKV
 from .sampling import SamplingOptions, sample_host
-from .weights import DeviceWeights
+from .weights import DeviceWeights, DevQMat
 
 HIST_CAP = 256
 GEMM_SPLIT_WS_FLOATS = 8 << 20  # 32 MiB of fp32 split-K slabs (prefill GEMMs at small M)
@@ -65,6 +65,8 @@ class NativeExec:
                              moe_rows=p(r.moe_rows) if cfg.n_expert else 0, moe_tiles=p(r.moe_tiles),
                              moe_ntiles=p(r.moe_ntiles),
                              gws_elems=r.gws.numel(), max_B=r.max_batch, ld_logits=r.logits.shape[1],
+                             w16=p(r.w16), w16_elems=r.w16.numel() if r.w16 is not None else 0,
+                             yws=p(r.yws), yws_elems=r.yws.numel() if r.yws is not None else 0,
                              n_splits=1, **self._chain_ws(r)))
         # step buffers bound once: every stage call below passes integers only
         e.set_inputs(dict(tokens=p(r.d_tokens), pos=p(r.d_pos), slot=p(r.d_slot), q_len=p(r.d_qlen),
@@ -190,6 +192,15 @@ class Runner:
         self.moe_ntiles = torch.zeros(1, **i32)
         # split-K partial slabs of small-M prefill GEMMs (the kernel picks splits that fit)
         self.gws = torch.zeros(GEMM_SPLIT_WS_FLOATS if str(dev).startswith("cuda") else 1, **f32)
+        # large-M prefill on hipBLASLt (gemm.hip gemm_lib): fp16 dequantised-weight scratch sized for the
+        # largest dense layer matrix and its fp32 output slab at max_batch rows (OMX_GEMM_LIB=0: off)
+        self.w16 = self.yws = None
+        if self.is_gpu and os.environ.get("OMX_GEMM_LIB", "1") != "0" and max_batch >= 16:
+            mats = [v for L in self.w.layers for k, v in L.items()
+                    if isinstance(v, DevQMat) and k not in ("gu_exps", "down_exps", "router")]
+            if mats:
+                self.w16 = torch.empty(max(m.N * m.K for m in mats), device=dev, dtype=torch.float16)
+                self.yws = torch.empty(max_batch * max(m.N for m in mats), **f32)
         ws = max(self._ws_floats(B) for B in range(1, max_batch + 1))
         self.attn_ws = torch.zeros(max(ws, 1), **f32)
         self.attn_cnt = torch.zeros(max_batch * loc["H"], **i32)  # self re-arming tickets

@@ -1,4 +1,5 @@
-"""Prefill MFMA dequant-GEMM microbenchmark (csrc/kernels/gemm.hip) on Llama-2-7B Q4_K_M shapes:
+"""Prefill GEMM microbenchmark, fused MFMA dequant GEMM (csrc/kernels/gemm.hip) vs the hipBLASLt path
+(dequant to fp16 + library GEMM + epilogue; csrc/runtime/blas.cpp) on Llama-2-7B Q4_K_M shapes:
 time per call and achieved TFLOP/s vs M (prompt tokens). Run on the GPU box:
   python scripts/bench_gemm.py            (OMX_BENCH_SHAPES / OMX_BENCH_M filter for PMC runs)"""
 import os
@@ -21,7 +22,7 @@ def main():
     C = native()
     s = torch.cuda.current_stream().cuda_stream
     keep = os.environ.get("OMX_BENCH_SHAPES")
-    ms = [int(v) for v in os.environ.get("OMX_BENCH_M", "128,512,2048").split(",")]
+    ms = [int(v) for v in os.environ.get("OMX_BENCH_M", "128,256,512,2048").split(",")]
     for name, qt, N, K in SHAPES:
         if keep and name not in keep.split(","):
             continue
@@ -34,21 +35,26 @@ def main():
             y = torch.zeros(M, N, device="cuda")
             xws = torch.empty(M * K, device="cuda", dtype=torch.float16)
             gws = torch.empty(8 << 20, device="cuda")  # the runner's split-K workspace
-            fn = lambda: C.gemv(tup, M, x.data_ptr(), K, 0, 0, 0, 1e-5, 0, y.data_ptr(), N, 0, 0,  # noqa: E731
-                                {"xws": xws.data_ptr(), "gws": gws.data_ptr(), "gws_elems": gws.numel()}, s)
-            for _ in range(3):
-                fn()
-            torch.cuda.synchronize()
-            n = 20
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            for _ in range(n):
-                fn()
-            e1.record()
-            torch.cuda.synchronize()
-            us = e0.elapsed_time(e1) * 1e3 / n
-            print(f"{name:9s} {qt.name:5s} N={N:6d} K={K:6d} M={M:5d}: {us:9.1f} us  "
-                  f"{2 * M * N * K / us / 1e6:7.1f} TFLOP/s", flush=True)
+            w16 = torch.empty(N * K, device="cuda", dtype=torch.float16)
+            yws = torch.empty(M * N, device="cuda")
+            ws = {"xws": xws.data_ptr(), "gws": gws.data_ptr(), "gws_elems": gws.numel(), "w16ws": w16.data_ptr(),
+                  "w16_elems": w16.numel(), "yws": yws.data_ptr(), "yws_elems": yws.numel()}
+            fn = lambda: C.gemv(tup, M, x.data_ptr(), K, 0, 0, 0, 1e-5, 0, y.data_ptr(), N, 0, 0, ws, s)  # noqa: E731
+            for path, min_m in (("fused", 0), ("hipblaslt", 1)):
+                C.set_gemm_lib_min_m(min_m)
+                for _ in range(3):
+                    fn()
+                torch.cuda.synchronize()
+                n = 20
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(n):
+                    fn()
+                e1.record()
+                torch.cuda.synchronize()
+                us = e0.elapsed_time(e1) * 1e3 / n
+                print(f"{name:9s} {qt.name:5s} N={N:6d} K={K:6d} M={M:5d} {path:9s}: {us:9.1f} us  "
+                      f"{2 * M * N * K / us / 1e6:7.1f} TFLOP/s", flush=True)
 
 
 if __name__ == "__main__":

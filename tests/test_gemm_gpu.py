@@ -13,18 +13,32 @@ from test_kernels_gpu import QM, QTYPES, C, S, rel
 pytestmark = pytest.mark.gpu
 
 
-def gemm(m, x, norm=0, nw=None, nb=None, epi=0, y=None, bias=None, extra=None, eps=1e-5, split=True):
-    """split=True gives the kernel a split-K workspace (small M then runs split-K + finalize)."""
+def gemm(m, x, norm=0, nw=None, nb=None, epi=0, y=None, bias=None, extra=None, eps=1e-5, split=True, lib=False):
+    """split=True gives the kernel a split-K workspace (small M then runs split-K + finalize).
+    lib=True: the hipBLASLt path (dequantised fp16 weight scratch + fp32 slab) from M = 16 on."""
     B, K = x.shape
     xws = torch.empty(B * K, device="cuda", dtype=torch.float16)
     gws = torch.empty(8 << 20, device="cuda")
     p = lambda t: t.data_ptr() if t is not None else 0  # noqa: E731
     d = dict(extra or {})
     d["xws"] = xws.data_ptr()
-    if split:
+    if split or lib:
         d["gws"], d["gws_elems"] = gws.data_ptr(), gws.numel()
-    C().gemv(m.tup, B, p(x), K, norm, p(nw), p(nb), eps, epi, p(y), y.shape[1], p(bias), 0, d, S())
-    torch.cuda.synchronize()
+    keep = []
+    if lib:
+        w16 = torch.full((m.w.shape[0] * K,), float("nan"), device="cuda", dtype=torch.float16)
+        yws = torch.full((B * m.w.shape[0],), float("nan"), device="cuda")
+        keep += [w16, yws]
+        d.update(w16ws=w16.data_ptr(), w16_elems=w16.numel(), yws=yws.data_ptr(), yws_elems=yws.numel())
+    old = C().gemm_lib_min_m()
+    C().set_gemm_lib_min_m(16 if lib else 0)
+    try:
+        C().gemv(m.tup, B, p(x), K, norm, p(nw), p(nb), eps, epi, p(y), y.shape[1], p(bias), 0, d, S())
+        torch.cuda.synchronize()
+    finally:
+        C().set_gemm_lib_min_m(old)
+    if lib:  # the library path really ran: the fp32 slab holds the raw products
+        assert not torch.isnan(keep[1]).any()
 
 
 @pytest.mark.parametrize("qt", QTYPES)
@@ -129,3 +143,54 @@ def test_gemm_matches_batched_gemv():
     C().gemv(m.tup, B, x.data_ptr(), K, 0, 0, 0, 1e-5, 0, y2.data_ptr(), N, 0, 0, {}, S())
     torch.cuda.synchronize()
     assert rel(y1, y2) < 1e-2
+
+
+# ---- large-M library path (gemm.hip gemm_lib -> blas.cpp hipBLASLt) ---------------------------------
+@pytest.mark.parametrize("qt", QTYPES)
+@pytest.mark.parametrize("B,K", [(16, 256), (130, 4096), (300, 288), (64, 11008)])
+def test_gemm_lib_store(qt, B, K):
+    if K % 256 and qt in (GGMLType.Q4_K, GGMLType.Q5_K, GGMLType.Q6_K):
+        pytest.skip("k-quant rows are whole super-blocks")
+    N = 384 + 64
+    m = QM(qt, N, K, seed=K + B + 1)
+    x = torch.randn(B, K, device="cuda")
+    y = torch.zeros(B, N, device="cuda")
+    gemm(m, x, y=y, lib=True)
+    assert rel(y, x @ m.w.T) < 1e-2
+
+
+def test_gemm_lib_rmsnorm_add_bias():
+    N, K, B = 512, 2048, 96
+    m = QM(GGMLType.Q6_K, N, K, seed=13)
+    x = torch.randn(B, K, device="cuda") * 3
+    nw = torch.rand(K, device="cuda") + 0.5
+    bias = torch.randn(N, device="cuda")
+    y0 = torch.randn(B, N, device="cuda")
+    y = y0.clone()
+    gemm(m, x, norm=1, nw=nw, epi=1, y=y, bias=bias, lib=True)
+    xn = x * torch.rsqrt(x.pow(2).mean(-1, keepdim=True) + 1e-5) * nw
+    ref = y0 + xn @ m.w.T + bias
+    assert rel(y - y0, ref - y0) < 1e-2
+
+
+def test_gemm_lib_glu():
+    F, K, B = 320, 1024, 257
+    m = QM(GGMLType.Q4_K, 2 * F, K, seed=15)
+    x = torch.randn(B, K, device="cuda")
+    y = torch.zeros(B, F, device="cuda")
+    gemm(m, x, epi=2, y=y, lib=True)
+    gu = x @ m.w.T
+    ref = torch.nn.functional.silu(gu[:, 0::2]) * gu[:, 1::2]
+    assert rel(y, ref) < 1.5e-2
+
+
+def test_gemm_lib_matches_fused():
+    """Both prefill paths compute the same product (fp16 operands, fp32 accumulation)."""
+    N, K, B = 1024, 4096, 512
+    m = QM(GGMLType.Q4_K, N, K, seed=17)
+    x = torch.randn(B, K, device="cuda")
+    y1 = torch.zeros(B, N, device="cuda")
+    y2 = torch.zeros(B, N, device="cuda")
+    gemm(m, x, y=y1, split=False)
+    gemm(m, x, y=y2, lib=True)
+    assert rel(y1, y2) < 2e-3
