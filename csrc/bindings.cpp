@@ -440,6 +440,7 @@ PYBIND11_MODULE(_C, m) {
         w.x16 = Pp<void>(ptr("x16"));
         w.gws = Pp<float>(ptr("gws"));
         w.gws_elems = d.contains("gws_elems") ? d["gws_elems"].cast<long long>() : 0;
+        w.ext = Pp<const float>(ptr("ext"));
         w.w16 = Pp<void>(ptr("w16"));
         w.w16_elems = d.contains("w16_elems") ? d["w16_elems"].cast<long long>() : 0;
         w.yws = Pp<float>(ptr("yws"));

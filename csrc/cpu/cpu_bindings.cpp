@@ -120,6 +120,7 @@ PYBIND11_MODULE(_cpu, m) {
         b.abuf = Pp<float>(ptr("abuf"));
         b.hbuf = Pp<float>(ptr("hbuf"));
         b.ypart = Pp<float>(ptr("ypart"));
+        b.ext = Pp<const float>(ptr("ext"));
         b.max_B = d["max_B"].cast<int>();
         b.ld_logits = d.contains("ld_logits") ? d["ld_logits"].cast<int>() : e.cfg.V;
       })

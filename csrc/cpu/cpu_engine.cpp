@@ -47,9 +47,16 @@ static inline float silu(float x) { return x / (1.f + std::exp(-x)); }
 float* Engine::dst(int B) { return cfg.tp > 1 ? buf.ypart : buf.resid; }
 
 void Engine::embed(int B) {
+  for (int b = 0; b < B && !buf.ext; ++b)
+    if (buf.tokens[b] < 0) throw std::runtime_error("negative token id without external embeddings");
 #pragma omp parallel for schedule(static) if (B > 1)
   for (int b = 0; b < B; ++b) {
     float* r = buf.resid + (long long)b * cfg.E;
+    if (buf.tokens[b] < 0) {  // external embedding row -(id + 1): copied as is
+      const float* src = buf.ext + (long long)(-buf.tokens[b] - 1) * cfg.E;
+      std::copy(src, src + cfg.E, r);
+      continue;
+    }
     dequant_row(tok_embd, buf.tokens[b], r);
     if (cfg.embed_scale != 1.f)
       for (int j = 0; j < cfg.E; ++j) r[j] *= cfg.embed_scale;

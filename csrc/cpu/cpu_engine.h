@@ -51,6 +51,7 @@ struct Layer {
 struct Buffers {
   float *resid = nullptr, *qbuf = nullptr, *abuf = nullptr, *hbuf = nullptr, *ypart = nullptr;
   float *logits = nullptr;
+  const float* ext = nullptr;  // [*][E] external embedding rows for negative token ids (image patches)
   int max_B = 0, ld_logits = 0;
   // step inputs (int32 [B] each)
   const int *tokens = nullptr, *pos = nullptr, *slot = nullptr, *q_len = nullptr, *q_seq = nullptr;

@@ -5,12 +5,21 @@
 
 namespace omx {
 
-// one block per gathered row; each thread dequantises 32-weight pieces
-__global__ __launch_bounds__(256) void embed_rows_kernel(QMat w, const int* rows, float* out, int ldo, float scale) {
+// one block per gathered row; each thread dequantises 32-weight pieces. A negative row id -(j + 1)
+// takes row j of `ext` ([*][K] fp32, unscaled) instead: multimodal inputs (projected image patches,
+// models/clip.py) enter the sequence as such rows
+__global__ __launch_bounds__(256) void embed_rows_kernel(QMat w, const int* rows, float* out, int ldo, float scale,
+                                                         const float* ext) {
   const int b = blockIdx.x;
   const long long row = rows[b];
   const int P = w.K / 32;
   float* o = out + (long long)b * ldo;
+  if (row < 0) {
+    const float* src = ext + (-row - 1) * (long long)w.K;
+    OMX_KASSERT(ext != nullptr);
+    for (int i = threadIdx.x; i < w.K; i += blockDim.x) o[i] = ext ? src[i] : 0.f;
+    return;
+  }
   for (int p = threadIdx.x; p < P; p += blockDim.x) {
     float lo[16], hi[16];
     int olo, ohi;
@@ -25,9 +34,10 @@ __global__ __launch_bounds__(256) void embed_rows_kernel(QMat w, const int* rows
   }
 }
 
-void embed_rows(const QMat& w, const int* rows, int n, float* out, int ldo, hipStream_t s, float scale) {
+void embed_rows(const QMat& w, const int* rows, int n, float* out, int ldo, hipStream_t s, float scale,
+                const float* ext) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(embed_rows_kernel, dim3(n), dim3(256), 0, s, w, rows, out, ldo, scale);
+  hipLaunchKernelGGL(embed_rows_kernel, dim3(n), dim3(256), 0, s, w, rows, out, ldo, scale, ext);
 }
 
 // grid-stride over (row, piece); PERM: K order (0, 2, 1, 3) inside every 4, the order prep_x16 writes the

@@ -134,7 +134,9 @@ void set_gemv_tuning(int blocks_per_cu, int rows, int debug, int ks = -1, int xf
                      int stream = -1, int stream_bpc = -1, int pf = -1, int ws = -1);
 
 // Dequantize rows of a repacked matrix (embedding gather / fp16 copies)
-void embed_rows(const QMat& w, const int* rows, int n, float* out, int ldo, hipStream_t s, float scale = 1.f);
+// rows[i] < 0: row -(rows[i] + 1) of ext [*][w.K] (external embeddings, e.g. image patches)
+void embed_rows(const QMat& w, const int* rows, int n, float* out, int ldo, hipStream_t s, float scale = 1.f,
+                const float* ext = nullptr);
 void dequant_f16(const QMat& w, void* out_f16, hipStream_t s, int perm = 0);  // perm: prep_x16 K order
 
 struct AttnParams {

@@ -74,7 +74,7 @@ bool Executor::chain_capable() const {
 }
 
 void Executor::embed(const StepInputs& in, hipStream_t s) {
-  embed_rows(tok_embd, in.tokens, in.B, ws.resid, cfg.E, s, cfg.embed_scale);
+  embed_rows(tok_embd, in.tokens, in.B, ws.resid, cfg.E, s, cfg.embed_scale, ws.ext);
 }
 
 void Executor::attn_block(int i, const StepInputs& in, hipStream_t s) {

@@ -62,6 +62,7 @@ struct Workspace {
   int* moe_tiles = nullptr;  // [(maxB*k/128 + X + 1)*3] expert row tiles
   int* moe_ntiles = nullptr; // [1]
   long long gws_elems = 0;
+  const float* ext = nullptr;  // [*][E] external embedding rows (negative token ids), e.g. image patches
   void* w16 = nullptr;       // large-M prefill library GEMM: fp16 dequantised weight [N][K] scratch
   long long w16_elems = 0;
   float* yws = nullptr;      //   and its fp32 output slab [M][N]

@@ -184,14 +184,35 @@ def cmd_stop(a):
         c.post("/api/generate", json={"model": a.model, "keep_alive": 0})
 
 
+_IMAGE_EXT = (".png", ".jpg", ".jpeg", ".webp", ".bmp", ".gif")
+
+
+def _extract_images(prompt: str) -> tuple[str, list[str]]:
+    """As `ollama run`: words naming existing image files are attached as base64 images (multimodal
+    models) and dropped from the prompt text."""
+    import base64
+    words, images = [], []
+    for w in prompt.split(" "):
+        p = os.path.expanduser(w.strip("'\""))
+        if p.lower().endswith(_IMAGE_EXT) and os.path.isfile(p):
+            with open(p, "rb") as f:
+                images.append(base64.b64encode(f.read()).decode())
+        else:
+            words.append(w)
+    return " ".join(words), images
+
+
 def cmd_run(a):
     with _client() as c:
         r = c.post("/api/show", json={"model": a.model})
         if r.status_code == 404:
             _progress(_stream(c, "POST", "/api/pull", {"model": a.model}))
         if a.prompt:
-            prompt = " ".join(a.prompt)
-            for ev in _stream(c, "POST", "/api/generate", {"model": a.model, "prompt": prompt}):
+            prompt, images = _extract_images(" ".join(a.prompt))
+            req = {"model": a.model, "prompt": prompt}
+            if images:
+                req["images"] = images
+            for ev in _stream(c, "POST", "/api/generate", req):
                 sys.stdout.write(ev.get("response", ""))
                 sys.stdout.flush()
                 if ev.get("done") and a.verbose:

@@ -65,7 +65,7 @@ class NativeExec:
                              moe_rows=p(r.moe_rows) if cfg.n_expert else 0, moe_tiles=p(r.moe_tiles),
                              moe_ntiles=p(r.moe_ntiles),
                              gws_elems=r.gws.numel(), max_B=r.max_batch, ld_logits=r.logits.shape[1],
-                             w16=p(r.w16), w16_elems=r.w16.numel() if r.w16 is not None else 0,
+                             ext=p(r.ext), w16=p(r.w16), w16_elems=r.w16.numel() if r.w16 is not None else 0,
                              yws=p(r.yws), yws_elems=r.yws.numel() if r.yws is not None else 0,
                              n_splits=1, **self._chain_ws(r)))
         # step buffers bound once: every stage call below passes integers only
@@ -112,10 +112,11 @@ class Runner:
     def __init__(self, model_path: str, device: str | None = None, max_batch: int = 64, max_seqs: int = 4,
                  ctx: int | None = None, block_size: int = 16, tp_rank: int = 0, tp_size: int = 1,
                  tp_group=None, use_graphs: bool | None = None, weights: DeviceWeights | None = None,
-                 tp_ctrl=None, cpu_backend: str | None = None):
+                 tp_ctrl=None, cpu_backend: str | None = None, ext_rows: int = 0):
         """cpu_backend (device "cpu" only): "native" = the quantised C++ backend (csrc/cpu, the serving
         default), "torch" = the fp32 torch twin (test oracle). Default: $OMX_CPU_BACKEND, else native
-        when its module is built."""
+        when its module is built. ext_rows: capacity of the external embedding rows (image patches of
+        multimodal prompts, `set_ext`); 0 = text only."""
         t0 = time.perf_counter()
         if device is None:
             device = f"cuda:{torch.cuda.current_device()}" if torch.cuda.is_available() else "cpu"
@@ -190,6 +191,11 @@ class Runner:
         self.moe_rows = torch.zeros(n_pairs, **i32)
         self.moe_tiles = torch.zeros(3 * (n_pairs // 128 + max(1, cfg.n_expert) + 1), **i32)
         self.moe_ntiles = torch.zeros(1, **i32)
+        # external embedding rows (multimodal prompts): token id t < 0 maps through _ext_map to a row of
+        # self.ext, which the embed stage copies instead of a token embedding (models/clip.py)
+        self.ext = torch.zeros(ext_rows, E, **f32) if ext_rows > 0 else None
+        self._ext_map: dict[int, int] = {}
+        self._ext_next = 0
         # split-K partial slabs of small-M prefill GEMMs (the kernel picks splits that fit)
         self.gws = torch.zeros(GEMM_SPLIT_WS_FLOATS if str(dev).startswith("cuda") else 1, **f32)
         # large-M prefill on hipBLASLt (gemm.hip gemm_lib): fp16 dequantised-weight scratch sized for the
@@ -379,8 +385,48 @@ class Runner:
         self._adv_next = None
         self.kv.free_seq(sid)
 
+    def set_ext(self, ids: list[int], rows) -> None:
+        """Register external embedding rows (e.g. an image's projected patches) under negative token
+        ids; prompts then carry those ids where the rows belong. Rows are kept in a ring of ext_rows
+        (an id already registered keeps its row), so ids of requests still waiting for their prefill
+        stay valid while the ring holds them."""
+        if self.ext is None:
+            raise ValueError("this runner has no external embedding rows (ext_rows=0)")
+        rows = torch.as_tensor(np.asarray(rows, np.float32) if not isinstance(rows, torch.Tensor) else rows)
+        if rows.dim() != 2 or rows.shape[1] != self.ext.shape[1] or rows.shape[0] != len(ids):
+            raise ValueError(f"external rows must be [{len(ids)}, {self.ext.shape[1]}], got {tuple(rows.shape)}")
+        cap = self.ext.shape[0]
+        if len(ids) > cap:
+            raise ValueError(f"{len(ids)} external rows exceed the capacity {cap}")
+        if any(i >= 0 for i in ids):
+            raise ValueError("external embedding ids must be negative")
+        new = [j for j, i in enumerate(ids) if i not in self._ext_map]
+        if not new:
+            return
+        if self._ext_next + len(new) > cap:
+            self._ext_next = 0
+        taken = set(range(self._ext_next, self._ext_next + len(new)))
+        self._ext_map = {i: r for i, r in self._ext_map.items() if r not in taken}
+        dst = torch.arange(self._ext_next, self._ext_next + len(new))
+        self.ext[dst.to(self.ext.device)] = rows[new].to(self.ext.device, torch.float32)
+        for k, j in enumerate(new):
+            self._ext_map[ids[j]] = self._ext_next + k
+        self._ext_next += len(new)
+        if self.is_gpu:
+            torch.cuda.synchronize(self.device)  # visible to a prefill issued from another thread
+
+    def _device_tokens(self, tokens) -> np.ndarray:
+        a = np.asarray(tokens, np.int64)
+        if (a < 0).any():
+            try:
+                a = np.array([t if t >= 0 else -(self._ext_map[t] + 1) for t in a.tolist()], np.int64)
+            except KeyError as e:
+                raise ValueError(f"external embedding id {e.args[0]} is not registered (set_ext)") from None
+        return a.astype(np.int32)
+
     def prefill(self, sid: int, tokens: list[int], want_logits: bool = True) -> None:
-        """Append `tokens` to sequence `sid` (KV computed), leaving logits of the last one in row 0."""
+        """Append `tokens` to sequence `sid` (KV computed), leaving logits of the last one in row 0.
+        Negative ids are external embedding rows registered with `set_ext`."""
         s = self.kv.seqs[sid]
         start = s.length
         n = len(tokens)
@@ -397,7 +443,7 @@ class Runner:
             last = c0 + B >= n
             arr = np.stack([pos, slots, pos + 1, np.full(B, s.row, np.int32),
                             np.full(B, B - 1, np.int32)]).astype(np.int32)
-            self._upload(arr, np.asarray(chunk, np.int32))
+            self._upload(arr, self._device_tokens(chunk))
             with trace_range(f"prefill B={B}"):
                 self.forward(B, 1 if (last and want_logits) else 0, use_idx=True, prefill=True)
         s.tokens.extend(tokens)
@@ -425,6 +471,7 @@ class Runner:
 
     # ------------------------------------------------------------------ sampling
     def _set_sampler(self, row: int, o: SamplingOptions, history: list[int], seed: int, step: int = 0):
+        history = [t for t in history if t >= 0]  # external embedding rows (images) are not tokens
         self.s_temp[row] = o.temperature
         self.s_topk[row] = o.top_k
         self.s_topp[row] = o.top_p

@@ -1,0 +1,284 @@
+"""LLaVA vision side: the CLIP ViT image encoder + multimodal projector of an Ollama `projector` layer
+(a GGUF with general.architecture = "clip", llama.cpp's mmproj layout), producing one LLM-width
+embedding row per image patch. The rows enter the language model's sequence as external embedding
+rows (negative token ids, engine/runner.py `set_ext`), so prefill, KV prefix reuse, continuous
+batching and tensor parallelism work for image prompts unchanged.
+
+The reference lists LLaVA among the models its images serve (/root/reference/README.md:57, via
+ollama/ollama); the projector media type is `application/vnd.ollama.image.projector`
+(server/store.py MT_PROJECTOR).
+
+Design: the encoder runs once per image (576 patches for LLaVA-1.5 at 336 px), so it is a plain
+PyTorch module on the runner's device -- fp16 GEMMs on hipBLASLt and fused SDPA attention on the
+GPU -- not a hand-written kernel path; the language model's prefill/decode loop is where the time
+goes. Image preprocessing follows LLaVA-1.5 ("pad" aspect): pad to a square with the mean colour,
+resize to image_size, normalise by image_mean / image_std.
+
+Tensor names / metadata (llama.cpp clip GGUF): v.patch_embd.weight [E,3,p,p], v.class_embd [E],
+v.position_embd.weight [n_pos,E], v.pre_ln.{weight,bias}, v.blk.{i}.{attn_q,attn_k,attn_v,attn_out,
+ffn_up,ffn_down}.{weight,bias}, v.blk.{i}.{ln1,ln2}.{weight,bias}, optional v.post_ln, projector
+mm.0 / mm.2 (Linear-GELU-Linear, projector_type "mlp"); clip.vision.{image_size, patch_size,
+embedding_length, feature_length, block_count, attention.head_count, attention.layer_norm_epsilon,
+image_mean, image_std}, clip.use_gelu (false: quick-GELU as OpenAI CLIP). Parity unpinned: no real
+mmproj file exists in this environment; tests pin the module to an independent fp32 numpy oracle.
+"""
+from __future__ import annotations
+
+import hashlib
+import io
+import math
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from ..gguf import read_gguf
+
+MAX_PATCHES_PER_IMAGE = 4096
+
+
+class VisionError(ValueError):
+    pass
+
+
+@dataclass
+class ClipConfig:
+    image_size: int
+    patch_size: int
+    E: int
+    F: int
+    n_layer: int
+    n_head: int
+    eps: float
+    mean: tuple[float, float, float]
+    std: tuple[float, float, float]
+    use_gelu: bool
+    projector: str
+    out_dim: int
+
+    @property
+    def n_patches(self) -> int:
+        return (self.image_size // self.patch_size) ** 2
+
+
+def clip_config(md: dict, tensors: dict) -> ClipConfig:
+    if str(md.get("general.architecture", "")) != "clip":
+        raise VisionError("projector is not a CLIP GGUF (general.architecture != clip)")
+    g = lambda k, d=None: md.get("clip.vision." + k, d)  # noqa: E731
+    proj = str(md.get("clip.projector_type", "mlp"))
+    if proj != "mlp":
+        raise VisionError(f"unsupported projector type {proj!r} (supported: mlp)")
+    out_dim = tensors["mm.2.weight"].torch_shape[0]
+    return ClipConfig(image_size=int(g("image_size", 336)), patch_size=int(g("patch_size", 14)),
+                      E=int(g("embedding_length")), F=int(g("feature_length")), n_layer=int(g("block_count")),
+                      n_head=int(g("attention.head_count")), eps=float(g("attention.layer_norm_epsilon", 1e-5)),
+                      mean=tuple(float(v) for v in g("image_mean", (0.48145466, 0.4578275, 0.40821073))),
+                      std=tuple(float(v) for v in g("image_std", (0.26862954, 0.26130258, 0.27577711))),
+                      use_gelu=bool(md.get("clip.use_gelu", False)), projector=proj, out_dim=int(out_dim))
+
+
+def preprocess(image: bytes | np.ndarray, cfg: ClipConfig) -> np.ndarray:
+    """Encoded image bytes (PNG/JPEG/...) or an HxWx3 uint8 array -> float32 [3, S, S] normalised."""
+    from PIL import Image
+    if isinstance(image, (bytes, bytearray)):
+        try:
+            im = Image.open(io.BytesIO(image))
+            im.load()
+        except Exception as e:  # noqa: BLE001 -- any decoder error is a bad request
+            raise VisionError(f"cannot decode image: {e}") from None
+    else:
+        im = Image.fromarray(np.asarray(image, dtype=np.uint8))
+    im = im.convert("RGB")
+    w, h = im.size
+    side = max(w, h)
+    bg = tuple(int(round(255 * m)) for m in cfg.mean)
+    sq = Image.new("RGB", (side, side), bg)
+    sq.paste(im, ((side - w) // 2, (side - h) // 2))
+    sq = sq.resize((cfg.image_size, cfg.image_size), Image.BICUBIC)
+    a = np.asarray(sq, dtype=np.float32) / 255.0
+    a = (a - np.asarray(cfg.mean, np.float32)) / np.asarray(cfg.std, np.float32)
+    return np.ascontiguousarray(a.transpose(2, 0, 1))
+
+
+class ClipEncoder:
+    """CLIP ViT + LLaVA MLP projector on `device` (fp16 on GPU, fp32 on CPU)."""
+
+    def __init__(self, path: str, device: str | torch.device = "cpu"):
+        self.device = torch.device(device)
+        self.dtype = torch.float16 if self.device.type == "cuda" else torch.float32
+        g = read_gguf(path)
+        try:
+            self.cfg = clip_config(g.metadata, g.tensors)
+            t = lambda n: torch.from_numpy(np.array(g.array(n), np.float32)).to(self.device, self.dtype)  # noqa: E731
+            opt = lambda n: t(n) if n in g.tensors else None  # noqa: E731
+            self.patch_w = t("v.patch_embd.weight")
+            self.patch_b = opt("v.patch_embd.bias")
+            self.cls = t("v.class_embd").reshape(-1)
+            self.pos = t("v.position_embd.weight")
+            self.pre_ln = (opt("v.pre_ln.weight"), opt("v.pre_ln.bias"))
+            self.post_ln = (opt("v.post_ln.weight"), opt("v.post_ln.bias"))
+            self.blocks = []
+            for i in range(self.cfg.n_layer):
+                b = f"v.blk.{i}."
+                self.blocks.append({k: t(b + k) for k in (
+                    "attn_q.weight", "attn_q.bias", "attn_k.weight", "attn_k.bias", "attn_v.weight", "attn_v.bias",
+                    "attn_out.weight", "attn_out.bias", "ln1.weight", "ln1.bias", "ln2.weight", "ln2.bias",
+                    "ffn_up.weight", "ffn_up.bias", "ffn_down.weight", "ffn_down.bias")})
+            self.mm = [(t("mm.0.weight"), t("mm.0.bias")), (t("mm.2.weight"), t("mm.2.bias"))]
+        finally:
+            g.close()
+        if self.pos.shape[0] != self.cfg.n_patches + 1:
+            raise VisionError(f"position table has {self.pos.shape[0]} rows, expected {self.cfg.n_patches + 1}")
+
+    @property
+    def out_dim(self) -> int:
+        return self.cfg.out_dim
+
+    def _act(self, x: torch.Tensor) -> torch.Tensor:
+        if self.cfg.use_gelu:
+            return F.gelu(x)
+        return x * torch.sigmoid(1.702 * x)  # quick-GELU (OpenAI CLIP)
+
+    @torch.no_grad()
+    def encode_pixels(self, px: np.ndarray | torch.Tensor) -> torch.Tensor:
+        """[3, S, S] normalised pixels -> [n_patches, out_dim] fp32 LLM embedding rows."""
+        c = self.cfg
+        x = torch.as_tensor(px).to(self.device, self.dtype)[None]
+        x = F.conv2d(x, self.patch_w, self.patch_b, stride=c.patch_size)  # [1, E, g, g]
+        x = x.flatten(2).transpose(1, 2)[0]  # [n_patches, E], row-major patch order
+        x = torch.cat([self.cls[None], x], 0) + self.pos
+        if self.pre_ln[0] is not None:
+            x = F.layer_norm(x, (c.E,), self.pre_ln[0], self.pre_ln[1], c.eps)
+        H, D = c.n_head, c.E // c.n_head
+        n = x.shape[0]
+        for b in self.blocks:
+            h = F.layer_norm(x, (c.E,), b["ln1.weight"], b["ln1.bias"], c.eps)
+            q = F.linear(h, b["attn_q.weight"], b["attn_q.bias"]).view(n, H, D).transpose(0, 1)
+            k = F.linear(h, b["attn_k.weight"], b["attn_k.bias"]).view(n, H, D).transpose(0, 1)
+            v = F.linear(h, b["attn_v.weight"], b["attn_v.bias"]).view(n, H, D).transpose(0, 1)
+            a = F.scaled_dot_product_attention(q[None], k[None], v[None])[0]  # bidirectional
+            x = x + F.linear(a.transpose(0, 1).reshape(n, c.E), b["attn_out.weight"], b["attn_out.bias"])
+            h = F.layer_norm(x, (c.E,), b["ln2.weight"], b["ln2.bias"], c.eps)
+            h = self._act(F.linear(h, b["ffn_up.weight"], b["ffn_up.bias"]))
+            x = x + F.linear(h, b["ffn_down.weight"], b["ffn_down.bias"])
+        if self.post_ln[0] is not None:
+            x = F.layer_norm(x, (c.E,), self.post_ln[0], self.post_ln[1], c.eps)
+        x = x[1:]  # LLaVA drops the class token
+        (w0, b0), (w2, b2) = self.mm
+        x = F.linear(F.gelu(F.linear(x, w0, b0)), w2, b2)
+        return x.float()
+
+    def encode(self, image: bytes | np.ndarray) -> torch.Tensor:
+        return self.encode_pixels(preprocess(image, self.cfg))
+
+
+def image_token_ids(image: bytes, n: int) -> list[int]:
+    """Content-derived negative ids for an image's n patch rows: the same image gets the same ids (so a
+    KV prefix holding it is reused), different images practically never collide. |id| < 2^31."""
+    if n > MAX_PATCHES_PER_IMAGE:
+        raise VisionError(f"{n} patches per image exceeds {MAX_PATCHES_PER_IMAGE}")
+    h = int.from_bytes(hashlib.sha256(bytes(image)).digest()[:8], "little") % 500_000
+    base = 1 + h * MAX_PATCHES_PER_IMAGE
+    return [-(base + j) for j in range(n)]
+
+
+# ---------------------------------------------------------------------------------------------------
+# fp32 numpy oracle (tests) and random-init projector files
+def reference_encode(path: str, px: np.ndarray) -> np.ndarray:
+    """Independent float64 numpy forward of the same GGUF (test oracle for ClipEncoder)."""
+    g = read_gguf(path)
+    try:
+        c = clip_config(g.metadata, g.tensors)
+        a = lambda n: np.asarray(g.array(n), np.float64)  # noqa: E731
+        p = c.patch_size
+        gsz = c.image_size // p
+        w = a("v.patch_embd.weight").reshape(c.E, -1)  # [E, 3*p*p]
+        patches = px.astype(np.float64).reshape(3, gsz, p, gsz, p).transpose(1, 3, 0, 2, 4).reshape(gsz * gsz, -1)
+        x = patches @ w.T
+        if "v.patch_embd.bias" in g.tensors:
+            x = x + a("v.patch_embd.bias")
+        x = np.concatenate([a("v.class_embd").reshape(1, -1), x], 0) + a("v.position_embd.weight")
+
+        def ln(x, wn, bn):
+            mu = x.mean(-1, keepdims=True)
+            var = ((x - mu) ** 2).mean(-1, keepdims=True)
+            return (x - mu) / np.sqrt(var + c.eps) * a(wn) + a(bn)
+
+        if "v.pre_ln.weight" in g.tensors:
+            x = ln(x, "v.pre_ln.weight", "v.pre_ln.bias")
+        H, D = c.n_head, c.E // c.n_head
+        n = x.shape[0]
+        lin = lambda h, name: h @ a(name + ".weight").T + a(name + ".bias")  # noqa: E731
+        for i in range(c.n_layer):
+            b = f"v.blk.{i}."
+            h = ln(x, b + "ln1.weight", b + "ln1.bias")
+            q = lin(h, b + "attn_q").reshape(n, H, D).transpose(1, 0, 2)
+            k = lin(h, b + "attn_k").reshape(n, H, D).transpose(1, 0, 2)
+            v = lin(h, b + "attn_v").reshape(n, H, D).transpose(1, 0, 2)
+            s = q @ k.transpose(0, 2, 1) / math.sqrt(D)
+            s = np.exp(s - s.max(-1, keepdims=True))
+            s /= s.sum(-1, keepdims=True)
+            o = (s @ v).transpose(1, 0, 2).reshape(n, c.E)
+            x = x + lin(o, b + "attn_out")
+            h = lin(ln(x, b + "ln2.weight", b + "ln2.bias"), b + "ffn_up")
+            h = 0.5 * h * (1 + np.vectorize(math.erf)(h / math.sqrt(2))) if c.use_gelu else h / (1 + np.exp(-1.702 * h))
+            x = x + lin(h, b + "ffn_down")
+        if "v.post_ln.weight" in g.tensors:
+            x = ln(x, "v.post_ln.weight", "v.post_ln.bias")
+        x = x[1:]
+        h = lin(x, "mm.0")
+        h = 0.5 * h * (1 + np.vectorize(math.erf)(h / math.sqrt(2)))
+        return lin(h, "mm.2")
+    finally:
+        g.close()
+
+
+def write_random_clip_gguf(path: str, out_dim: int, image_size: int = 336, patch_size: int = 14, E: int = 1024,
+                           F_: int = 4096, n_layer: int = 23, n_head: int = 16, seed: int = 0,
+                           use_gelu: bool = False) -> None:
+    """Random-init LLaVA-1.5-shaped projector file (F16 matrices, F32 norms/biases), as llama.cpp's
+    llava surgery writes it. Defaults: CLIP ViT-L/14-336 with 23 of 24 blocks, 4096-wide MLP projector."""
+    from ..gguf.constants import GGMLType
+    from ..gguf.writer import GGUFWriter
+    rng = np.random.default_rng(seed)
+    w = GGUFWriter(path)
+    md = {"general.architecture": "clip", "general.name": "random-clip", "clip.has_text_encoder": False,
+          "clip.has_vision_encoder": True, "clip.has_llava_projector": True, "clip.projector_type": "mlp",
+          "clip.use_gelu": bool(use_gelu), "clip.vision.image_size": image_size, "clip.vision.patch_size": patch_size,
+          "clip.vision.embedding_length": E, "clip.vision.feature_length": F_, "clip.vision.projection_dim": 768,
+          "clip.vision.block_count": n_layer, "clip.vision.attention.head_count": n_head,
+          "clip.vision.attention.layer_norm_epsilon": 1e-5,
+          "clip.vision.image_mean": [0.48145466, 0.4578275, 0.40821073],
+          "clip.vision.image_std": [0.26862954, 0.26130258, 0.27577711]}
+    for k, v in md.items():
+        w.add(k, v)
+    n_pos = (image_size // patch_size) ** 2 + 1
+
+    def add(name, torch_shape, std, f16=True, base=0.0):
+        data = (base + std * rng.standard_normal(int(np.prod(torch_shape)))).astype(np.float32)
+        gt = GGMLType.F16 if f16 else GGMLType.F32
+        w.add_tensor(name, tuple(reversed(torch_shape)), gt, data.astype(np.float16) if f16 else data)
+
+    add("v.patch_embd.weight", (E, 3, patch_size, patch_size), 0.02)
+    add("v.class_embd", (E,), 0.02, f16=False)
+    add("v.position_embd.weight", (n_pos, E), 0.02)
+    add("v.pre_ln.weight", (E,), 0.05, f16=False, base=1.0)
+    add("v.pre_ln.bias", (E,), 0.02, f16=False)
+    for i in range(n_layer):
+        b = f"v.blk.{i}."
+        for m in ("attn_q", "attn_k", "attn_v", "attn_out"):
+            add(b + m + ".weight", (E, E), 1.0 / math.sqrt(E))
+            add(b + m + ".bias", (E,), 0.02, f16=False)
+        add(b + "ffn_up.weight", (F_, E), 1.0 / math.sqrt(E))
+        add(b + "ffn_up.bias", (F_,), 0.02, f16=False)
+        add(b + "ffn_down.weight", (E, F_), 1.0 / math.sqrt(F_))
+        add(b + "ffn_down.bias", (E,), 0.02, f16=False)
+        for ln in ("ln1", "ln2"):
+            add(b + ln + ".weight", (E,), 0.05, f16=False, base=1.0)
+            add(b + ln + ".bias", (E,), 0.02, f16=False)
+    add("mm.0.weight", (out_dim, E), 1.0 / math.sqrt(E))
+    add("mm.0.bias", (out_dim,), 0.02, f16=False)
+    add("mm.2.weight", (out_dim, out_dim), 1.0 / math.sqrt(out_dim))
+    add("mm.2.bias", (out_dim,), 0.02, f16=False)
+    w.write()

@@ -64,7 +64,10 @@ class TorchExecutor:
     def embed(self, B: int):
         r = self.r
         toks = r.d_tokens[:B].long()
-        r.resid[:B] = self.W(self.w.tok_embd)[toks] * self.w.cfg.embed_scale
+        r.resid[:B] = self.W(self.w.tok_embd)[toks.clamp(min=0)] * self.w.cfg.embed_scale
+        ext = toks < 0  # external embedding rows -(id + 1) (image patches), unscaled
+        if bool(ext.any()):
+            r.resid[:B][ext] = r.ext[(-toks[ext] - 1)].to(r.resid.dtype)
 
     def attn(self, i: int, B: int):
         r, w = self.r, self.w

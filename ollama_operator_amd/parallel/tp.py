@@ -197,6 +197,13 @@ class TPRunnerProxy:
         self._mirror("embed", tokens=list(tokens))
         return self.r.embed(tokens)
 
+    def set_ext(self, ids: list[int], rows) -> None:  # image patch rows: every rank embeds them
+        import numpy as np
+        rows = np.ascontiguousarray(rows.detach().float().cpu().numpy() if hasattr(rows, "detach") else rows,
+                                    dtype=np.float32)
+        self._mirror("set_ext", ids=list(ids), rows=rows)
+        self.r.set_ext(ids, rows)
+
     def generate(self, sid: int, prompt: list[int], options=None, max_tokens: int = 128, stop=None, times=None):
         from ..engine.sampling import SamplingOptions
         o = options or SamplingOptions()
@@ -232,12 +239,12 @@ class TPRunnerProxy:
         self.r.close()
 
 
-def load_tp_runner(world: TPWorld, path: str, max_batch: int, max_seqs: int, ctx: int):
+def load_tp_runner(world: TPWorld, path: str, max_batch: int, max_seqs: int, ctx: int, ext_rows: int = 0):
     from ..engine.runner import Runner
-    cmd = dict(path=path, max_batch=max_batch, max_seqs=max_seqs, ctx=ctx)
+    cmd = dict(path=path, max_batch=max_batch, max_seqs=max_seqs, ctx=ctx, ext_rows=ext_rows)
     world.ctrl.send_cmd({"op": "load", **cmd})
     r = Runner(path, device=world.device, max_batch=max_batch, max_seqs=max_seqs, ctx=ctx, tp_rank=0,
-               tp_size=world.size, tp_group=world.compute_group, tp_ctrl=world.ctrl)
+               tp_size=world.size, tp_group=world.compute_group, tp_ctrl=world.ctrl, ext_rows=ext_rows)
     if r.ar is not None:
         world.ar_probe = r.ar.error
     return TPRunnerProxy(world, r, cmd)
@@ -260,7 +267,8 @@ def worker_main() -> None:
             break
         if op == "load":
             runner = Runner(cmd["path"], device=dev, max_batch=cmd["max_batch"], max_seqs=cmd["max_seqs"],
-                            ctx=cmd["ctx"], tp_rank=rank, tp_size=size, tp_group=compute, tp_ctrl=ctrl)
+                            ctx=cmd["ctx"], tp_rank=rank, tp_size=size, tp_group=compute, tp_ctrl=ctrl,
+                            ext_rows=cmd.get("ext_rows", 0))
         elif op == "unload":
             if runner is not None:
                 runner.close()
@@ -275,6 +283,8 @@ def worker_main() -> None:
             runner.free_sequence(cmd["sid"])
         elif op == "embed":
             runner.embed(cmd["tokens"])
+        elif op == "set_ext":
+            runner.set_ext(cmd["ids"], cmd["rows"])
         elif op == "generate":
             for _ in runner.generate(cmd["sid"], cmd["prompt"], cmd["options"], max_tokens=cmd["max_tokens"]):
                 pass

@@ -25,8 +25,10 @@ from fastapi.responses import JSONResponse, PlainTextResponse, Response, Streami
 from .. import __version__
 from .manager import GenResult, ModelManager
 from .registry import PullError, pull, push
-from .store import (MT_TEMPLATE, ModelName, ModelStore, StoreError, gguf_config, now_rfc3339, parse_modelfile,
+from .store import (MT_TEMPLATE, ModelName, ModelStore, StoreError, gguf_arch, gguf_config, now_rfc3339,
+                    parse_modelfile,
                     render_modelfile)
+from ..models.clip import VisionError
 from .template import TemplateError, render_chat, render_generate
 
 OLLAMA_COMPAT_VERSION = "0.5.4"
@@ -56,6 +58,41 @@ def _ndjson(it: Iterator[dict], on_fault=None) -> StreamingResponse:
                 on_fault()
             yield json.dumps({"error": f"{type(e).__name__}: {e}"}) + "\n"
     return StreamingResponse(gen(), media_type="application/x-ndjson")
+
+
+def _images(raw) -> list[bytes]:
+    """Ollama `images`: base64 strings (a data: URL prefix is tolerated)."""
+    import base64
+    import binascii
+    out = []
+    for v in raw or []:
+        v = str(v)
+        if v.startswith("data:") and "," in v:
+            v = v.split(",", 1)[1]
+        try:
+            out.append(base64.b64decode(v, validate=False))
+        except (binascii.Error, ValueError):
+            raise VisionError("images must be base64-encoded") from None
+    return out
+
+
+def _with_image_marks(text: str, n: int, first: int) -> str:
+    """Images [first, first + n) of the request go where their [img-N] markers are, else in front."""
+    missing = [i for i in range(first, first + n) if f"[img-{i}]" not in text]
+    return "".join(f"[img-{i}] " for i in missing) + text
+
+
+def _chat_images(msgs: list[dict]) -> tuple[list[dict], list[bytes]]:
+    out, images = [], []
+    for m in msgs:
+        imgs = _images(m.get("images"))
+        m = dict(m)
+        if imgs:
+            m["content"] = _with_image_marks(m.get("content") or "", len(imgs), len(images))
+            images += imgs
+        m.pop("images", None)
+        out.append(m)
+    return out, images
 
 
 def _model_of(body: dict) -> str:
@@ -159,6 +196,7 @@ def create_app(store: ModelStore | None = None, manager: ModelManager | None = N
                 text = body.get("modelfile") or open(body["path"]).read()
                 mf = parse_modelfile(text)
                 frm = mf.get("from")
+                extra = list(mf.get("froms") or [])[1:]
                 tmpl, system, params = mf.get("template"), mf.get("system"), mf.get("parameters") or None
                 messages = mf.get("messages") or None
                 license_text = mf.get("license")
@@ -166,15 +204,23 @@ def create_app(store: ModelStore | None = None, manager: ModelManager | None = N
                 frm = body.get("from")
                 tmpl, system, params = body.get("template"), body.get("system"), body.get("parameters")
                 messages, license_text = body.get("messages"), body.get("license")
+                extra = []
                 if body.get("files"):  # {"name.gguf": "sha256:..."} uploaded via /api/blobs
-                    digest = next(iter(body["files"].values()))
-                    frm = store.blob_path(digest)
+                    paths = [store.blob_path(d) for d in body["files"].values()]
+                    frm, extra = paths[0], paths[1:]
             if not frm:
                 raise StoreError("no FROM line")
-            src = os.path.expanduser(frm)
+            # LLaVA: the CLIP GGUF (mmproj) among the FROM files becomes the projector layer
+            files = [os.path.expanduser(f) for f in [frm] + extra]
+            proj = [f for f in files if os.path.isfile(f) and gguf_arch(f) == "clip"]
+            rest = [f for f in files if f not in proj]
+            if len(proj) > 1 or len(rest) != 1:
+                raise StoreError("create takes one model and at most one projector")
+            src = rest[0]
             is_file = os.path.isfile(src) or src.startswith(store.blobs_dir)
-            store.create(name, gguf_path=src if is_file else None, from_model=None if is_file else frm,
-                         template=tmpl, system=system, params=params, license_text=license_text, messages=messages)
+            store.create(name, gguf_path=src if is_file else None, from_model=None if is_file else src,
+                         template=tmpl, system=system, params=params, license_text=license_text, messages=messages,
+                         projector_path=proj[0] if proj else None)
         except (StoreError, OSError, ValueError) as e:
             return _err(str(e))
         evs = [{"status": "reading model metadata"}, {"status": "writing manifest"}, {"status": "success"}]
@@ -286,13 +332,16 @@ def create_app(store: ModelStore | None = None, manager: ModelManager | None = N
                 return {"model": model, "created_at": now_rfc3339(), "response": "", "done": True,
                         "done_reason": "load"}
             lm, load_ns = await run_in_threadpool(_load, body)
+            images = _images(body.get("images"))
+            prompt = _with_image_marks(body.get("prompt", ""), len(images), 0)
             if body.get("raw"):
-                text = body.get("prompt", "")
+                text = prompt
             else:
-                text = render_generate(body.get("template") or lm.template, body.get("prompt", ""),
+                text = render_generate(body.get("template") or lm.template, prompt,
                                        body.get("system") or lm.system, body.get("suffix"))
-            ids = list(body.get("context") or []) + lm.tokenizer.encode(text, add_bos=not body.get("context"))
-        except (StoreError, TemplateError) as e:
+            ids = list(body.get("context") or []) + await run_in_threadpool(
+                manager.encode_prompt, lm, text, images, not body.get("context"))
+        except (StoreError, TemplateError, VisionError) as e:
             return _err(str(e), 404 if "not found" in str(e) else 400)
         gen = manager.generate(lm, ids, body.get("options"), load_ns, t_start)
         base = {"model": model, "created_at": ""}
@@ -338,9 +387,10 @@ def create_app(store: ModelStore | None = None, manager: ModelManager | None = N
                 return {"model": model, "created_at": now_rfc3339(), "message": {"role": "assistant", "content": ""},
                         "done": True, "done_reason": "load"}
             lm, load_ns = await run_in_threadpool(_load, body)
+            msgs, images = _chat_images(msgs)
             text = render_chat(lm.template, msgs, lm.system, body.get("tools"))
-            ids = lm.tokenizer.encode(text)
-        except (StoreError, TemplateError) as e:
+            ids = await run_in_threadpool(manager.encode_prompt, lm, text, images)
+        except (StoreError, TemplateError, VisionError) as e:
             return _err(str(e), 404 if "not found" in str(e) else 400)
         gen = manager.generate(lm, ids, body.get("options"), load_ns, t_start)
         metrics.requests.labels("chat").inc()
@@ -428,11 +478,20 @@ def create_app(store: ModelStore | None = None, manager: ModelManager | None = N
             msgs = []
             for m in body.get("messages") or []:
                 c = m.get("content", "")
-                if isinstance(c, list):  # content parts
+                imgs = []
+                if isinstance(c, list):  # content parts; images as base64 data URLs
+                    for p in c:
+                        if p.get("type") == "image_url":
+                            url = (p.get("image_url") or {}).get("url", "") if isinstance(p.get("image_url"), dict) \
+                                else str(p.get("image_url") or "")
+                            if not url.startswith("data:") or "," not in url:
+                                raise VisionError("only base64 data: URLs are supported for image_url")
+                            imgs.append(url.split(",", 1)[1])
                     c = "".join(p.get("text", "") for p in c if p.get("type") == "text")
-                msgs.append({"role": m.get("role"), "content": c})
-            ids = lm.tokenizer.encode(render_chat(lm.template, msgs, lm.system))
-        except (StoreError, TemplateError) as e:
+                msgs.append({"role": m.get("role"), "content": c, "images": imgs})
+            msgs, images = _chat_images(msgs)
+            ids = await run_in_threadpool(manager.encode_prompt, lm, render_chat(lm.template, msgs, lm.system), images)
+        except (StoreError, TemplateError, VisionError) as e:
             return JSONResponse({"error": {"message": str(e), "type": "invalid_request_error"}},
                                 status_code=404 if "not found" in str(e) else 400)
         cid = "chatcmpl-" + uuid.uuid4().hex[:12]

@@ -15,10 +15,18 @@ import numpy as np
 
 from ..engine.sampling import SamplingOptions
 from ..tokenizer import StreamDecoder, Tokenizer, from_gguf_metadata
-from .store import MT_SYSTEM, MT_TEMPLATE, ModelName, ModelStore, StoreError
+from .store import MT_PROJECTOR, MT_SYSTEM, MT_TEMPLATE, ModelName, ModelStore, StoreError
 
 DEFAULT_KEEP_ALIVE = float(os.environ.get("OLLAMA_KEEP_ALIVE_SECONDS", "300"))
 DEFAULT_NUM_CTX = int(os.environ.get("OLLAMA_CONTEXT_LENGTH", "2048"))
+
+
+def _cuda_available() -> bool:
+    try:
+        import torch
+        return torch.cuda.is_available()
+    except Exception:  # noqa: BLE001
+        return False
 
 
 def parse_keep_alive(v: Any) -> float:
@@ -57,6 +65,7 @@ class LoadedModel:
     lock: threading.Lock = field(default_factory=threading.Lock)
     sid: int | None = None
     scheduler: Any = None  # engine.scheduler.BatchScheduler (OLLAMA_NUM_PARALLEL > 1, single rank)
+    vision: Any = None     # models.clip.ClipEncoder when the manifest has a projector layer (LLaVA)
 
 
 @dataclass
@@ -149,6 +158,16 @@ class ModelManager:
         ctx = min(num_ctx, ctx_cap) if ctx_cap else num_ctx
         # prefill chunk = MFMA GEMM M dimension (weights cross HBM once per chunk)
         chunk = int(os.environ.get("OMX_PREFILL_CHUNK", "2048"))  # 2048-token TTFT 117 -> 94 ms vs 512
+        # multimodal (LLaVA): the projector layer's CLIP encoder runs on the leader; its patch rows enter
+        # the sequence as external embedding rows (room for OMX_IMAGE_ROWS, default 8 LLaVA-1.5 images)
+        vision, ext_rows = None, 0
+        pl = m.layer(MT_PROJECTOR)
+        if pl is not None:
+            from ..models.clip import ClipEncoder
+            dev = self.tp_world.device if self.tp_world is not None else (self.device or (
+                "cuda" if _cuda_available() else "cpu"))
+            vision = ClipEncoder(self.store.blob_path(pl["digest"]), dev)
+            ext_rows = int(os.environ.get("OMX_IMAGE_ROWS", str(8 * vision.cfg.n_patches)))
         scheduler = None
         # continuous batching (Ollama OLLAMA_NUM_PARALLEL): parallel rows + as many idle sequences
         # kept for prefix reuse; KV is sized for all of them at full context (288 GB HBM)
@@ -159,15 +178,19 @@ class ModelManager:
         max_seqs = max(2, 2 * par + 1)
         if self.tp_world is not None:  # tensor parallel: every rank loads its shard (parallel/tp.py)
             from ..parallel.tp import load_tp_runner
-            runner = load_tp_runner(self.tp_world, path, max_batch=chunk, max_seqs=max_seqs, ctx=ctx)
+            runner = load_tp_runner(self.tp_world, path, max_batch=chunk, max_seqs=max_seqs, ctx=ctx,
+                                    ext_rows=ext_rows)
         else:
-            runner = Runner(path, device=self.device, max_batch=chunk, max_seqs=max_seqs, ctx=ctx)
+            runner = Runner(path, device=self.device, max_batch=chunk, max_seqs=max_seqs, ctx=ctx, ext_rows=ext_rows)
+        if vision is not None and vision.out_dim != runner.cfg.n_embd:
+            raise StoreError(f"projector output width {vision.out_dim} != model embedding width {runner.cfg.n_embd}")
         runner.warmup()
         if par > 1:  # under TP the scheduler drives the leader's proxy; followers replay every call
             from ..engine.scheduler import BatchScheduler
             runner.capture_batch_graphs(par)
             scheduler = BatchScheduler(runner, max_parallel=par)
         return LoadedModel(name=name, digest=m.digest, path=path, runner=runner, tokenizer=tok, scheduler=scheduler,
+                           vision=vision,
                            template=self.store.text_layer(m, MT_TEMPLATE), system=self.store.text_layer(m, MT_SYSTEM),
                            params=self.store.params(m), num_ctx=runner.ctx, size=os.path.getsize(path),
                            load_duration_ns=int((time.perf_counter() - t0) * 1e9))
@@ -265,6 +288,44 @@ class ModelManager:
         res.eval_duration = int(times.gen_s * 1e9)
         res.total_duration = int((time.perf_counter() - t_start) * 1e9)
         yield "", res
+
+    def encode_prompt(self, lm: LoadedModel, text: str, images: list[bytes] | None = None,
+                      add_bos: bool = True) -> list[int]:
+        """Tokenize `text`; each `[img-N]` marker becomes image N's patch rows (negative ids registered
+        with the runner). Images without a marker go in front of the text, as Ollama does for LLaVA."""
+        import re
+        images = list(images or [])
+        if not images:
+            return lm.tokenizer.encode(text, add_bos=add_bos)
+        if lm.vision is None:
+            raise StoreError("this model does not support images (no projector layer)")
+        from ..models.clip import image_token_ids
+        marks = {int(x) for x in re.findall(r"\[img-(\d+)\]", text)}
+        text = "".join(f"[img-{i}]" for i in range(len(images)) if i not in marks) + text
+        img_ids = []
+        for data in images:
+            rows = lm.vision.encode(data)
+            ids = image_token_ids(data, rows.shape[0])
+            if lm.scheduler is not None:  # between batched decode steps, on the scheduler thread
+                lm.scheduler.run_exclusive(lambda r, ids=ids, rows=rows: r.set_ext(ids, rows))
+            else:
+                with lm.lock:
+                    lm.runner.set_ext(ids, rows)
+            img_ids.append(ids)
+        out: list[int] = []
+        pos = 0
+        for mt in re.finditer(r"\[img-(\d+)\]", text):
+            seg = text[pos:mt.start()]
+            if seg or not out:
+                out += lm.tokenizer.encode(seg, add_bos=add_bos and not out)
+            k = int(mt.group(1))
+            if k >= len(img_ids):
+                raise StoreError(f"prompt references [img-{k}] but only {len(img_ids)} images were given")
+            out += img_ids[k]
+            pos = mt.end()
+        if text[pos:]:
+            out += lm.tokenizer.encode(text[pos:], add_bos=False)
+        return out
 
     def embed(self, lm: LoadedModel, texts: list[str], truncate: bool = True) -> tuple[list[list[float]], int]:
         total = 0

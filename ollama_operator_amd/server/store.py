@@ -289,8 +289,10 @@ class ModelStore:
     # ------------------------------------------------------------------ create
     def create(self, name: str, gguf_path: str | None = None, from_model: str | None = None,
                template: str | None = None, system: str | None = None, params: dict | None = None,
-               license_text: str | None = None, messages: list | None = None) -> Manifest:
-        """`ollama create` from a local GGUF (FROM ./x.gguf) or an existing model (FROM name)."""
+               license_text: str | None = None, messages: list | None = None,
+               projector_path: str | None = None) -> Manifest:
+        """`ollama create` from a local GGUF (FROM ./x.gguf) or an existing model (FROM name).
+        projector_path: a CLIP projector GGUF (LLaVA mmproj; a second FROM line in a Modelfile)."""
         layers: list[dict] = []
         cfg_extra: dict = {}
         if from_model:
@@ -311,6 +313,12 @@ class ModelStore:
             layers = [l for l in layers if l.get("mediaType") != mt]
             layers.append({"mediaType": mt, **self.put_blob_bytes(text.encode())})
 
+        if projector_path:
+            layers = [l for l in layers if l.get("mediaType") != MT_PROJECTOR]
+            layers.append({"mediaType": MT_PROJECTOR, **self.put_blob_file(projector_path)})
+            fam = list(cfg_extra.get("model_families") or [cfg_extra.get("model_family", "")])
+            if "clip" not in fam:
+                cfg_extra = dict(cfg_extra, model_families=[f for f in fam if f] + ["clip"])
         replace(MT_TEMPLATE, template)
         replace(MT_SYSTEM, system)
         replace(MT_LICENSE, license_text)
@@ -395,8 +403,9 @@ def parse_modelfile(text: str) -> dict[str, Any]:
             continue
         kw, _, rest = ln.partition(" ")
         kw = kw.upper()
-        if kw == "FROM":
-            out["from"] = read_value(rest)
+        if kw == "FROM":  # a second FROM (a CLIP projector GGUF for LLaVA) is kept in "froms"
+            out.setdefault("froms", []).append(read_value(rest))
+            out.setdefault("from", out["froms"][0])
         elif kw in ("TEMPLATE", "SYSTEM", "LICENSE", "ADAPTER"):
             out[kw.lower()] = read_value(lines[i0].strip()[len(kw):])
         elif kw == "PARAMETER":
@@ -451,3 +460,16 @@ def render_modelfile(name: str, m: Manifest, store: ModelStore) -> str:
 def now_rfc3339(ts: float | None = None) -> str:
     t = time.time() if ts is None else ts
     return time.strftime("%Y-%m-%dT%H:%M:%S", time.gmtime(t)) + f".{int((t % 1) * 1e6):06d}Z"
+
+
+def gguf_arch(path: str) -> str | None:
+    """general.architecture of a GGUF file, None when it is not one."""
+    from ..gguf import read_gguf
+    try:
+        g = read_gguf(path)
+    except Exception:  # noqa: BLE001
+        return None
+    try:
+        return g.architecture
+    finally:
+        g.close()

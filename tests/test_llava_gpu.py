@@ -1,0 +1,41 @@
+"""LLaVA on the MI355X: CLIP encoder (fp16 on the GPU) against the fp64 oracle, and external embedding
+rows through the native HIP engine (embed_rows_kernel ext path) -- exact-invariant check as on CPU."""
+import numpy as np
+import pytest
+import torch
+
+from test_llava import E_LLM, _png, tiny_clip  # noqa: F401  (fixture)
+
+pytestmark = pytest.mark.gpu
+
+
+def test_clip_encoder_gpu_matches_oracle(tiny_clip):  # noqa: F811
+    from ollama_operator_amd.models.clip import ClipEncoder, preprocess, reference_encode
+    enc = ClipEncoder(tiny_clip, "cuda")
+    px = preprocess(_png(seed=4), enc.cfg)
+    got = enc.encode_pixels(px).cpu().numpy()
+    ref = reference_encode(tiny_clip, px)
+    assert np.linalg.norm(got - ref) / np.linalg.norm(ref) < 2e-2
+
+
+def test_ext_rows_native_gpu(tiny_models):
+    from ollama_operator_amd.engine.runner import Runner
+    from ollama_operator_amd.gguf import read_gguf
+    from ollama_operator_amd.quant import dequantize
+    r = Runner(tiny_models["tiny-llama"], device="cuda", max_batch=16, max_seqs=4, ctx=64, ext_rows=8)
+    V = r.cfg.n_vocab
+    prompt = [1, 17, 42, 99, 5, 230, 7, 11, 64, 3, 8, 21, 77, 300, 12, 14, 400, 2]  # >= GEMM_MIN_B rows
+    r.prefill(r.new_sequence(), prompt)
+    want = r.logits[0, :V].clone()
+    g = read_gguf(tiny_models["tiny-llama"])
+    t = g.tensors["token_embd.weight"]
+    emb = dequantize(g.raw("token_embd.weight"), t.ggml_type, t.n_elements).reshape(t.torch_shape)
+    g.close()
+    r.set_ext([-7, -8], emb[[42, 300]] * r.cfg.embed_scale)
+    p2 = list(prompt)
+    p2[2], p2[13] = -7, -8
+    r.prefill(r.new_sequence(), p2)
+    torch.cuda.synchronize()
+    assert torch.allclose(r.logits[0, :V], want, rtol=1e-4, atol=1e-4)
+    toks = list(r.generate(r.new_sequence(), p2[:6], max_tokens=4))
+    assert len(toks) == 4 and all(0 <= x < V for x in toks)
