@@ -286,8 +286,9 @@ PYBIND11_MODULE(_C, m) {
     argmax(Pp<const float>(logits), B, V, ld, Pp<int>(out), S(stream));
   });
   m.def("moe_router", [](py::object wq, int B, uintptr_t x, int ldx, uintptr_t norm_w, float eps, int k, uintptr_t ids,
-                         uintptr_t w, uintptr_t stream) {
+                         uintptr_t w, uintptr_t stream, uintptr_t dbg_ts) {
     GemvParams P{};
+    P.dbg_ts = Pp<unsigned long long>(dbg_ts);  // [B][8] phase stamps (scripts/bench_router.py) or null
     P.w = qmat(wq);
     if (P.w.N > 64 || k < 1 || k > P.w.N) throw std::runtime_error("moe_router: X <= 64 experts, 1 <= k <= X");
     P.B = B;
@@ -297,7 +298,8 @@ PYBIND11_MODULE(_C, m) {
     P.norm_w = Pp<const float>(norm_w);
     P.eps = eps;
     if (!moe_router(P, k, Pp<int>(ids), Pp<float>(w), S(stream))) throw std::runtime_error("moe_router: shape not covered");
-  });
+  }, py::arg("w"), py::arg("B"), py::arg("x"), py::arg("ldx"), py::arg("norm_w"), py::arg("eps"), py::arg("k"),
+     py::arg("ids"), py::arg("wout"), py::arg("stream"), py::arg("dbg_ts") = 0);
   m.def("moe_route", [](uintptr_t logits, int B, int X, int k, uintptr_t ids, uintptr_t w, uintptr_t stream) {
     moe_route(Pp<const float>(logits), B, X, k, Pp<int>(ids), Pp<float>(w), S(stream));
   });

@@ -45,30 +45,53 @@ constexpr int ROUTER_KMAX = 16384;  // normalised token staged in LDS (72 KiB wi
 __device__ __forceinline__ int rpad(int o) { return o + (o >> 5) * 4; }
 constexpr int ROUTER_PPT = 2;       // 32-weight pieces per thread: X * K / 32 <= 2048 (X = 8 at K <= 8192)
 // one 1024-thread block per token; thread t owns pieces t, t + 1024 of the flattened (expert, piece)
-// list, all requested before the token's statistics are waited for (a single block is latency-bound:
-// one round trip for x and one for the router rows, not one per expert)
+// list. A single block is latency-bound, so everything it reads from memory is requested up front:
+// Q8 (the loader's requantised F32 router, Mixtral): the raw piece bytes go to registers before the
+// token is read and are converted only after the statistics (one round trip for everything); other
+// types dequantise through the generic dequant_piece. Measured phases (scripts/bench_router.py)
+// before this: statistics 2.6 us, dots 2.7 us (piece loads serialised behind a per-type branch
+// loop), top-k 1.6 us (a 16-deep dependent LDS sum per expert).
+template <bool Q8>
 __global__ __launch_bounds__(ROUTER_NT) void moe_router_kernel(GemvParams P, int k, int* ids, float* wout) {
   extern __shared__ __attribute__((aligned(16))) float xs[];  // [K padded to whole super-blocks]
   __shared__ float red[ROUTER_NT / 64];
-  __shared__ float lg[64];
   const int b = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const QMat& W = P.w;
   const int K = W.K, X = W.N, SB = n_sb(K), np = SB * 8, total = X * np;
   const float* x = P.x + (long long)b * P.ldx;
-  if (tid < 64) lg[tid] = 0.f;
-  // 1. this thread's token slice and router pieces in flight together
+  // timeline probe (scripts/bench_router.py): 5 x s_memrealtime per block (entry, statistics reduced,
+  // token staged, dots reduced, done); null in production
+  auto stamp = [&](int k) {
+    if (P.dbg_ts && tid == 0) P.dbg_ts[8 * b + k] = __builtin_amdgcn_s_memrealtime();
+  };
+  stamp(0);
+  // 1. router pieces, then this thread's token slice, all in flight together
+  int olo[ROUTER_PPT], ohi[ROUTER_PPT];
+  u32x4 qa[Q8 ? ROUTER_PPT : 1][2];
+  unsigned qd[Q8 ? ROUTER_PPT : 1];
+  float lo[Q8 ? 1 : ROUTER_PPT][16], hi[Q8 ? 1 : ROUTER_PPT][16];
+#pragma unroll
+  for (int j = 0; j < ROUTER_PPT; ++j) {
+    const int i = min(tid + j * ROUTER_NT, total - 1);
+    const int e = i / np, p = i - e * np;
+    if constexpr (Q8) {
+      const int sb = p >> 3, t = p & 7;
+      const long long pi = (long long)t * SB + sb;
+      const uint8_t* q = W.s0 + (long long)e * SB * 256 + 32 * pi;
+      qa[j][0] = *(const u32x4*)q;
+      qa[j][1] = *(const u32x4*)(q + 16);
+      qd[j] = *(const uint16_t*)(W.s1 + (long long)e * SB * 16 + 16LL * sb + 2 * t);
+      olo[j] = 256 * sb + 32 * t;
+      ohi[j] = olo[j] + 16;
+    } else {
+      dequant_piece(W, e, p, lo[j], hi[j], olo[j], ohi[j]);
+    }
+  }
   f32x4 xv = {0.f, 0.f, 0.f, 0.f};
   f32x4 nv = {1.f, 1.f, 1.f, 1.f};
   if (4 * tid < K) {
     xv = *(const f32x4*)(x + 4 * tid);
     if (P.norm_w) nv = *(const f32x4*)(P.norm_w + 4 * tid);
-  }
-  float lo[ROUTER_PPT][16], hi[ROUTER_PPT][16];
-  int olo[ROUTER_PPT], ohi[ROUTER_PPT];
-#pragma unroll
-  for (int j = 0; j < ROUTER_PPT; ++j) {
-    const int i = min(tid + j * ROUTER_NT, total - 1);
-    dequant_piece(W, i / np, i % np, lo[j], hi[j], olo[j], ohi[j]);
   }
   // 2. RMS statistics (K <= 4 * ROUTER_NT in one pass; larger K: strided remainder), normalised copy
   float ss = xv.x * xv.x + xv.y * xv.y + xv.z * xv.z + xv.w * xv.w;
@@ -77,6 +100,7 @@ __global__ __launch_bounds__(ROUTER_NT) void moe_router_kernel(GemvParams P, int
     ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
   }
   ss = block_sum<ROUTER_NT>(ss, red);
+  stamp(1);
   const float rstd = P.norm == NORM_RMS ? rsqrtf(ss / K + P.eps) : 1.f;
   for (int i = tid; i < SB * 64; i += ROUTER_NT) {
     f32x4 v = {0.f, 0.f, 0.f, 0.f};
@@ -91,22 +115,36 @@ __global__ __launch_bounds__(ROUTER_NT) void moe_router_kernel(GemvParams P, int
     *(f32x4*)(xs + rpad(4 * i)) = v;
   }
   __syncthreads();
+  stamp(2);
   // 3. piece dots, summed per expert (pieces of one expert are consecutive in the flat list)
   float part[ROUTER_PPT];
 #pragma unroll
   for (int j = 0; j < ROUTER_PPT; ++j) {
     float acc = 0.f;
+    if constexpr (Q8) {
+      const unsigned qq[8] = {qa[j][0].x, qa[j][0].y, qa[j][0].z, qa[j][0].w,
+                              qa[j][1].x, qa[j][1].y, qa[j][1].z, qa[j][1].w};
 #pragma unroll
-    for (int i = 0; i < 16; i += 4) {
-      const f32x4 a = *(const f32x4*)(xs + rpad(olo[j]) + i), c = *(const f32x4*)(xs + rpad(ohi[j]) + i);
-      acc += lo[j][i] * a.x + lo[j][i + 1] * a.y + lo[j][i + 2] * a.z + lo[j][i + 3] * a.w;
-      acc += hi[j][i] * c.x + hi[j][i + 1] * c.y + hi[j][i + 2] * c.z + hi[j][i + 3] * c.w;
+      for (int c = 0; c < 8; ++c) {  // 4 weights per dword; dwords 0-3 at olo, 4-7 at ohi
+        const f32x4 a = *(const f32x4*)(xs + rpad(c < 4 ? olo[j] : ohi[j]) + 4 * (c & 3));
+        const int w = (int)qq[c];
+        acc += (float)((w << 24) >> 24) * a.x + (float)((w << 16) >> 24) * a.y + (float)((w << 8) >> 24) * a.z +
+               (float)(w >> 24) * a.w;
+      }
+      acc *= h2f((uint16_t)qd[j]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 16; i += 4) {
+        const f32x4 a = *(const f32x4*)(xs + rpad(olo[j]) + i), c = *(const f32x4*)(xs + rpad(ohi[j]) + i);
+        acc += lo[j][i] * a.x + lo[j][i + 1] * a.y + lo[j][i + 2] * a.z + lo[j][i + 3] * a.w;
+        acc += hi[j][i] * c.x + hi[j][i + 1] * c.y + hi[j][i + 2] * c.z + hi[j][i + 3] * c.w;
+      }
     }
     part[j] = tid + j * ROUTER_NT < total ? acc : 0.f;
   }
   // np is a multiple of 8: an expert's pieces span whole 8-lane groups; reduce within groups of 8,
-  // then one LDS add per group (deterministic order is not needed for a top-k over distinct logits,
-  // but the sum order is fixed anyway: groups are added by one wave in order below)
+  // one LDS slot per group; wave 0 adds an expert's SB slots in fixed order (deterministic logits:
+  // TP ranks must route identically)
   __shared__ float gsum[ROUTER_PPT * ROUTER_NT / 8];
 #pragma unroll
   for (int j = 0; j < ROUTER_PPT; ++j) {
@@ -114,19 +152,22 @@ __global__ __launch_bounds__(ROUTER_NT) void moe_router_kernel(GemvParams P, int
     if ((lane & 7) == 0) gsum[(tid + j * ROUTER_NT) / 8] = v;
   }
   __syncthreads();
+  stamp(3);
   if (wave != 0) return;
-  // 4. wave 0: logit of expert e (lane e) = sum of its np / 8 group sums, top-k, softmax
+  // 4. wave 0: logit of expert e (lane e) = sum of its SB group sums (reads issued 16 at a time), top-k
   float v = -INFINITY;
   if (lane < X) {
     float t = 0.f;
-    for (int g = lane * (np / 8); g < (lane + 1) * (np / 8); ++g) t += gsum[g];
+    const float* g = gsum + lane * SB;
+#pragma unroll 16
+    for (int m = 0; m < SB; ++m) t += g[m];
     v = t;
   }
   const float mx = wave_max(v);
   float tot = 0.f, mine = 0.f;
   int rank = -1;
   for (int j = 0; j < k; ++j) {
-    const float bv = wave_max(v);
+    const float bv = j == 0 ? mx : wave_max(v);
     const unsigned long long hit = __ballot(v == bv && lane < X);
     const int best = hit ? __ffsll((long long)hit) - 1 : 0;
     const float pr = __expf(bv - mx);
@@ -141,19 +182,25 @@ __global__ __launch_bounds__(ROUTER_NT) void moe_router_kernel(GemvParams P, int
     ids[b * k + rank] = lane;
     wout[b * k + rank] = mine / tot;
   }
+  stamp(4);
 }
 
 bool moe_router(const GemvParams& P, int k, int* ids, float* w, hipStream_t s) {
   const int np = (P.w.K + 255) / 256 * 8;
   if (P.w.N > 64 || P.w.K > ROUTER_KMAX || P.w.K % 4 || P.w.N * np > ROUTER_PPT * ROUTER_NT) return false;
-  static bool attr = false;  // 64 KiB of dynamic LDS: one attribute call, before any graph capture
+  static bool attr = false;  // dynamic LDS above 64 KiB: one attribute call, before any graph capture
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)moe_router_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)moe_router_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              ROUTER_KMAX * 9 / 8 * (int)sizeof(float));
+    (void)hipFuncSetAttribute((const void*)moe_router_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               ROUTER_KMAX * 9 / 8 * (int)sizeof(float));
     attr = true;
   }
   const size_t lds = (size_t)((P.w.K + 255) / 256) * 288 * sizeof(float);
-  hipLaunchKernelGGL(moe_router_kernel, dim3(P.B), dim3(ROUTER_NT), lds, s, P, k, ids, w);
+  if (P.w.qtype == QT_Q8_0)
+    hipLaunchKernelGGL(moe_router_kernel<true>, dim3(P.B), dim3(ROUTER_NT), lds, s, P, k, ids, w);
+  else
+    hipLaunchKernelGGL(moe_router_kernel<false>, dim3(P.B), dim3(ROUTER_NT), lds, s, P, k, ids, w);
   return true;
 }
 
