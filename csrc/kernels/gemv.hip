@@ -640,7 +640,9 @@ static int flight_ks(int need, int tiles, int bz) {
   // K <= 4096 (need 1): a split leaves half of every row group's lanes idle and doubles the VALU
   // work (measured: O 4.4 -> 5.0 us, V Q6_K 5.0 -> 7.8 us); enough tiles fill the CUs anyway
   if (need < 2 || tiles * bz > 256 * 2) return 1;
-  return need >= 3 ? 3 : 2;
+  // need 4 (K 12289..16384: Mixtral expert down, Llama-2-13B down): KS 4 x NSB 1 for Q6_K only
+  // (launch_flight_split) -- Mixtral expert down Q6_K 30.6 -> 29.5 us, Q4_K 17.2 -> 19.9 us
+  return need >= 4 ? 4 : need >= 3 ? 3 : 2;
 }
 
 // VGPRs a K-split flight instantiation needs (weight tile + activation / norm registers + ~24 of
@@ -670,7 +672,8 @@ template <int QT>
 static bool launch_flight_split(const GemvParams& P, int need, hipStream_t s) {
   const int tiles = (P.w.N + 4 * GEMV_NW - 1) / (4 * GEMV_NW);
   const int bz = P.expert_ids ? P.n_sel : 1;
-  const int ks = flight_ks(need, tiles, bz);
+  int ks = flight_ks(need, tiles, bz);
+  if (ks == 4 && QT != QT_Q6_K && g_tune.ks <= 0) ks = 2;  // Q4_K need 4: KS 2 x NSB 2
   if (ks <= 1) return false;
   const int nsb = (need + ks - 1) / ks;  // 16 * nsb >= ceil(SB / ks)
   if (ks == 2 && nsb == 1) return launch_flight_ks_fit<QT, 1, 2>(P, tiles, s);

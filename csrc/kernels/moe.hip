@@ -50,7 +50,11 @@ constexpr int ROUTER_PPT = 2;       // 32-weight pieces per thread: X * K / 32 <
 // token is read and are converted only after the statistics (one round trip for everything); other
 // types dequantise through the generic dequant_piece. Measured phases (scripts/bench_router.py)
 // before this: statistics 2.6 us, dots 2.7 us (piece loads serialised behind a per-type branch
-// loop), top-k 1.6 us (a 16-deep dependent LDS sum per expert).
+// loop), top-k 1.6 us (a 16-deep dependent LDS sum per expert); after: 1.9 / 0.8 / 0.9 us, 4.9 us
+// per launch (profiles/r3_moe/bench_router_after.log). Variants measured and dropped: v_readlane
+// selection, group_max over the first 8 lanes, lane-0 serial top-k, DPP wave totals -- none faster
+// in the engine (5.9-6.6 us); what remains in each phase is latency (cold instruction fetch of a
+// once-per-layer kernel, HBM round trip of the token), not instruction count.
 template <bool Q8>
 __global__ __launch_bounds__(ROUTER_NT) void moe_router_kernel(GemvParams P, int k, int* ids, float* wout) {
   extern __shared__ __attribute__((aligned(16))) float xs[];  // [K padded to whole super-blocks]
@@ -72,6 +76,7 @@ __global__ __launch_bounds__(ROUTER_NT) void moe_router_kernel(GemvParams P, int
   float lo[Q8 ? 1 : ROUTER_PPT][16], hi[Q8 ? 1 : ROUTER_PPT][16];
 #pragma unroll
   for (int j = 0; j < ROUTER_PPT; ++j) {
+    if (j > 0 && ROUTER_NT * j >= total) break;  // block-uniform: X * np <= 1024 needs one piece each
     const int i = min(tid + j * ROUTER_NT, total - 1);
     const int e = i / np, p = i - e * np;
     if constexpr (Q8) {
@@ -120,6 +125,8 @@ __global__ __launch_bounds__(ROUTER_NT) void moe_router_kernel(GemvParams P, int
   float part[ROUTER_PPT];
 #pragma unroll
   for (int j = 0; j < ROUTER_PPT; ++j) {
+    part[j] = 0.f;
+    if (j > 0 && ROUTER_NT * j >= total) continue;
     float acc = 0.f;
     if constexpr (Q8) {
       const unsigned qq[8] = {qa[j][0].x, qa[j][0].y, qa[j][0].z, qa[j][0].w,
@@ -148,6 +155,7 @@ __global__ __launch_bounds__(ROUTER_NT) void moe_router_kernel(GemvParams P, int
   __shared__ float gsum[ROUTER_PPT * ROUTER_NT / 8];
 #pragma unroll
   for (int j = 0; j < ROUTER_PPT; ++j) {
+    if (j > 0 && ROUTER_NT * j >= total) break;
     float v = group_sum<8>(part[j]);
     if ((lane & 7) == 0) gsum[(tid + j * ROUTER_NT) / 8] = v;
   }

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 3 pass ab: router all loads up front; KS=4 split for need=4 expert down; Mixtral breakdown
 set -o pipefail
-O=gpurun_out/r3ac
+O=gpurun_out/r3aj
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py tests/test_engine_gpu.py -k "moe or mixtral" -x -q --timeout 200 --timeout-method thread > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
