@@ -279,6 +279,9 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("set_gemm_lib_min_m", &set_gemm_lib_min_m, "prefill rows from which the hipBLASLt path runs (0 = off)");
   m.def("gemm_lib_min_m", &gemm_lib_min_m);
+  m.def("gemm_lib_prepare", [](int N, int K, int min_M, int max_M, size_t ws_bytes) {
+    blas_prepare(N, K, min_M, max_M, ws_bytes);
+  });
   m.def("dequant_f16", [](py::object w, uintptr_t out, uintptr_t stream, int perm) {
     dequant_f16(qmat(w), Pp<void>(out), S(stream), perm);
   }, py::arg("w"), py::arg("out"), py::arg("stream"), py::arg("perm") = 0);

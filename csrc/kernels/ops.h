@@ -103,6 +103,9 @@ int gemm_lib_min_m();
 // no algorithm fits (the caller falls back)
 bool blas_gemm_tn(const void* w16, const void* x16, float* d, int M, int N, int K, void* ws, size_t ws_bytes,
                   hipStream_t s);
+// plan (heuristic algorithm) every power-of-two M bucket from min_M to max_M ahead of serving: the first
+// GEMM of a bucket would otherwise pay the heuristic query inside a request's TTFT
+void blas_prepare(int N, int K, int min_M, int max_M, size_t ws_bytes);
 // batched decode GEMV on the matrix cores (gemv_mfma.hip): 2 <= B <= 16 rows, needs the layout M
 // copy (QMat::mt) built by repack_m; false = shape not covered (the caller takes the int8 GEMV)
 bool gemv_mb(const GemvParams& P, hipStream_t s);

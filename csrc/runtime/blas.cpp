@@ -9,8 +9,10 @@
 //
 // Layout: hipBLASLt is column-major. Row-major D[M][N] is column-major N x M (ld N); row-major
 // W[N][K] is column-major K x N (ld K) used transposed; row-major X[M][K] is column-major K x M.
-// So D = op_T(W) * X, a "TN" GEMM. Plans (descriptors + heuristic algorithm) are cached per shape
-// and device.
+// So D = op_T(W) * X, a "TN" GEMM. Plans (descriptors + algorithm) are cached per shape and device;
+// the heuristic runs once per power-of-two M bucket (blas_prepare at model load) and its algorithm is
+// reused for the other M of the bucket.
+#include <hipblaslt/hipblaslt-ext.hpp>
 #include <hipblaslt/hipblaslt.h>
 
 #include <cstdio>
@@ -34,7 +36,28 @@ struct Plan {
 
 std::mutex g_mu;
 std::map<int, hipblasLtHandle_t> g_handles;
+// exact-shape plans (layouts + algorithm); the algorithm comes from a heuristic query at the
+// power-of-two M bucket (>= 128) and is reused for every M in the bucket once
+// hipblaslt_ext::matmulIsAlgoSupported accepts it -- a heuristic query costs tens of ms, so one per
+// prompt length would land in the TTFT
 std::map<std::tuple<int, int, int, int, size_t>, Plan> g_plans;
+std::map<std::tuple<int, int, int, int, size_t>, Plan> g_bucket;
+
+int bucket_of(int M) {
+  int b = 128;
+  while (b < M) b <<= 1;
+  return b;
+}
+
+bool layouts(Plan& p, int M, int N, int K) {
+  if (hipblasLtMatmulDescCreate(&p.op, HIPBLAS_COMPUTE_32F, HIP_R_32F) != HIPBLAS_STATUS_SUCCESS) return false;
+  const hipblasOperation_t ta = HIPBLAS_OP_T, tb = HIPBLAS_OP_N;
+  hipblasLtMatmulDescSetAttribute(p.op, HIPBLASLT_MATMUL_DESC_TRANSA, &ta, sizeof(ta));
+  hipblasLtMatmulDescSetAttribute(p.op, HIPBLASLT_MATMUL_DESC_TRANSB, &tb, sizeof(tb));
+  return hipblasLtMatrixLayoutCreate(&p.a, HIP_R_16F, K, N, K) == HIPBLAS_STATUS_SUCCESS &&
+         hipblasLtMatrixLayoutCreate(&p.b, HIP_R_16F, K, M, K) == HIPBLAS_STATUS_SUCCESS &&
+         hipblasLtMatrixLayoutCreate(&p.d, HIP_R_32F, N, M, N) == HIPBLAS_STATUS_SUCCESS;
+}
 
 hipblasLtHandle_t handle(int dev) {
   auto it = g_handles.find(dev);
@@ -45,16 +68,9 @@ hipblasLtHandle_t handle(int dev) {
   return h;
 }
 
-Plan make_plan(hipblasLtHandle_t h, int M, int N, int K, size_t ws_bytes) {
+Plan heuristic_plan(hipblasLtHandle_t h, int M, int N, int K, size_t ws_bytes) {
   Plan p;
-  if (hipblasLtMatmulDescCreate(&p.op, HIPBLAS_COMPUTE_32F, HIP_R_32F) != HIPBLAS_STATUS_SUCCESS) return p;
-  const hipblasOperation_t ta = HIPBLAS_OP_T, tb = HIPBLAS_OP_N;
-  hipblasLtMatmulDescSetAttribute(p.op, HIPBLASLT_MATMUL_DESC_TRANSA, &ta, sizeof(ta));
-  hipblasLtMatmulDescSetAttribute(p.op, HIPBLASLT_MATMUL_DESC_TRANSB, &tb, sizeof(tb));
-  if (hipblasLtMatrixLayoutCreate(&p.a, HIP_R_16F, K, N, K) != HIPBLAS_STATUS_SUCCESS ||
-      hipblasLtMatrixLayoutCreate(&p.b, HIP_R_16F, K, M, K) != HIPBLAS_STATUS_SUCCESS ||
-      hipblasLtMatrixLayoutCreate(&p.d, HIP_R_32F, N, M, N) != HIPBLAS_STATUS_SUCCESS)
-    return p;
+  if (!layouts(p, M, N, K)) return p;
   hipblasLtMatmulPreference_t pref = nullptr;
   if (hipblasLtMatmulPreferenceCreate(&pref) != HIPBLAS_STATUS_SUCCESS) return p;
   const uint64_t wsb = ws_bytes;
@@ -75,6 +91,35 @@ Plan make_plan(hipblasLtHandle_t h, int M, int N, int K, size_t ws_bytes) {
   return p;
 }
 
+// caller holds g_mu
+Plan plan_for(hipblasLtHandle_t h, int dev, int M, int N, int K, size_t ws_bytes) {
+  const auto key = std::make_tuple(dev, M, N, K, ws_bytes);
+  auto it = g_plans.find(key);
+  if (it != g_plans.end()) return it->second;
+  const int Mb = bucket_of(M);
+  const auto bkey = std::make_tuple(dev, Mb, N, K, ws_bytes);
+  auto bt = g_bucket.find(bkey);
+  if (bt == g_bucket.end()) bt = g_bucket.emplace(bkey, heuristic_plan(h, Mb, N, K, ws_bytes)).first;
+  Plan p;
+  if (M == Mb) {
+    p = bt->second;
+  } else if (bt->second.ok && layouts(p, M, N, K)) {
+    hipblasLtMatmulAlgo_t algo = bt->second.algo;
+    size_t need = 0;
+    const float alpha = 1.f, beta = 0.f;
+    if (hipblaslt_ext::matmulIsAlgoSupported(h, p.op, &alpha, p.a, p.b, &beta, p.d, p.d, algo, need) ==
+            HIPBLAS_STATUS_SUCCESS &&
+        need <= ws_bytes) {
+      p.algo = algo;
+      p.ws = need;
+      p.ok = true;
+    }
+  }
+  if (!p.ok) p = heuristic_plan(h, M, N, K, ws_bytes);
+  g_plans.emplace(key, p);
+  return p;
+}
+
 }  // namespace
 
 bool blas_gemm_tn(const void* w16, const void* x16, float* d, int M, int N, int K, void* ws, size_t ws_bytes,
@@ -87,10 +132,7 @@ bool blas_gemm_tn(const void* w16, const void* x16, float* d, int M, int N, int 
     std::lock_guard<std::mutex> lk(g_mu);
     h = handle(dev);
     if (!h) return false;
-    const auto key = std::make_tuple(dev, M, N, K, ws_bytes);
-    auto it = g_plans.find(key);
-    if (it == g_plans.end()) it = g_plans.emplace(key, make_plan(h, M, N, K, ws_bytes)).first;
-    p = it->second;
+    p = plan_for(h, dev, M, N, K, ws_bytes);
   }
   if (!p.ok) return false;
   const float alpha = 1.f, beta = 0.f;
@@ -103,6 +145,15 @@ bool blas_gemm_tn(const void* w16, const void* x16, float* d, int M, int N, int 
     return false;
   }
   return true;
+}
+
+void blas_prepare(int N, int K, int min_M, int max_M, size_t ws_bytes) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return;
+  std::lock_guard<std::mutex> lk(g_mu);
+  hipblasLtHandle_t h = handle(dev);
+  if (!h) return;
+  for (int Mb = bucket_of(min_M); Mb <= bucket_of(max_M); Mb <<= 1) (void)plan_for(h, dev, Mb, N, K, ws_bytes);
 }
 
 }  // namespace omx

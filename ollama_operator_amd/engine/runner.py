@@ -551,12 +551,30 @@ class Runner:
         which any sequence overwrites at prefill before reading."""
         if not self.is_gpu:
             return
-        # one short prompt through the prefill path (GEMM + prep/finalize kernels resolved once)
-        sid = self.new_sequence()
-        try:
-            self.prefill(sid, [self.cfg.bos_id] * min(self.max_batch, 32))
-        finally:
-            self.free_sequence(sid)
+        if self.w16 is not None:  # hipBLASLt plans for the long-prefill path (gemm.hip gemm_lib)
+            C = native()
+            lm = C.gemm_lib_min_m()
+            if lm > 0 and self.max_batch >= lm:
+                shapes = {(v.N, v.K) for L in self.w.layers for k, v in L.items()
+                          if isinstance(v, DevQMat) and k not in ("gu_exps", "down_exps", "router")}
+                for N, K in sorted(shapes):
+                    if N * K <= self.w16.numel():
+                        C.gemm_lib_prepare(N, K, lm, self.max_batch, self.gws.numel() * 4)
+        # short prompts through the prefill path (GEMM + prep/finalize kernels resolved once); one per
+        # hipBLASLt M bucket too -- a bucket's first GEMM also loads its kernel's code object (~0.1 s),
+        # which must not land in a request's TTFT
+        lens = [min(self.max_batch, 32)]
+        if self.w16 is not None and native().gemm_lib_min_m() > 0:
+            m = native().gemm_lib_min_m()
+            while m <= min(self.max_batch, self.ctx - 1):
+                lens.append(m)
+                m *= 2
+        for n in lens:
+            sid = self.new_sequence()
+            try:
+                self.prefill(sid, [self.cfg.bos_id] * n)
+            finally:
+                self.free_sequence(sid)
         if self.use_graphs:
             buckets = sorted({self.decode_splits(n) for n in range(1, self.ctx + 1)})
             for S in buckets:  # one decode graph per split bucket reachable at this context size
