@@ -43,7 +43,7 @@ void embed_rows(const QMat& w, const int* rows, int n, float* out, int ldo, hipS
 // grid-stride over (row, piece); PERM: K order (0, 2, 1, 3) inside every 4, the order prep_x16 writes the
 // prefill activations in (gemm.hip), so the library GEMM can consume both as they are
 template <bool PERM>
-__global__ __launch_bounds__(256) void dequant_f16_kernel(QMat w, f16* out) {
+__global__ __launch_bounds__(256) void dequant_f16_kernel(QMat w, f16* out, long long row0) {
   const int P = w.K / 32;
   const long long total = (long long)w.N * P;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
@@ -52,7 +52,7 @@ __global__ __launch_bounds__(256) void dequant_f16_kernel(QMat w, f16* out) {
     const int p = (int)(i % P);
     float lo[16], hi[16];
     int olo, ohi;
-    dequant_piece(w, row, p, lo, hi, olo, ohi);
+    dequant_piece(w, row0 + row, p, lo, hi, olo, ohi);
     f16* o = out + row * w.K;
     f16x8 a, b, c, d;
 #pragma unroll
@@ -68,13 +68,13 @@ __global__ __launch_bounds__(256) void dequant_f16_kernel(QMat w, f16* out) {
   }
 }
 
-void dequant_f16(const QMat& w, void* out, hipStream_t s, int perm) {
+void dequant_f16(const QMat& w, void* out, hipStream_t s, int perm, long long row0) {
   const long long total = (long long)w.N * (w.K / 32);
   const int blocks = (int)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192);
   if (perm)
-    hipLaunchKernelGGL(dequant_f16_kernel<true>, dim3(blocks), dim3(256), 0, s, w, (f16*)out);
+    hipLaunchKernelGGL(dequant_f16_kernel<true>, dim3(blocks), dim3(256), 0, s, w, (f16*)out, row0);
   else
-    hipLaunchKernelGGL(dequant_f16_kernel<false>, dim3(blocks), dim3(256), 0, s, w, (f16*)out);
+    hipLaunchKernelGGL(dequant_f16_kernel<false>, dim3(blocks), dim3(256), 0, s, w, (f16*)out, row0);
 }
 
 // Q6_K -> QT_Q6_K8 widening at load (qmat.h): one thread per (row, super-block, piece) writes the

@@ -26,6 +26,8 @@
 //    the slabs in fixed order (deterministic, no atomics) and applies the fused epilogue.
 //  * Epilogue through LDS: the fp32 tile is staged so each output has its row-pair partner (SiLU-GLU
 //    gate/up, RoPE pairs) and stores are coalesced; the element epilogue is the GEMV's (epilogue.h).
+#include <stdexcept>
+
 #include "common.h"
 #include "epilogue.h"
 #include "ops.h"
@@ -393,8 +395,9 @@ __global__ __launch_bounds__(GM_NT, 2) void qgemm_kernel(GemvParams P, const f16
   }
 }
 
-// sums the split-K slabs in fixed order; each thread owns an output pair (n, n ^ 1)
-__global__ __launch_bounds__(256) void gemm_finalize_kernel(GemvParams P, int sk) {
+// sums the split-K slabs in fixed order; each thread owns an output pair (n, n ^ 1). scatter_rows
+// (MoE down on the library path): output row m is the token of sorted pair scatter_rows[m]
+__global__ __launch_bounds__(256) void gemm_finalize_kernel(GemvParams P, int sk, const int* scatter_rows) {
   const int N = P.w.N, M = P.B;
   const int half = (N + 1) / 2;
   const long long slab = (long long)M * N;
@@ -408,8 +411,14 @@ __global__ __launch_bounds__(256) void gemm_finalize_kernel(GemvParams P, int sk
       v0 += src[z * slab];
       if (two) v1 += src[z * slab + 1];
     }
-    epi_apply(P, m, n + P.row_offset, v0, v1, 0);
-    if (two) epi_apply(P, m, n + 1 + P.row_offset, v1, v0, 0);
+    int bb = m, zsel = 0;
+    if (scatter_rows) {
+      const int pair = scatter_rows[m];
+      bb = pair / P.n_sel;
+      zsel = pair % P.n_sel;
+    }
+    epi_apply(P, bb, n + P.row_offset, v0, v1, zsel);
+    if (two) epi_apply(P, bb, n + 1 + P.row_offset, v1, v0, zsel);
   }
 }
 
@@ -432,7 +441,7 @@ static void launch_gemm(const GemvParams& P, const f16* x16, hipStream_t s) {
   if (sk > 1) {
     const long long pairs = (long long)P.B * ((P.w.N + 1) / 2);
     const int blocks = (int)((pairs + 255) / 256 < 2048 ? (pairs + 255) / 256 : 2048);
-    hipLaunchKernelGGL(gemm_finalize_kernel, dim3(blocks), dim3(256), 0, s, P, sk);
+    hipLaunchKernelGGL(gemm_finalize_kernel, dim3(blocks), dim3(256), 0, s, P, sk, (const int*)nullptr);
   }
 }
 
@@ -453,6 +462,43 @@ void moe_gemm(const GemvParams& P, hipStream_t s) {
     case QT_Q8_0: launch_moe<QT_Q8_0>(P, x16, s); break;
     default: break;
   }
+}
+
+bool moe_gemm_lib(const GemvParams& P, const int* counts, int X, hipStream_t s) {
+  const int lm = gemm_lib_min_m();
+  const long long N = P.w.N, K = P.w.K;  // per-expert rows
+  int maxc = 0, total = 0;
+  for (int e = 0; e < X; ++e) {
+    maxc = counts[e] > maxc ? counts[e] : maxc;
+    total += counts[e];
+  }
+  if (lm <= 0 || total != P.B || !P.w16ws || !P.yws || N * K > P.w16_elems || (long long)maxc * N > P.yws_elems)
+    return false;
+  const size_t wsb = P.gws ? (size_t)P.gws_elems * 4 : 0;
+  for (int e = 0; e < X; ++e)  // every expert's plan before any launch: no partial (atomic) output
+    if (counts[e] > 0 && !blas_plan_ok(counts[e], (int)N, (int)K, wsb)) return false;
+  f16* x16 = (f16*)P.xws;
+  hipLaunchKernelGGL(prep_x16_kernel, dim3(P.B), dim3(256), 0, s, P, x16);  // all pairs (gathered when moe_gather)
+  int off = 0;
+  for (int e = 0; e < X; ++e) {
+    const int cnt = counts[e];
+    if (cnt > 0) {
+      dequant_f16(P.w, P.w16ws, s, 1, (long long)e * N);
+      if (!blas_gemm_tn(P.w16ws, x16 + (long long)off * K, P.yws, cnt, (int)N, (int)K, P.gws, wsb, s))
+        throw std::runtime_error("moe_gemm_lib: hipBLASLt matmul failed after its plan was accepted");
+      GemvParams F = P;
+      F.gws = P.yws;
+      F.B = cnt;
+      const int* scatter = nullptr;
+      if (P.moe_scatter) scatter = P.moe_rows + off;
+      else F.y = P.y + (long long)off * P.ldy;  // GLU output in sorted order
+      const long long pairs = (long long)cnt * ((N + 1) / 2);
+      const int blocks = (int)((pairs + 255) / 256 < 4096 ? (pairs + 255) / 256 : 4096);
+      hipLaunchKernelGGL(gemm_finalize_kernel, dim3(blocks), dim3(256), 0, s, F, 1, scatter);
+    }
+    off += cnt;
+  }
+  return true;
 }
 
 bool gemm_eligible(const GemvParams& P) {
@@ -486,7 +532,7 @@ static bool gemm_lib(const GemvParams& P, const f16* x16, hipStream_t s) {
   F.gws = P.yws;
   const long long pairs = M * ((N + 1) / 2);
   const int blocks = (int)((pairs + 255) / 256 < 4096 ? (pairs + 255) / 256 : 4096);
-  hipLaunchKernelGGL(gemm_finalize_kernel, dim3(blocks), dim3(256), 0, s, F, 1);
+  hipLaunchKernelGGL(gemm_finalize_kernel, dim3(blocks), dim3(256), 0, s, F, 1, (const int*)nullptr);
   return true;
 }
 

@@ -106,6 +106,7 @@ bool blas_gemm_tn(const void* w16, const void* x16, float* d, int M, int N, int 
 // plan (heuristic algorithm) every power-of-two M bucket from min_M to max_M ahead of serving: the first
 // GEMM of a bucket would otherwise pay the heuristic query inside a request's TTFT
 void blas_prepare(int N, int K, int min_M, int max_M, size_t ws_bytes);
+bool blas_plan_ok(int M, int N, int K, size_t ws_bytes);  // a plan exists (created now if needed)
 // batched decode GEMV on the matrix cores (gemv_mfma.hip): 2 <= B <= 16 rows, needs the layout M
 // copy (QMat::mt) built by repack_m; false = shape not covered (the caller takes the int8 GEMV)
 bool gemv_mb(const GemvParams& P, hipStream_t s);
@@ -140,7 +141,8 @@ void set_gemv_tuning(int blocks_per_cu, int rows, int debug, int ks = -1, int xf
 // rows[i] < 0: row -(rows[i] + 1) of ext [*][w.K] (external embeddings, e.g. image patches)
 void embed_rows(const QMat& w, const int* rows, int n, float* out, int ldo, hipStream_t s, float scale = 1.f,
                 const float* ext = nullptr);
-void dequant_f16(const QMat& w, void* out_f16, hipStream_t s, int perm = 0);  // perm: prep_x16 K order
+// rows [row0, row0 + w.N) of w (an expert's slice of a stacked MoE matrix); perm: prep_x16 K order
+void dequant_f16(const QMat& w, void* out_f16, hipStream_t s, int perm = 0, long long row0 = 0);
 
 struct AttnParams {
   const float* q;              // [NQ][ldq] fp32 (roped)
@@ -204,6 +206,11 @@ void gather_rows(const float* x, int ld, const int* idx, int rows, int n, float*
 void moe_sort(const int* eids, int n_pairs, int X, int* rows, int* tiles, int* n_tiles, int tile_m, hipStream_t s);
 // grouped dequant GEMM over expert-homogeneous row tiles (P.moe_* set; P.B = number of pairs)
 void moe_gemm(const GemvParams& P, hipStream_t s);
+// MoE prefill on hipBLASLt: one dequant + library GEMM per expert over its contiguous sorted rows
+// (host counts from moe_sort's order: ascending expert, counts[e] rows each), the grouped-GEMM
+// epilogue (GLU in sorted order / routing-weighted atomic scatter) in the finalize pass; false = shape
+// or workspace not covered (the caller runs moe_gemm)
+bool moe_gemm_lib(const GemvParams& P, const int* counts, int X, hipStream_t s);
 constexpr int MOE_TILE_M = 128;
 
 // One-shot all-reduce / all-gather over peer-mapped (hipIpc) slabs for TP decode (allreduce.hip)

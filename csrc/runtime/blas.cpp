@@ -147,6 +147,14 @@ bool blas_gemm_tn(const void* w16, const void* x16, float* d, int M, int N, int 
   return true;
 }
 
+bool blas_plan_ok(int M, int N, int K, size_t ws_bytes) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return false;
+  std::lock_guard<std::mutex> lk(g_mu);
+  hipblasLtHandle_t h = handle(dev);
+  return h && plan_for(h, dev, M, N, K, ws_bytes).ok;
+}
+
 void blas_prepare(int N, int K, int min_M, int max_M, size_t ws_bytes) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return;

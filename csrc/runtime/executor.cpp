@@ -2,6 +2,7 @@
 
 #include <cmath>
 #include <stdexcept>
+#include <vector>
 
 namespace omx {
 
@@ -230,7 +231,23 @@ void Executor::ffn_block(int i, const StepInputs& in, hipStream_t s) {
       G.ldy = F;
       grouped(G);
       G.moe_gather = 1;
-      moe_gemm(G, s);
+      // long prompts: per-expert hipBLASLt GEMMs (gemm.hip moe_gemm_lib) need the routed counts on the
+      // host -- one small D2H copy + sync per layer (prefill is never graph-captured)
+      std::vector<int> counts;
+      hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+      (void)hipStreamIsCapturing(s, &cap);
+      const int lm = gemm_lib_min_m();
+      if (lm > 0 && B >= lm && ws.w16 && ws.yws && cap == hipStreamCaptureStatusNone) {
+        std::vector<int> e_host(pairs);
+        if (hipMemcpyAsync(e_host.data(), ws.eids, sizeof(int) * pairs, hipMemcpyDeviceToHost, s) == hipSuccess &&
+            hipStreamSynchronize(s) == hipSuccess) {
+          counts.assign(X, 0);
+          for (int v : e_host)
+            if (v >= 0 && v < X) ++counts[v];
+        }
+      }
+      const bool lib = !counts.empty() && moe_gemm_lib(G, counts.data(), X, s);
+      if (!lib) moe_gemm(G, s);
       if (cfg.tp > 1) hipMemsetAsync(dst, 0, sizeof(float) * (size_t)B * E, s);
       GemvParams Dn = base_params(L.down_exps, pairs, ws.hbuf, F, ws);
       Dn.epi = EPI_ADD;  // routing-weighted, atomically accumulated per token
@@ -240,7 +257,7 @@ void Executor::ffn_block(int i, const StepInputs& in, hipStream_t s) {
       Dn.expert_w = ws.ew;
       grouped(Dn);
       Dn.moe_scatter = 1;
-      moe_gemm(Dn, s);
+      if (!(lib && moe_gemm_lib(Dn, counts.data(), X, s))) moe_gemm(Dn, s);
       return;
     }
     GemvParams G = base_params(L.gu_exps, B, ws.resid, E, ws);

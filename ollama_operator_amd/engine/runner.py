@@ -202,8 +202,8 @@ class Runner:
         # largest dense layer matrix and its fp32 output slab at max_batch rows (OMX_GEMM_LIB=0: off)
         self.w16 = self.yws = None
         if self.is_gpu and os.environ.get("OMX_GEMM_LIB", "1") != "0" and max_batch >= 16:
-            mats = [v for L in self.w.layers for k, v in L.items()
-                    if isinstance(v, DevQMat) and k not in ("gu_exps", "down_exps", "router")]
+            # expert stacks count per expert (DevQMat.N = rows of one expert): moe_gemm_lib
+            mats = [v for L in self.w.layers for k, v in L.items() if isinstance(v, DevQMat) and k != "router"]
             if mats:
                 self.w16 = torch.empty(max(m.N * m.K for m in mats), device=dev, dtype=torch.float16)
                 self.yws = torch.empty(max_batch * max(m.N for m in mats), **f32)
@@ -556,10 +556,10 @@ class Runner:
             lm = C.gemm_lib_min_m()
             if lm > 0 and self.max_batch >= lm:
                 shapes = {(v.N, v.K) for L in self.w.layers for k, v in L.items()
-                          if isinstance(v, DevQMat) and k not in ("gu_exps", "down_exps", "router")}
+                          if isinstance(v, DevQMat) and k != "router"}
                 for N, K in sorted(shapes):
-                    if N * K <= self.w16.numel():
-                        C.gemm_lib_prepare(N, K, lm, self.max_batch, self.gws.numel() * 4)
+                    if N * K <= self.w16.numel():  # from 128: MoE experts see any row count
+                        C.gemm_lib_prepare(N, K, 128, self.max_batch, self.gws.numel() * 4)
         # short prompts through the prefill path (GEMM + prep/finalize kernels resolved once); one per
         # hipBLASLt M bucket too -- a bucket's first GEMM also loads its kernel's code object (~0.1 s),
         # which must not land in a request's TTFT
@@ -569,10 +569,11 @@ class Runner:
             while m <= min(self.max_batch, self.ctx - 1):
                 lens.append(m)
                 m *= 2
-        for n in lens:
+        V = self.cfg.n_vocab
+        for n in lens:  # varied tokens: MoE routing spreads over the experts (per-expert row buckets)
             sid = self.new_sequence()
             try:
-                self.prefill(sid, [self.cfg.bos_id] * n)
+                self.prefill(sid, [self.cfg.bos_id] + [3 + (i * 7919) % max(1, V - 3) for i in range(n - 1)])
             finally:
                 self.free_sequence(sid)
         if self.use_graphs:

@@ -5,6 +5,7 @@ import torch
 
 from ollama_operator_amd.engine.runner import Runner
 from ollama_operator_amd.engine.sampling import SamplingOptions
+from ollama_operator_amd.ops import native
 
 pytestmark = pytest.mark.gpu
 
@@ -74,6 +75,36 @@ def test_prefill_gemm_path_vs_torch(tiny_models, name):
     g.prefill(sg, [5])  # then a decode-shaped step on the KV the GEMM path wrote
     c.prefill(sc, [5])
     assert rel(g.logits[0, :V].cpu(), c.logits[0, :V]) < 3e-2
+
+
+@pytest.mark.parametrize("name", ["tiny-llama", "tiny-mixtral", "tiny-gemma", "tiny-phi2"])
+def test_prefill_library_path_vs_torch(tiny_models, name):
+    """The hipBLASLt prefill path (gemm.hip gemm_lib; for Mixtral per-expert GEMMs over the sorted
+    rows with the GLU / routing-weighted scatter epilogues, moe_gemm_lib) forced from 16 rows: logits
+    must match the torch twin, and the dequantised-weight scratch must have been used."""
+    C = native()
+    old = C.gemm_lib_min_m()
+    C.set_gemm_lib_min_m(16)
+    try:
+        path = tiny_models[name]
+        g = Runner(path, device="cuda", max_batch=64, max_seqs=2, ctx=160)
+        c = Runner(path, device="cpu", max_batch=64, max_seqs=2, ctx=160)
+        assert g.w16 is not None
+        g.w16.fill_(float("nan"))
+        rng = np.random.default_rng(2)
+        toks = [1] + [int(x) for x in rng.integers(3, 500, 69)]
+        sg, sc = g.new_sequence(), c.new_sequence()
+        g.prefill(sg, toks)
+        c.prefill(sc, toks)
+        torch.cuda.synchronize()
+        assert not torch.isnan(g.w16).all()  # some matrix went through the library path
+        V = g.cfg.n_vocab
+        assert rel(g.logits[0, :V].cpu(), c.logits[0, :V]) < 3e-2
+        g.prefill(sg, [5])
+        c.prefill(sc, [5])
+        assert rel(g.logits[0, :V].cpu(), c.logits[0, :V]) < 3e-2
+    finally:
+        C.set_gemm_lib_min_m(old)
 
 
 @pytest.mark.parametrize("name", ["tiny-llama", "tiny-phi2"])
