@@ -443,6 +443,7 @@ PYBIND11_MODULE(_C, m) {
         w.attn_ws = Pp<float>(ptr("attn_ws"));
         w.attn_cnt = Pp<int>(ptr("attn_cnt"));
         w.x16 = Pp<void>(ptr("x16"));
+        w.x16_elems = d.contains("x16_elems") ? d["x16_elems"].cast<long long>() : 0;
         w.gws = Pp<float>(ptr("gws"));
         w.gws_elems = d.contains("gws_elems") ? d["gws_elems"].cast<long long>() : 0;
         w.ext = Pp<const float>(ptr("ext"));

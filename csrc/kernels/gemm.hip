@@ -475,8 +475,13 @@ bool moe_gemm_lib(const GemvParams& P, const int* counts, int X, hipStream_t s) 
   if (lm <= 0 || total != P.B || !P.w16ws || !P.yws || N * K > P.w16_elems || (long long)maxc * N > P.yws_elems)
     return false;
   const size_t wsb = P.gws ? (size_t)P.gws_elems * 4 : 0;
-  for (int e = 0; e < X; ++e)  // every expert's plan before any launch: no partial (atomic) output
-    if (counts[e] > 0 && !blas_plan_ok(counts[e], (int)N, (int)K, wsb)) return false;
+  const long long xrows = P.xws_elems ? P.xws_elems / K : P.B, yrows = P.yws_elems / N;
+  auto cap_at = [&](int off) {  // rows readable from x16 row `off` on and writable in the slab
+    const long long c = xrows - off < yrows ? xrows - off : yrows;
+    return (int)(c > 0 ? c : 0);
+  };
+  for (int e = 0, o = 0; e < X; o += counts[e], ++e)  // every plan before any launch: no partial output
+    if (counts[e] > 0 && !blas_plan_ok(counts[e], (int)N, (int)K, wsb, cap_at(o))) return false;
   f16* x16 = (f16*)P.xws;
   hipLaunchKernelGGL(prep_x16_kernel, dim3(P.B), dim3(256), 0, s, P, x16);  // all pairs (gathered when moe_gather)
   int off = 0;
@@ -484,7 +489,7 @@ bool moe_gemm_lib(const GemvParams& P, const int* counts, int X, hipStream_t s) 
     const int cnt = counts[e];
     if (cnt > 0) {
       dequant_f16(P.w, P.w16ws, s, 1, (long long)e * N);
-      if (!blas_gemm_tn(P.w16ws, x16 + (long long)off * K, P.yws, cnt, (int)N, (int)K, P.gws, wsb, s))
+      if (!blas_gemm_tn(P.w16ws, x16 + (long long)off * K, P.yws, cnt, (int)N, (int)K, P.gws, wsb, s, cap_at(off)))
         throw std::runtime_error("moe_gemm_lib: hipBLASLt matmul failed after its plan was accepted");
       GemvParams F = P;
       F.gws = P.yws;
@@ -525,9 +530,13 @@ static bool gemm_lib(const GemvParams& P, const f16* x16, hipStream_t s) {
   // M >= lm (256). Taking the wide QKV / gate_up matrices from 128 rows (where the library GEMM wins
   // per call, 66 -> 60 / 109 -> 90 us) left the 128-token TTFT unchanged (11.3 vs 12.3 ms), so no
   if (lm <= 0 || M < lm || !P.w16ws || !P.yws || N * K > P.w16_elems || M * N > P.yws_elems) return false;
+  const long long xcap = P.xws_elems ? P.xws_elems / K : M, ycap = P.yws_elems / N;
+  const int m_cap = (int)(xcap < ycap ? xcap : ycap);
+  if (!blas_plan_ok((int)M, (int)N, (int)K, P.gws ? (size_t)P.gws_elems * 4 : 0, m_cap)) return false;
   dequant_f16(P.w, P.w16ws, s, 1);
-  if (!blas_gemm_tn(P.w16ws, x16, P.yws, (int)M, (int)N, (int)K, P.gws, P.gws ? (size_t)P.gws_elems * 4 : 0, s))
-    return false;
+  if (!blas_gemm_tn(P.w16ws, x16, P.yws, (int)M, (int)N, (int)K, P.gws, P.gws ? (size_t)P.gws_elems * 4 : 0, s,
+                    m_cap))
+    throw std::runtime_error("gemm_lib: hipBLASLt matmul failed after its plan was accepted");
   GemvParams F = P;
   F.gws = P.yws;
   const long long pairs = M * ((N + 1) / 2);

@@ -42,6 +42,7 @@ struct GemvParams {
   long long y_sel_stride;      // elements between experts' y (EPI_GLU output)
   // prefill GEMM path: fp16 activation scratch, >= B * K halves (null -> always the GEMV)
   void* xws;
+  long long xws_elems;          // its capacity in halves (0: exactly B * K assumed)
   // split-K partial slabs for small-M GEMMs: fp32 [splits][B][N], capacity gws_elems (0 -> no split)
   float* gws;
   long long gws_elems;
@@ -101,12 +102,14 @@ void set_gemm_lib_min_m(int m);
 int gemm_lib_min_m();
 // D[M][N] (fp32, row-major) = X[M][K] . W[N][K]^T, X and W fp16 row-major, on hipBLASLt; false when
 // no algorithm fits (the caller falls back)
+// m_cap: rows of x16 / d the buffers hold (>= M); when the M-bucket's algorithm does not accept M
+// exactly, the GEMM runs the bucket's rows (<= m_cap) instead of paying a heuristic query
 bool blas_gemm_tn(const void* w16, const void* x16, float* d, int M, int N, int K, void* ws, size_t ws_bytes,
-                  hipStream_t s);
+                  hipStream_t s, int m_cap = 0);
 // plan (heuristic algorithm) every power-of-two M bucket from min_M to max_M ahead of serving: the first
 // GEMM of a bucket would otherwise pay the heuristic query inside a request's TTFT
 void blas_prepare(int N, int K, int min_M, int max_M, size_t ws_bytes);
-bool blas_plan_ok(int M, int N, int K, size_t ws_bytes);  // a plan exists (created now if needed)
+bool blas_plan_ok(int M, int N, int K, size_t ws_bytes, int m_cap = 0);  // a plan exists (created if needed)
 // batched decode GEMV on the matrix cores (gemv_mfma.hip): 2 <= B <= 16 rows, needs the layout M
 // copy (QMat::mt) built by repack_m; false = shape not covered (the caller takes the int8 GEMV)
 bool gemv_mb(const GemvParams& P, hipStream_t s);

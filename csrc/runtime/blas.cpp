@@ -32,6 +32,7 @@ struct Plan {
   hipblasLtMatmulAlgo_t algo{};
   size_t ws = 0;
   bool ok = false;
+  int m_run = 0;  // rows the plan's layouts describe (M, or the bucket's rows when padded)
 };
 
 std::mutex g_mu;
@@ -91,8 +92,10 @@ Plan heuristic_plan(hipblasLtHandle_t h, int M, int N, int K, size_t ws_bytes) {
   return p;
 }
 
-// caller holds g_mu
-Plan plan_for(hipblasLtHandle_t h, int dev, int M, int N, int K, size_t ws_bytes) {
+// caller holds g_mu; m_cap: rows the caller's buffers hold (0 = exactly M). Order: exact-M plan
+// cached; the bucket's algorithm accepted for M; running the bucket's rows when they fit m_cap; a
+// heuristic query at exactly M (slow: tens of ms) as the last resort
+Plan plan_for(hipblasLtHandle_t h, int dev, int M, int N, int K, size_t ws_bytes, int m_cap) {
   const auto key = std::make_tuple(dev, M, N, K, ws_bytes);
   auto it = g_plans.find(key);
   if (it != g_plans.end()) return it->second;
@@ -103,6 +106,7 @@ Plan plan_for(hipblasLtHandle_t h, int dev, int M, int N, int K, size_t ws_bytes
   Plan p;
   if (M == Mb) {
     p = bt->second;
+    p.m_run = Mb;
   } else if (bt->second.ok && layouts(p, M, N, K)) {
     hipblasLtMatmulAlgo_t algo = bt->second.algo;
     size_t need = 0;
@@ -113,9 +117,18 @@ Plan plan_for(hipblasLtHandle_t h, int dev, int M, int N, int K, size_t ws_bytes
       p.algo = algo;
       p.ws = need;
       p.ok = true;
+      p.m_run = M;
     }
   }
-  if (!p.ok) p = heuristic_plan(h, M, N, K, ws_bytes);
+  if (!p.ok && bt->second.ok && m_cap >= Mb) {  // padded rows: not cached (m_cap may differ per call)
+    Plan q = bt->second;
+    q.m_run = Mb;
+    return q;
+  }
+  if (!p.ok) {
+    p = heuristic_plan(h, M, N, K, ws_bytes);
+    p.m_run = M;
+  }
   g_plans.emplace(key, p);
   return p;
 }
@@ -123,7 +136,7 @@ Plan plan_for(hipblasLtHandle_t h, int dev, int M, int N, int K, size_t ws_bytes
 }  // namespace
 
 bool blas_gemm_tn(const void* w16, const void* x16, float* d, int M, int N, int K, void* ws, size_t ws_bytes,
-                  hipStream_t s) {
+                  hipStream_t s, int m_cap) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return false;
   Plan p;
@@ -132,7 +145,7 @@ bool blas_gemm_tn(const void* w16, const void* x16, float* d, int M, int N, int 
     std::lock_guard<std::mutex> lk(g_mu);
     h = handle(dev);
     if (!h) return false;
-    p = plan_for(h, dev, M, N, K, ws_bytes);
+    p = plan_for(h, dev, M, N, K, ws_bytes, m_cap);
   }
   if (!p.ok) return false;
   const float alpha = 1.f, beta = 0.f;
@@ -147,12 +160,12 @@ bool blas_gemm_tn(const void* w16, const void* x16, float* d, int M, int N, int 
   return true;
 }
 
-bool blas_plan_ok(int M, int N, int K, size_t ws_bytes) {
+bool blas_plan_ok(int M, int N, int K, size_t ws_bytes, int m_cap) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return false;
   std::lock_guard<std::mutex> lk(g_mu);
   hipblasLtHandle_t h = handle(dev);
-  return h && plan_for(h, dev, M, N, K, ws_bytes).ok;
+  return h && plan_for(h, dev, M, N, K, ws_bytes, m_cap).ok;
 }
 
 void blas_prepare(int N, int K, int min_M, int max_M, size_t ws_bytes) {
@@ -161,7 +174,7 @@ void blas_prepare(int N, int K, int min_M, int max_M, size_t ws_bytes) {
   std::lock_guard<std::mutex> lk(g_mu);
   hipblasLtHandle_t h = handle(dev);
   if (!h) return;
-  for (int Mb = bucket_of(min_M); Mb <= bucket_of(max_M); Mb <<= 1) (void)plan_for(h, dev, Mb, N, K, ws_bytes);
+  for (int Mb = bucket_of(min_M); Mb <= bucket_of(max_M); Mb <<= 1) (void)plan_for(h, dev, Mb, N, K, ws_bytes, 0);
 }
 
 }  // namespace omx

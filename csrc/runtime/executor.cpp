@@ -9,6 +9,7 @@ namespace omx {
 static GemvParams base_params(const QMat& w, int B, const float* x, int ldx, const Workspace& ws) {
   GemvParams P{};
   P.xws = ws.x16;
+  P.xws_elems = ws.x16_elems;
   P.gws = ws.gws;
   P.gws_elems = ws.gws_elems;
   P.w16ws = ws.w16;

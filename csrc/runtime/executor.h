@@ -57,6 +57,7 @@ struct Workspace {
   float* attn_ws = nullptr;  // split-K workspace
   int* attn_cnt = nullptr;   // [maxB][H] split arrival tickets (zero-initialised)
   void* x16 = nullptr;       // [maxB][max K] fp16 activations for the prefill MFMA GEMM
+  long long x16_elems = 0;
   float* gws = nullptr;      // split-K partial slabs for small-M prefill GEMMs
   int* moe_rows = nullptr;   // [maxB*k] MoE prefill: pairs sorted by expert
   int* moe_tiles = nullptr;  // [(maxB*k/128 + X + 1)*3] expert row tiles

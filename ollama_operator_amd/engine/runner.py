@@ -61,7 +61,8 @@ class NativeExec:
             e.set_layer(i, d)
         e.set_workspace(dict(resid=p(r.resid), qbuf=p(r.qbuf), abuf=p(r.abuf), hbuf=p(r.hbuf), ypart=p(r.ypart),
                              lbuf=p(r.lbuf), rlogits=p(r.rlogits), eids=p(r.eids), ew=p(r.ew),
-                             attn_ws=p(r.attn_ws), attn_cnt=p(r.attn_cnt), x16=p(r.x16), gws=p(r.gws),
+                             attn_ws=p(r.attn_ws), attn_cnt=p(r.attn_cnt), x16=p(r.x16), x16_elems=r.x16.numel(),
+                             gws=p(r.gws),
                              moe_rows=p(r.moe_rows) if cfg.n_expert else 0, moe_tiles=p(r.moe_tiles),
                              moe_ntiles=p(r.moe_ntiles),
                              gws_elems=r.gws.numel(), max_B=r.max_batch, ld_logits=r.logits.shape[1],
@@ -570,12 +571,26 @@ class Runner:
                 lens.append(m)
                 m *= 2
         V = self.cfg.n_vocab
+        toks = lambda n, k=0: [self.cfg.bos_id] + [3 + (i * 7919 + k) % max(1, V - 3) for i in range(n - 1)]  # noqa: E731
         for n in lens:  # varied tokens: MoE routing spreads over the experts (per-expert row buckets)
             sid = self.new_sequence()
             try:
-                self.prefill(sid, [self.cfg.bos_id] + [3 + (i * 7919) % max(1, V - 3) for i in range(n - 1)])
+                self.prefill(sid, toks(n))
             finally:
                 self.free_sequence(sid)
+        # batched admission once with a row count off the power-of-two buckets (admit_many rows,
+        # hipBLASLt's algorithm check for an exact M): the first call of that check costs ~0.3 s,
+        # which the first burst of concurrent requests would otherwise pay
+        lm = native().gemm_lib_min_m()
+        n_each = max(67, lm // 2 + 3) if self.w16 is not None and lm > 0 else 67
+        if len(self.kv.rows_free) >= 2 and self.max_batch >= 2 * n_each and self.ctx > n_each:
+            sids = [self.new_sequence(), self.new_sequence()]
+            try:
+                o = SamplingOptions()
+                self.admit_many([(sid, 0, toks(n_each, j), o, [], 0) for j, sid in enumerate(sids)])
+            finally:
+                for sid in sids:
+                    self.free_sequence(sid)
         if self.use_graphs:
             buckets = sorted({self.decode_splits(n) for n in range(1, self.ctx + 1)})
             for S in buckets:  # one decode graph per split bucket reachable at this context size
@@ -637,6 +652,48 @@ class Runner:
         self.prefill(sid, tokens)
         self._set_sampler(0, opts, history, seed, 0)
         self._sample(1)
+
+    def admit_many(self, items: list[tuple]) -> list[int]:
+        """Start several requests with ONE forward: items[i] = (sid, keep, tokens, opts, history, seed).
+        Their prompt rows go through the step as independent rows (own position / KV slot / block-table
+        row; the multi-sequence paged attention, as a batched decode step), so queued requests prefill
+        together instead of stalling the running batch once each. Returns the first sampled tokens
+        (row i = items[i]). Falls back to one `admit` per item when the rows exceed max_batch."""
+        total = sum(len(it[2]) for it in items)
+        if len(items) == 1 or total > self.max_batch or len(items) > self.max_batch:
+            out = []
+            for sid, keep, tokens, opts, history, seed in items:
+                self.admit(sid, keep, tokens, opts, history, seed)
+                out.append(int(self.s_out[0].item()))
+            return out
+        pos_l, slot_l, row_l, toks, last = [], [], [], [], []
+        for sid, keep, tokens, _o, _h, _sd in items:
+            self.kv.truncate(sid, keep)
+            s = self.kv.seqs[sid]
+            start = s.length
+            if start + len(tokens) > self.ctx:
+                raise ValueError(f"context overflow: {start + len(tokens)} > {self.ctx}")
+            self.kv.reserve(sid, start + len(tokens))
+            self._sync_block_table(sid)
+            for i in range(len(tokens)):
+                pos_l.append(start + i)
+                slot_l.append(self.kv.slot(sid, start + i))
+                row_l.append(s.row)
+            toks += list(tokens)
+            last.append(len(toks) - 1)
+        B, n = len(toks), len(items)
+        pos = np.asarray(pos_l, np.int32)
+        lidx = np.zeros(B, np.int32)
+        lidx[:n] = last
+        arr = np.stack([pos, np.asarray(slot_l, np.int32), pos + 1, np.asarray(row_l, np.int32), lidx])
+        self._upload(arr.astype(np.int32), self._device_tokens(toks))
+        with trace_range(f"admit_many rows={B} seqs={n}"):
+            self.forward(B, n, use_idx=True, prefill=False)
+        for i, (sid, _k, tokens, opts, history, seed) in enumerate(items):
+            self.kv.seqs[sid].tokens.extend(tokens)
+            self._set_sampler(i, opts, history, seed, 0)
+        self._sample(n)
+        return [int(t) for t in self.s_out[:n].tolist()]
 
     def recompose(self, rows: list[tuple], tokens: list[int]) -> None:
         """New batch composition: rows[b] = (opts, history, seed, n_sampled) and the rows' next inputs."""

@@ -221,41 +221,62 @@ class BatchScheduler:
         return self.r.new_sequence(), 0
 
     def _admit(self) -> None:
+        """Admit every queued request that fits; several at once prefill in ONE forward
+        (Runner.admit_many: their prompt rows are independent rows of one step), so a burst of
+        arrivals stalls the running rows once, not once per request."""
         r = self.r
         while True:
+            batch = []
             with self.cv:
-                if not self.pending or len(self.active) >= self.max_parallel:
-                    return
-                req = self.pending.popleft()
-            if req.cancelled.is_set() or req.max_tokens <= 0:
-                req.out.put(_DONE)
-                continue
-            try:
-                sid, keep = self._take_sequence(req.prompt)
-                keep = min(keep, len(req.prompt) - 1)
+                while self.pending and len(self.active) + len(batch) < self.max_parallel:
+                    batch.append(self.pending.popleft())
+            if not batch:
+                return
+            ready = []
+            for req in batch:
+                if req.cancelled.is_set() or req.max_tokens <= 0:
+                    req.out.put(_DONE)
+                    continue
+                try:
+                    sid, keep = self._take_sequence(req.prompt)
+                except BaseException as e:  # noqa: BLE001 -- this request fails, the batch goes on
+                    req.out.put(e)
+                    continue
                 req.sid = sid
-                t0 = time.perf_counter()
-                r.admit(sid, keep, req.prompt[keep:], req.opts, req.prompt, req.seed)
-                first = int(r.s_out[0].item())
-            except BaseException as e:  # noqa: BLE001 -- this request fails, the batch goes on
-                if req.sid is not None and req.sid in r.kv.seqs:
-                    r.free_sequence(req.sid)
-                req.out.put(e)
+                ready.append((req, min(keep, len(req.prompt) - 1)))
+            if not ready:
                 continue
-            req.n_sampled = 1
-            req.history = list(req.prompt) + [first]
-            req.pos = r.kv.seqs[sid].length
-            req.max_tokens = min(req.max_tokens, r.ctx - req.pos)
-            req.last_input = first
-            req.t_gen0 = time.perf_counter()
-            if req.times is not None:
-                req.times.prompt_tokens = len(req.prompt) - keep
-                req.times.prompt_s = req.t_gen0 - t0
-            self._deliver(req, first)
-            if req.finished():
-                self._retire(req)
-            else:
-                self.active.append(req)
+            t0 = time.perf_counter()
+            try:
+                if len(ready) == 1:
+                    req, keep = ready[0]
+                    r.admit(req.sid, keep, req.prompt[keep:], req.opts, req.prompt, req.seed)
+                    firsts = [int(r.s_out[0].item())]
+                else:
+                    firsts = r.admit_many([(req.sid, keep, req.prompt[keep:], req.opts, req.prompt, req.seed)
+                                           for req, keep in ready])
+            except BaseException as e:  # noqa: BLE001 -- these requests fail, the batch goes on
+                for req, _ in ready:
+                    if req.sid is not None and req.sid in r.kv.seqs:
+                        r.free_sequence(req.sid)
+                    req.out.put(e)
+                continue
+            t1 = time.perf_counter()
+            for (req, keep), first in zip(ready, firsts):
+                req.n_sampled = 1
+                req.history = list(req.prompt) + [first]
+                req.pos = r.kv.seqs[req.sid].length
+                req.max_tokens = min(req.max_tokens, r.ctx - req.pos)
+                req.last_input = first
+                req.t_gen0 = t1
+                if req.times is not None:
+                    req.times.prompt_tokens = len(req.prompt) - keep
+                    req.times.prompt_s = t1 - t0
+                self._deliver(req, first)
+                if req.finished():
+                    self._retire(req)
+                else:
+                    self.active.append(req)
 
     def _deliver(self, req: _Req, tok: int) -> None:
         req.delivered += 1

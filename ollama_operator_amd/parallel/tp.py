@@ -216,6 +216,11 @@ class TPRunnerProxy:
         self._mirror("admit", sid=sid, keep=keep, tokens=list(tokens), opts=opts, history=list(history), seed=seed)
         self.r.admit(sid, keep, tokens, opts, history, seed)
 
+    def admit_many(self, items: list[tuple]) -> list[int]:
+        items = [(sid, keep, list(t), o, list(h), sd) for sid, keep, t, o, h, sd in items]
+        self._mirror("admit_many", items=items)
+        return self.r.admit_many(items)
+
     def recompose(self, rows: list[tuple], tokens: list[int]) -> None:
         rows = [(o, list(h), sd, n) for o, h, sd, n in rows]
         self._mirror("recompose", rows=rows, tokens=list(tokens))
@@ -290,6 +295,8 @@ def worker_main() -> None:
                 pass
         elif op == "admit":
             runner.admit(cmd["sid"], cmd["keep"], cmd["tokens"], cmd["opts"], cmd["history"], cmd["seed"])
+        elif op == "admit_many":
+            runner.admit_many(cmd["items"])
         elif op == "recompose":
             runner.recompose(cmd["rows"], cmd["tokens"])
         elif op == "decode_batch":

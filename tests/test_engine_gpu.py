@@ -87,7 +87,8 @@ def test_prefill_library_path_vs_torch(tiny_models, name):
     C.set_gemm_lib_min_m(16)
     try:
         path = tiny_models[name]
-        g = Runner(path, device="cuda", max_batch=64, max_seqs=2, ctx=160)
+        # max_batch 128: 70 prompt rows run on the 128-row bucket's plan padded (rows 70..127 unused)
+        g = Runner(path, device="cuda", max_batch=128, max_seqs=2, ctx=160)
         c = Runner(path, device="cpu", max_batch=64, max_seqs=2, ctx=160)
         assert g.w16 is not None
         g.w16.fill_(float("nan"))
@@ -229,3 +230,26 @@ def _scheduler_concurrent(tiny_models, invariant):
         k = min(4, lens[i])
         assert solo[:k] == first[i][:k], i
         assert sum(a == b for a, b in zip(solo, first[i])) >= lens[i] // 2, i
+
+
+@pytest.mark.parametrize("name", ["tiny-llama", "tiny-mixtral"])
+def test_admit_many_gpu_matches_sequential(tiny_models, name):
+    """Queued requests prefilled together (Runner.admit_many: one forward over every prompt row,
+    multi-sequence paged attention) against each request's own prefill."""
+    g = Runner(tiny_models[name], device="cuda", max_batch=64, max_seqs=6, ctx=128)
+    V = g.cfg.n_vocab
+    rng = np.random.default_rng(6)
+    prompts = [[1] + [int(x) for x in rng.integers(3, 500, n)] for n in (9, 23, 4)]
+    o = SamplingOptions(temperature=0)
+    ref = []
+    for p in prompts:
+        sid = g.new_sequence()
+        g.admit(sid, 0, p, o, p, 0)
+        torch.cuda.synchronize()
+        ref.append(g.logits[0, :V].float().cpu().clone())
+        g.free_sequence(sid)
+    sids = [g.new_sequence() for _ in prompts]
+    g.admit_many([(sid, 0, p, o, p, 0) for sid, p in zip(sids, prompts)])
+    torch.cuda.synchronize()
+    for i, lg in enumerate(ref):
+        assert rel(g.logits[i, :V].float().cpu(), lg) < 2e-2, i

@@ -56,3 +56,29 @@ def test_seeded_sampling_reproducible(tiny_models):
     a = list(r.generate(r.new_sequence(), [1, 2, 3], o, max_tokens=8))
     b = list(r.generate(r.new_sequence(), [1, 2, 3], o, max_tokens=8))
     assert a == b
+
+
+def test_admit_many_matches_sequential_admits(tiny_models):
+    """Several requests prefilled in one forward (independent rows, multi-sequence paged attention)
+    give each the logits its own prefill gives."""
+    import numpy as np
+    from ollama_operator_amd.engine.runner import Runner
+    from ollama_operator_amd.engine.sampling import SamplingOptions
+    r = Runner(tiny_models["tiny-llama"], device="cpu", max_batch=64, max_seqs=6, ctx=128)
+    V = r.cfg.n_vocab
+    rng = np.random.default_rng(4)
+    prompts = [[1] + [int(x) for x in rng.integers(3, 500, n)] for n in (9, 23, 4)]
+    o = SamplingOptions(temperature=0)
+    ref = []
+    for p in prompts:
+        sid = r.new_sequence()
+        r.admit(sid, 0, p, o, p, 0)
+        ref.append((r.logits[0, :V].clone(), int(r.s_out[0])))
+        r.free_sequence(sid)
+    sids = [r.new_sequence() for _ in prompts]
+    firsts = r.admit_many([(sid, 0, p, o, p, 0) for sid, p in zip(sids, prompts)])
+    for i, (lg, tok) in enumerate(ref):
+        assert float((r.logits[i, :V] - lg).norm() / lg.norm()) < 1e-4
+        assert firsts[i] == tok
+    for sid, p in zip(sids, prompts):
+        assert r.kv.seqs[sid].tokens == p
