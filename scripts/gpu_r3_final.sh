@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 3 final rehearsal: full GPU suite, smoke(), default bench (server + concurrency), Llama decode profile
 set -o pipefail
-O=gpurun_out/r3_final
+O=gpurun_out/r3_final2
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -40 $O/pytest_gpu.log; exit 1; }
