@@ -343,9 +343,9 @@ def main():
     ap.add_argument("--model", default="llama2-7b")
     ap.add_argument("--ftype", default="Q4_K_M", type=str.upper)
     ap.add_argument("--dir", default=os.environ.get("OMX_BENCH_DIR", "/tmp/omx_bench"))
-    ap.add_argument("--batch-extra", type=int, default=0,
+    ap.add_argument("--batch-extra", type=int, default=4,
                     help="also measure continuous-batching throughput with this many concurrent sequences per "
-                         "GPU (Ollama OLLAMA_NUM_PARALLEL default 4; reported under extra, 0 = skip)")
+                         "GPU (Ollama OLLAMA_NUM_PARALLEL default 4; reported under extra.continuous_batching, 0 = skip)")
     ap.add_argument("--via-server", type=int, default=1,
                     help="1 (default, single-GPU runs): also measure through the REST server (/api/generate) "
                          "and report it under extra.server")
