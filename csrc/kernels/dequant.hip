@@ -40,41 +40,41 @@ void embed_rows(const QMat& w, const int* rows, int n, float* out, int ldo, hipS
   hipLaunchKernelGGL(embed_rows_kernel, dim3(n), dim3(256), 0, s, w, rows, out, ldo, scale, ext);
 }
 
-// grid-stride over (row, piece); PERM: K order (0, 2, 1, 3) inside every 4, the order prep_x16 writes the
-// prefill activations in (gemm.hip), so the library GEMM can consume both as they are
+// rows on blockIdx.y (grid-stride), pieces of a row on x (no 64-bit index division per piece); PERM:
+// K order (0, 2, 1, 3) inside every 4, the order prep_x16 writes the prefill activations in
+// (gemm.hip), so the library GEMM can consume both as they are
 template <bool PERM>
 __global__ __launch_bounds__(256) void dequant_f16_kernel(QMat w, f16* out, long long row0) {
   const int P = w.K / 32;
-  const long long total = (long long)w.N * P;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-       i += (long long)gridDim.x * blockDim.x) {
-    const long long row = i / P;
-    const int p = (int)(i % P);
-    float lo[16], hi[16];
-    int olo, ohi;
-    dequant_piece(w, row0 + row, p, lo, hi, olo, ohi);
-    f16* o = out + row * w.K;
-    f16x8 a, b, c, d;
+  for (int row = blockIdx.y; row < w.N; row += gridDim.y) {
+    for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P; p += gridDim.x * blockDim.x) {
+      float lo[16], hi[16];
+      int olo, ohi;
+      dequant_piece(w, row0 + row, p, lo, hi, olo, ohi);
+      f16* o = out + (long long)row * w.K;
+      f16x8 a, b, c, d;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int k = PERM ? (j & ~3) | ((j & 1) << 1) | ((j >> 1) & 1) : j;  // 0 2 1 3
-      a[j] = (f16)lo[k]; b[j] = (f16)lo[8 + k];
-      c[j] = (f16)hi[k]; d[j] = (f16)hi[8 + k];
+      for (int j = 0; j < 8; ++j) {
+        const int k = PERM ? (j & ~3) | ((j & 1) << 1) | ((j >> 1) & 1) : j;  // 0 2 1 3
+        a[j] = (f16)lo[k]; b[j] = (f16)lo[8 + k];
+        c[j] = (f16)hi[k]; d[j] = (f16)hi[8 + k];
+      }
+      *(f16x8*)(o + olo) = a;
+      *(f16x8*)(o + olo + 8) = b;
+      *(f16x8*)(o + ohi) = c;
+      *(f16x8*)(o + ohi + 8) = d;
     }
-    *(f16x8*)(o + olo) = a;
-    *(f16x8*)(o + olo + 8) = b;
-    *(f16x8*)(o + ohi) = c;
-    *(f16x8*)(o + ohi + 8) = d;
   }
 }
 
 void dequant_f16(const QMat& w, void* out, hipStream_t s, int perm, long long row0) {
-  const long long total = (long long)w.N * (w.K / 32);
-  const int blocks = (int)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192);
+  const int P = w.K / 32;
+  const int nt = P >= 256 ? 256 : (P + 63) / 64 * 64;  // K = 4096: 128 pieces, 128 threads per row
+  const dim3 grid((P + nt - 1) / nt > 0 ? (P + nt - 1) / nt : 1, w.N < 65535 ? (w.N > 0 ? w.N : 1) : 65535);
   if (perm)
-    hipLaunchKernelGGL(dequant_f16_kernel<true>, dim3(blocks), dim3(256), 0, s, w, (f16*)out, row0);
+    hipLaunchKernelGGL(dequant_f16_kernel<true>, grid, dim3(nt > 0 ? nt : 64), 0, s, w, (f16*)out, row0);
   else
-    hipLaunchKernelGGL(dequant_f16_kernel<false>, dim3(blocks), dim3(256), 0, s, w, (f16*)out, row0);
+    hipLaunchKernelGGL(dequant_f16_kernel<false>, grid, dim3(nt > 0 ? nt : 64), 0, s, w, (f16*)out, row0);
 }
 
 // Q6_K -> QT_Q6_K8 widening at load (qmat.h): one thread per (row, super-block, piece) writes the

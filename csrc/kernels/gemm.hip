@@ -395,31 +395,54 @@ __global__ __launch_bounds__(GM_NT, 2) void qgemm_kernel(GemvParams P, const f16
   }
 }
 
-// sums the split-K slabs in fixed order; each thread owns an output pair (n, n ^ 1). scatter_rows
-// (MoE down on the library path): output row m is the token of sorted pair scatter_rows[m]
+// sums the split-K slabs in fixed order; each thread owns output pairs (n, n ^ 1), two per step
+// (16-byte slab loads). scatter_rows (MoE down on the library path): output row m is the token of
+// sorted pair scatter_rows[m]. 32-bit index math: the 64-bit division per element made this pass a
+// third of the library GEMM's time at M = 2048 (profiles/r3_gemm PMC)
 __global__ __launch_bounds__(256) void gemm_finalize_kernel(GemvParams P, int sk, const int* scatter_rows) {
   const int N = P.w.N, M = P.B;
-  const int half = (N + 1) / 2;
+  const int half = (N + 1) / 2, quads = (half + 1) / 2;  // pair pairs per row
   const long long slab = (long long)M * N;
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < (long long)M * half;
-       i += (long long)gridDim.x * 256) {
-    const int m = (int)(i / half), n = 2 * (int)(i % half);
-    const float* src = P.gws + (long long)m * N + n;
-    float v0 = 0.f, v1 = 0.f;
-    const bool two = n + 1 < N;
-    for (int z = 0; z < sk; ++z) {
-      v0 += src[z * slab];
-      if (two) v1 += src[z * slab + 1];
-    }
+  const unsigned total = (unsigned)M * (unsigned)quads;
+  for (unsigned i = blockIdx.x * 256u + threadIdx.x; i < total; i += gridDim.x * 256u) {
+    const int m = (int)(i / (unsigned)quads), q = (int)(i - (unsigned)m * (unsigned)quads);
     int bb = m, zsel = 0;
     if (scatter_rows) {
       const int pair = scatter_rows[m];
       bb = pair / P.n_sel;
       zsel = pair % P.n_sel;
     }
-    epi_apply(P, bb, n + P.row_offset, v0, v1, zsel);
-    if (two) epi_apply(P, bb, n + 1 + P.row_offset, v1, v0, zsel);
+    const float* row = P.gws + (long long)m * N;
+    const int n0 = 4 * q;
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    if ((N & 3) == 0) {  // n0 + 3 < N, 16-byte aligned
+      for (int z = 0; z < sk; ++z) {
+        const f32x4 t = *(const f32x4*)(row + z * slab + n0);
+        v[0] += t.x;
+        v[1] += t.y;
+        v[2] += t.z;
+        v[3] += t.w;
+      }
+    } else {
+      for (int z = 0; z < sk; ++z)
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          if (n0 + c < N) v[c] += row[z * slab + n0 + c];
+    }
+#pragma unroll
+    for (int c = 0; c < 4; c += 2) {
+      const int n = n0 + c;
+      if (n >= N) break;
+      epi_apply(P, bb, n + P.row_offset, v[c], v[c + 1], zsel);
+      if (n + 1 < N) epi_apply(P, bb, n + 1 + P.row_offset, v[c + 1], v[c], zsel);
+    }
   }
+}
+
+static dim3 finalize_grid(long long M, long long N) {
+  const long long quads = ((N + 1) / 2 + 1) / 2;
+  const long long b = (M * quads + 255) / 256;
+  return dim3((unsigned)(b < 4096 ? (b > 0 ? b : 1) : 4096));
 }
 
 // split-K factor: fill ~2 blocks per CU when the (M, N) tile grid alone cannot, keeping >= 4 K
@@ -439,9 +462,7 @@ static void launch_gemm(const GemvParams& P, const f16* x16, hipStream_t s) {
   const int sk = split_k(P, nt * mt, (P.w.K + GM_BK - 1) / GM_BK);
   hipLaunchKernelGGL(qgemm_kernel<QT>, dim3(nt, mt, sk), dim3(GM_NT), GM_LDS, s, P, x16);
   if (sk > 1) {
-    const long long pairs = (long long)P.B * ((P.w.N + 1) / 2);
-    const int blocks = (int)((pairs + 255) / 256 < 2048 ? (pairs + 255) / 256 : 2048);
-    hipLaunchKernelGGL(gemm_finalize_kernel, dim3(blocks), dim3(256), 0, s, P, sk, (const int*)nullptr);
+    hipLaunchKernelGGL(gemm_finalize_kernel, finalize_grid(P.B, P.w.N), dim3(256), 0, s, P, sk, (const int*)nullptr);
   }
 }
 
@@ -497,9 +518,7 @@ bool moe_gemm_lib(const GemvParams& P, const int* counts, int X, hipStream_t s) 
       const int* scatter = nullptr;
       if (P.moe_scatter) scatter = P.moe_rows + off;
       else F.y = P.y + (long long)off * P.ldy;  // GLU output in sorted order
-      const long long pairs = (long long)cnt * ((N + 1) / 2);
-      const int blocks = (int)((pairs + 255) / 256 < 4096 ? (pairs + 255) / 256 : 4096);
-      hipLaunchKernelGGL(gemm_finalize_kernel, dim3(blocks), dim3(256), 0, s, F, 1, scatter);
+      hipLaunchKernelGGL(gemm_finalize_kernel, finalize_grid(cnt, N), dim3(256), 0, s, F, 1, scatter);
     }
     off += cnt;
   }
@@ -539,9 +558,7 @@ static bool gemm_lib(const GemvParams& P, const f16* x16, hipStream_t s) {
     throw std::runtime_error("gemm_lib: hipBLASLt matmul failed after its plan was accepted");
   GemvParams F = P;
   F.gws = P.yws;
-  const long long pairs = M * ((N + 1) / 2);
-  const int blocks = (int)((pairs + 255) / 256 < 4096 ? (pairs + 255) / 256 : 4096);
-  hipLaunchKernelGGL(gemm_finalize_kernel, dim3(blocks), dim3(256), 0, s, F, 1, (const int*)nullptr);
+  hipLaunchKernelGGL(gemm_finalize_kernel, finalize_grid(M, N), dim3(256), 0, s, F, 1, (const int*)nullptr);
   return true;
 }
 
