@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 3 final rehearsal: full GPU suite, smoke(), default bench (server + concurrency), Llama decode profile
 set -o pipefail
-O=gpurun_out/r3_final2
+O=gpurun_out/r3_final3
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -40 $O/pytest_gpu.log; exit 1; }
@@ -10,6 +10,6 @@ timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smo
 tail -2 $O/smoke.log
 timeout -k 10 900 python -u bench.py > $O/bench_default.log 2>&1 || { tail -30 $O/bench_default.log; exit 1; }
 tail -1 $O/bench_default.log
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_decode -o k -- python3 bench.py --steps 32 --warmup 8 --via-server 0 > $O/prof_decode.log 2>&1 || { tail -20 $O/prof_decode.log; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_decode -o k -- python3 bench.py --steps 32 --warmup 8 --via-server 0 --batch-extra 0 > $O/prof_decode.log 2>&1 || { tail -20 $O/prof_decode.log; exit 1; }
 f=$(ls $O/prof_decode/*/k_kernel_trace.csv $O/prof_decode/k_kernel_trace.csv 2>/dev/null | head -1)
 python scripts/ktrace_step.py "$f" > $O/step_breakdown.txt 2>&1 && head -12 $O/step_breakdown.txt
