@@ -513,9 +513,9 @@ class Runner:
     def _decode_body(self, B: int):
         self.forward(B, B, use_idx=False)
         self._sample(B)
-        if self.is_gpu:  # token feedback (+ B == 1: on-device advance to the next position)
+        if self.is_gpu:  # token feedback + on-device advance of every row to its next position
             native().decode_feedback(self.d_step.data_ptr(), self.d_step.shape[1], self.s_out.data_ptr(), B,
-                                     int(B == 1), self.d_block_table.data_ptr(), self.max_blocks, self.block_size,
+                                     1, self.d_block_table.data_ptr(), self.max_blocks, self.block_size,
                                      self._host_ring_dev if B == 1 else 0, self._ring_n, stream_handle())
         else:
             self.d_tokens[:B].copy_(self.s_out[:B])
@@ -621,10 +621,10 @@ class Runner:
                 self._sync_block_table(sid)
                 reserved = True
             arr[:, b] = (pos, self.kv.slot(sid, pos), pos + 1, s.row, b)
-        # B == 1: the previous step's feedback kernel already advanced the device inputs to exactly
-        # this (sequence, position) -- replay without any host upload
-        nxt = (sids[0], poss[0]) if B == 1 else None
-        if not (self.is_gpu and nxt is not None and not reserved and self._adv_next == nxt):
+        # the previous step's feedback kernel already advanced the device inputs to exactly these
+        # (sequence, position) rows -- replay without any host upload (continuous batching too)
+        nxt = (sids[0], poss[0]) if B == 1 else (tuple(sids), tuple(poss))
+        if not (self.is_gpu and not reserved and self._adv_next == nxt):
             self._upload(arr, None)
         self._decode_S = self.decode_splits(poss[0] + 1) if B == 1 else 0
         try:
@@ -633,8 +633,8 @@ class Runner:
                     self._graph(B).replay()
                 else:
                     self._decode_body(B)
-            if nxt is not None and self.is_gpu:
-                self._adv_next = (nxt[0], nxt[1] + 1)
+            if self.is_gpu:
+                self._adv_next = (sids[0], poss[0] + 1) if B == 1 else (tuple(sids), tuple(p + 1 for p in poss))
         finally:
             self._decode_S = 0
 
