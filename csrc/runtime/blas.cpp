@@ -18,6 +18,7 @@
 #include <cstdio>
 #include <map>
 #include <mutex>
+#include <set>
 #include <tuple>
 
 #include "kernels/ops.h"
@@ -43,6 +44,17 @@ std::map<int, hipblasLtHandle_t> g_handles;
 // prompt length would land in the TTFT
 std::map<std::tuple<int, int, int, int, size_t>, Plan> g_plans;
 std::map<std::tuple<int, int, int, int, size_t>, Plan> g_bucket;
+// exact M whose bucket algorithm matmulIsAlgoSupported rejected: asked once, never again (the padded
+// bucket plan serves them when the caller's buffers hold the bucket's rows)
+std::set<std::tuple<int, int, int, int, size_t>> g_rejected;
+
+void destroy(Plan& p) {
+  if (p.a) hipblasLtMatrixLayoutDestroy(p.a);
+  if (p.b) hipblasLtMatrixLayoutDestroy(p.b);
+  if (p.d) hipblasLtMatrixLayoutDestroy(p.d);
+  if (p.op) hipblasLtMatmulDescDestroy(p.op);
+  p = Plan{};
+}
 
 int bucket_of(int M) {
   int b = 128;
@@ -71,9 +83,15 @@ hipblasLtHandle_t handle(int dev) {
 
 Plan heuristic_plan(hipblasLtHandle_t h, int M, int N, int K, size_t ws_bytes) {
   Plan p;
-  if (!layouts(p, M, N, K)) return p;
+  if (!layouts(p, M, N, K)) {
+    destroy(p);
+    return p;
+  }
   hipblasLtMatmulPreference_t pref = nullptr;
-  if (hipblasLtMatmulPreferenceCreate(&pref) != HIPBLAS_STATUS_SUCCESS) return p;
+  if (hipblasLtMatmulPreferenceCreate(&pref) != HIPBLAS_STATUS_SUCCESS) {
+    destroy(p);
+    return p;
+  }
   const uint64_t wsb = ws_bytes;
   hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsb, sizeof(wsb));
   hipblasLtMatmulHeuristicResult_t res[8];
@@ -86,9 +104,11 @@ Plan heuristic_plan(hipblasLtHandle_t h, int M, int N, int K, size_t ws_bytes) {
     p.ws = res[i].workspaceSize;
     p.ok = true;
   }
-  if (!p.ok)
+  if (!p.ok) {
     fprintf(stderr, "[omx] hipBLASLt: no algorithm for M=%d N=%d K=%d (status %d, %d candidates, %zu B workspace); "
             "fused dequant GEMM used\n", M, N, K, (int)st, n, ws_bytes);
+    destroy(p);  // a failed plan is cached as "no plan": it owns no descriptors
+  }
   return p;
 }
 
@@ -107,7 +127,7 @@ Plan plan_for(hipblasLtHandle_t h, int dev, int M, int N, int K, size_t ws_bytes
   if (M == Mb) {
     p = bt->second;
     p.m_run = Mb;
-  } else if (bt->second.ok && layouts(p, M, N, K)) {
+  } else if (bt->second.ok && !g_rejected.count(key) && layouts(p, M, N, K)) {
     hipblasLtMatmulAlgo_t algo = bt->second.algo;
     size_t need = 0;
     const float alpha = 1.f, beta = 0.f;
@@ -118,6 +138,9 @@ Plan plan_for(hipblasLtHandle_t h, int dev, int M, int N, int K, size_t ws_bytes
       p.ws = need;
       p.ok = true;
       p.m_run = M;
+    } else {
+      destroy(p);  // the descriptors of a rejected exact-M plan are not kept
+      g_rejected.insert(key);
     }
   }
   if (!p.ok && bt->second.ok && m_cap >= Mb) {  // padded rows: not cached (m_cap may differ per call)

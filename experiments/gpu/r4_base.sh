@@ -1,0 +1,15 @@
+#!/bin/bash
+# Round-4 baseline on the round-3 code: GPU suite, smoke(), driver-shaped bench, decode profile
+set -o pipefail
+O=gpurun_out/r4_base
+mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -40 $O/pytest_gpu.log; exit 1; }
+tail -1 $O/pytest_gpu.log
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
+tail -2 $O/smoke.log
+timeout -k 10 600 python -u bench.py --steps 20 --warmup 5 > $O/bench_default.log 2>&1 || { tail -30 $O/bench_default.log; exit 1; }
+tail -1 $O/bench_default.log
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_decode -o k -- python3 bench.py --steps 32 --warmup 8 --via-server 0 --batch-extra 0 > $O/prof_decode.log 2>&1 || { tail -20 $O/prof_decode.log; exit 1; }
+f=$(ls $O/prof_decode/*/k_kernel_trace.csv $O/prof_decode/k_kernel_trace.csv 2>/dev/null | head -1)
+python scripts/ktrace_step.py "$f" > $O/step_breakdown.txt 2>&1 && head -14 $O/step_breakdown.txt

@@ -644,14 +644,40 @@ class Runner:
 
     # -- continuous-batching operations (engine/scheduler.py); TPRunnerProxy mirrors each one to the
     # -- follower ranks, so every KV / sampler decision of the leader is replayed, never re-derived
+    def _keep_prefix(self, sid: int, keep: int, history: list[int]) -> None:
+        """Truncate `sid` to its first `keep` tokens, which the caller took from `history[:keep]` (the
+        scheduler's prefix match). Under tensor parallelism only the leader's scheduler appends the
+        tokens its batched steps decode (scheduler.py `_run_stable`); a follower ran the same steps, so
+        its KV holds those positions, but its token list may stop at the prompt. The leader's decision
+        is authoritative: restore the follower's bookkeeping from `history` before truncating, so every
+        rank keeps and prefills from the same position (a shorter follower list would otherwise free
+        KV blocks and prefill at a different start than the leader)."""
+        s = self.kv.seqs[sid]
+        if s.length < keep:
+            if keep > len(history) or keep > len(s.blocks) * self.block_size:
+                raise RuntimeError(f"sequence {sid}: cannot keep {keep} tokens (have {s.length}, "
+                                   f"{len(s.blocks) * self.block_size} KV slots)")
+            s.tokens[s.length:] = list(history[s.length:keep])
+        self.kv.truncate(sid, keep)
+
     def admit(self, sid: int, keep: int, tokens: list[int], opts: SamplingOptions, history: list[int],
               seed: int) -> None:
         """Start row 0 of a new request: keep `keep` cached tokens of `sid`, prefill `tokens`, seed the
         sampler and sample the first token into s_out[0]."""
-        self.kv.truncate(sid, keep)
+        self._keep_prefix(sid, keep, history)
         self.prefill(sid, tokens)
         self._set_sampler(0, opts, history, seed, 0)
         self._sample(1)
+
+    def check_admit(self, sid: int, keep: int, tokens: list[int]) -> None:
+        """Read-only validation of one admission (ValueError): every external id registered, the
+        prompt within the context window. Lets the scheduler fail one bad request of a burst without
+        touching the others' shared forward."""
+        s = self.kv.seqs[sid]
+        start = min(keep, max(s.length, keep))
+        if start + len(tokens) > self.ctx:
+            raise ValueError(f"context overflow: {start + len(tokens)} > {self.ctx}")
+        self._device_tokens(tokens)
 
     def admit_many(self, items: list[tuple]) -> list[int]:
         """Start several requests with ONE forward: items[i] = (sid, keep, tokens, opts, history, seed).
@@ -667,8 +693,8 @@ class Runner:
                 out.append(int(self.s_out[0].item()))
             return out
         pos_l, slot_l, row_l, toks, last = [], [], [], [], []
-        for sid, keep, tokens, _o, _h, _sd in items:
-            self.kv.truncate(sid, keep)
+        for sid, keep, tokens, _o, history, _sd in items:
+            self._keep_prefix(sid, keep, history)
             s = self.kv.seqs[sid]
             start = s.length
             if start + len(tokens) > self.ctx:

@@ -247,20 +247,33 @@ class BatchScheduler:
             if not ready:
                 continue
             t0 = time.perf_counter()
-            try:
-                if len(ready) == 1:
-                    req, keep = ready[0]
-                    r.admit(req.sid, keep, req.prompt[keep:], req.opts, req.prompt, req.seed)
-                    firsts = [int(r.s_out[0].item())]
-                else:
+            # per-request checks first (unregistered image ids, context overflow): a bad request fails
+            # alone instead of failing the whole burst's shared forward
+            ok = []
+            for req, keep in ready:
+                try:
+                    r.check_admit(req.sid, keep, req.prompt[keep:])
+                    ok.append((req, keep))
+                except ValueError as e:
+                    self._fail_req(req, e)
+            done, firsts = [], []
+            if len(ok) <= 1 or sum(len(q.prompt) - k for q, k in ok) > r.max_batch or len(ok) > r.max_batch:
+                for req, keep in ok:  # one forward each: a failure stays with its request
+                    try:
+                        r.admit(req.sid, keep, req.prompt[keep:], req.opts, req.prompt, req.seed)
+                        firsts.append(int(r.s_out[0].item()))
+                        done.append((req, keep))
+                    except BaseException as e:  # noqa: BLE001
+                        self._fail_req(req, e)
+            else:
+                try:
                     firsts = r.admit_many([(req.sid, keep, req.prompt[keep:], req.opts, req.prompt, req.seed)
-                                           for req, keep in ready])
-            except BaseException as e:  # noqa: BLE001 -- these requests fail, the batch goes on
-                for req, _ in ready:
-                    if req.sid is not None and req.sid in r.kv.seqs:
-                        r.free_sequence(req.sid)
-                    req.out.put(e)
-                continue
+                                           for req, keep in ok])
+                    done = ok
+                except BaseException as e:  # noqa: BLE001 -- the shared forward failed: its requests fail
+                    for req, _ in ok:
+                        self._fail_req(req, e)
+            ready = done
             t1 = time.perf_counter()
             for (req, keep), first in zip(ready, firsts):
                 req.n_sampled = 1
@@ -277,6 +290,11 @@ class BatchScheduler:
                     self._retire(req)
                 else:
                     self.active.append(req)
+
+    def _fail_req(self, req: _Req, e: BaseException) -> None:
+        if req.sid is not None and req.sid in self.r.kv.seqs:
+            self.r.free_sequence(req.sid)
+        req.out.put(e)
 
     def _deliver(self, req: _Req, tok: int) -> None:
         req.delivered += 1

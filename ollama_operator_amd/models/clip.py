@@ -78,19 +78,43 @@ def clip_config(md: dict, tensors: dict) -> ClipConfig:
                       use_gelu=bool(md.get("clip.use_gelu", False)), projector=proj, out_dim=int(out_dim))
 
 
+# decoded-size limits: a tiny file can declare a huge (or extremely thin) canvas; nothing larger than
+# this is ever decoded or padded (PIL's decompression-bomb check counts pixels only, so a 1 x 200000
+# image passes it and its square padding would be a 200000 x 200000 canvas)
+MAX_IMAGE_SIDE = 16384
+MAX_IMAGE_PIXELS = 1 << 26
+
+
 def preprocess(image: bytes | np.ndarray, cfg: ClipConfig) -> np.ndarray:
-    """Encoded image bytes (PNG/JPEG/...) or an HxWx3 uint8 array -> float32 [3, S, S] normalised."""
+    """Encoded image bytes (PNG/JPEG/...) or an HxWx3 uint8 array -> float32 [3, S, S] normalised.
+    LLaVA-1.5 "pad" aspect: pad to a square with the mean colour, resize to image_size. Images larger
+    than a few times image_size are first downscaled (aspect kept), so the padded canvas stays small."""
     from PIL import Image
     if isinstance(image, (bytes, bytearray)):
         try:
             im = Image.open(io.BytesIO(image))
-            im.load()
         except Exception as e:  # noqa: BLE001 -- any decoder error is a bad request
             raise VisionError(f"cannot decode image: {e}") from None
+        w, h = im.size  # from the header: checked before any pixel is decoded
+        if w <= 0 or h <= 0 or max(w, h) > MAX_IMAGE_SIDE or w * h > MAX_IMAGE_PIXELS:
+            raise VisionError(f"image {w}x{h} exceeds the limits ({MAX_IMAGE_SIDE} px a side, "
+                              f"{MAX_IMAGE_PIXELS} pixels)")
+        try:
+            im.load()
+        except Exception as e:  # noqa: BLE001
+            raise VisionError(f"cannot decode image: {e}") from None
     else:
-        im = Image.fromarray(np.asarray(image, dtype=np.uint8))
+        a = np.asarray(image, dtype=np.uint8)
+        if a.ndim != 3 or max(a.shape[:2]) > MAX_IMAGE_SIDE or a.shape[0] * a.shape[1] > MAX_IMAGE_PIXELS:
+            raise VisionError(f"image array of shape {a.shape} exceeds the limits")
+        im = Image.fromarray(a)
     im = im.convert("RGB")
     w, h = im.size
+    cap = 4 * cfg.image_size  # the final resize goes to image_size: nothing above this survives anyway
+    if max(w, h) > cap:
+        f = cap / max(w, h)
+        im = im.resize((max(1, round(w * f)), max(1, round(h * f))), Image.BICUBIC)
+        w, h = im.size
     side = max(w, h)
     bg = tuple(int(round(255 * m)) for m in cfg.mean)
     sq = Image.new("RGB", (side, side), bg)
@@ -173,14 +197,53 @@ class ClipEncoder:
         return self.encode_pixels(preprocess(image, self.cfg))
 
 
-def image_token_ids(image: bytes, n: int) -> list[int]:
-    """Content-derived negative ids for an image's n patch rows: the same image gets the same ids (so a
-    KV prefix holding it is reused), different images practically never collide. |id| < 2^31."""
-    if n > MAX_PATCHES_PER_IMAGE:
-        raise VisionError(f"{n} patches per image exceeds {MAX_PATCHES_PER_IMAGE}")
-    h = int.from_bytes(hashlib.sha256(bytes(image)).digest()[:8], "little") % 500_000
-    base = 1 + h * MAX_PATCHES_PER_IMAGE
-    return [-(base + j) for j in range(n)]
+ID_BUCKETS = 500_000  # id ranges of MAX_PATCHES_PER_IMAGE: |id| < 2^31
+
+
+class ImageIds:
+    """Negative token ids for images' patch rows, keyed by the FULL content digest.
+
+    The same image gets the same ids (a KV prefix holding it is reused across requests); two different
+    images never share ids: the digest picks a starting bucket and a bucket owned by another digest is
+    probed past (linear probing), so a collision of the truncated hash can never make one image's
+    prompt reuse another image's embedding rows or KV. A bucket is never handed to a second digest
+    during the registry's lifetime (one loaded model), because idle sequences may still hold KV under
+    its ids. Only ids issued here are valid in client-supplied `context` (`issued`)."""
+
+    def __init__(self, n_buckets: int = ID_BUCKETS):
+        self.n_buckets = n_buckets
+        self._bucket: dict[bytes, tuple[int, int]] = {}  # digest -> (bucket, rows)
+        self._owner: dict[int, bytes] = {}                # bucket -> digest
+        self._mu = __import__("threading").Lock()
+
+    def ids_for(self, image: bytes, n: int) -> list[int]:
+        if n > MAX_PATCHES_PER_IMAGE:
+            raise VisionError(f"{n} patches per image exceeds {MAX_PATCHES_PER_IMAGE}")
+        dg = hashlib.sha256(bytes(image)).digest()
+        with self._mu:
+            hit = self._bucket.get(dg)
+            if hit is None:
+                if len(self._owner) >= self.n_buckets:
+                    raise VisionError("image id space of this model load is exhausted; reload the model")
+                b = int.from_bytes(dg[:8], "little") % self.n_buckets
+                while b in self._owner:
+                    b = (b + 1) % self.n_buckets
+                self._owner[b] = dg
+                hit = self._bucket[dg] = (b, n)
+        b, n0 = hit
+        if n0 != n:
+            raise VisionError(f"image encoded to {n} rows, registered with {n0}")
+        base = 1 + b * MAX_PATCHES_PER_IMAGE
+        return [-(base + j) for j in range(n)]
+
+    def issued(self, tok: int) -> bool:
+        """True for a negative id this registry handed out (a patch row of a registered image)."""
+        if tok >= 0:
+            return False
+        b, j = divmod(-tok - 1, MAX_PATCHES_PER_IMAGE)
+        with self._mu:
+            dg = self._owner.get(b)
+            return dg is not None and j < self._bucket[dg][1]
 
 
 # ---------------------------------------------------------------------------------------------------

@@ -339,7 +339,7 @@ def create_app(store: ModelStore | None = None, manager: ModelManager | None = N
             else:
                 text = render_generate(body.get("template") or lm.template, prompt,
                                        body.get("system") or lm.system, body.get("suffix"))
-            ids = list(body.get("context") or []) + await run_in_threadpool(
+            ids = manager.check_context(lm, list(body.get("context") or [])) + await run_in_threadpool(
                 manager.encode_prompt, lm, text, images, not body.get("context"))
         except (StoreError, TemplateError, VisionError) as e:
             return _err(str(e), 404 if "not found" in str(e) else 400)

@@ -61,11 +61,13 @@ class LoadedModel:
     num_ctx: int
     size: int
     load_duration_ns: int
+    ctx_limit: int = 1 << 30  # the model's trained context (the runner never exceeds it)
     expires_at: float = 0.0
     lock: threading.Lock = field(default_factory=threading.Lock)
     sid: int | None = None
     scheduler: Any = None  # engine.scheduler.BatchScheduler (OLLAMA_NUM_PARALLEL > 1, single rank)
     vision: Any = None     # models.clip.ClipEncoder when the manifest has a projector layer (LLaVA)
+    images: Any = None     # models.clip.ImageIds: digest-keyed negative ids of this load's images
 
 
 @dataclass
@@ -134,7 +136,10 @@ class ModelManager:
             m = self.store.read_manifest(name)
             lm = self.loaded.get(key)
             want_ctx = num_ctx or int(self.store.params(m).get("num_ctx", DEFAULT_NUM_CTX))
-            if lm is not None and (lm.digest != m.digest or want_ctx > lm.num_ctx):
+            # a larger window reloads only if the loaded one is below what was asked AND below the model's
+            # own limit (the runner clamps num_ctx to the trained context: comparing against the clamped
+            # value alone reloaded such a model on every request, dropping its KV prefix cache)
+            if lm is not None and (lm.digest != m.digest or (want_ctx > lm.num_ctx and lm.num_ctx < lm.ctx_limit)):
                 self._unload(key)
                 lm = None
             if lm is None:
@@ -148,6 +153,7 @@ class ModelManager:
 
     def _load(self, name: ModelName, m, num_ctx: int) -> LoadedModel:
         from ..engine.runner import Runner
+        from ..models.clip import ImageIds
         from ..gguf import read_gguf
         t0 = time.perf_counter()
         path = self.store.model_blob(name)
@@ -190,9 +196,10 @@ class ModelManager:
             runner.capture_batch_graphs(par)
             scheduler = BatchScheduler(runner, max_parallel=par)
         return LoadedModel(name=name, digest=m.digest, path=path, runner=runner, tokenizer=tok, scheduler=scheduler,
-                           vision=vision,
+                           vision=vision, images=ImageIds() if vision is not None else None,
                            template=self.store.text_layer(m, MT_TEMPLATE), system=self.store.text_layer(m, MT_SYSTEM),
-                           params=self.store.params(m), num_ctx=runner.ctx, size=os.path.getsize(path),
+                           params=self.store.params(m), num_ctx=runner.ctx, ctx_limit=runner.cfg.ctx_len,
+                           size=os.path.getsize(path),
                            load_duration_ns=int((time.perf_counter() - t0) * 1e9))
 
     def ps(self) -> list[LoadedModel]:
@@ -289,6 +296,20 @@ class ModelManager:
         res.total_duration = int((time.perf_counter() - t_start) * 1e9)
         yield "", res
 
+    @staticmethod
+    def check_context(lm: LoadedModel, ids: list) -> list[int]:
+        """Client-supplied `context` ids: vocabulary tokens, or image patch ids THIS load issued (a
+        negative id is a row of the shared external-embedding ring; only the registry's own ids may
+        name one, so a client cannot address rows of images it never sent)."""
+        out = []
+        V = lm.runner.cfg.n_vocab
+        for t in ids:
+            if not isinstance(t, int) or isinstance(t, bool) or t >= V or (
+                    t < 0 and (lm.images is None or not lm.images.issued(t))):
+                raise StoreError(f"invalid context token {t!r}")
+            out.append(t)
+        return out
+
     def encode_prompt(self, lm: LoadedModel, text: str, images: list[bytes] | None = None,
                       add_bos: bool = True) -> list[int]:
         """Tokenize `text`; each `[img-N]` marker becomes image N's patch rows (negative ids registered
@@ -299,13 +320,12 @@ class ModelManager:
             return lm.tokenizer.encode(text, add_bos=add_bos)
         if lm.vision is None:
             raise StoreError("this model does not support images (no projector layer)")
-        from ..models.clip import image_token_ids
         marks = {int(x) for x in re.findall(r"\[img-(\d+)\]", text)}
         text = "".join(f"[img-{i}]" for i in range(len(images)) if i not in marks) + text
         img_ids = []
         for data in images:
             rows = lm.vision.encode(data)
-            ids = image_token_ids(data, rows.shape[0])
+            ids = lm.images.ids_for(data, rows.shape[0])
             if lm.scheduler is not None:  # between batched decode steps, on the scheduler thread
                 lm.scheduler.run_exclusive(lambda r, ids=ids, rows=rows: r.set_ext(ids, rows))
             else:

@@ -20,7 +20,7 @@ sys.path.insert(0, ROOT)
 from bench import ensure_model  # noqa: E402
 from ollama_operator_amd.engine.runner import Runner  # noqa: E402
 from ollama_operator_amd.engine.sampling import SamplingOptions  # noqa: E402
-from ollama_operator_amd.models.clip import ClipEncoder, image_token_ids, write_random_clip_gguf  # noqa: E402
+from ollama_operator_amd.models.clip import ClipEncoder, ImageIds, write_random_clip_gguf  # noqa: E402
 
 
 def main():
@@ -58,7 +58,7 @@ def main():
         torch.cuda.synchronize()
         t = time.perf_counter()
         rows = enc.encode(prompt_img)
-        ids = image_token_ids(prompt_img, rows.shape[0])
+        ids = ImageIds().ids_for(prompt_img, rows.shape[0])
         r.set_ext(ids, rows)
         sid = r.new_sequence()
         g = r.generate(sid, [1] + ids + text, SamplingOptions(temperature=0), max_tokens=a.steps)

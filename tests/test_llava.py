@@ -11,7 +11,7 @@ import numpy as np
 import pytest
 import torch
 
-from ollama_operator_amd.models.clip import (ClipEncoder, VisionError, image_token_ids, preprocess,
+from ollama_operator_amd.models.clip import (ClipEncoder, VisionError, ImageIds, preprocess,
                                              reference_encode, write_random_clip_gguf)
 
 E_LLM = 256  # tiny-llama n_embd
@@ -65,10 +65,41 @@ def test_preprocess_pads_to_square_with_mean(tiny_clip):
 
 
 def test_image_token_ids_stable_and_negative():
-    a = image_token_ids(b"img-a", 576)
-    assert a == image_token_ids(b"img-a", 576) and len(set(a)) == 576
+    reg = ImageIds()
+    a = reg.ids_for(b"img-a", 576)
+    assert a == reg.ids_for(b"img-a", 576) and len(set(a)) == 576
     assert all(-(2 ** 31) < t < 0 for t in a)
-    assert not set(a) & set(image_token_ids(b"img-b", 576))
+    assert not set(a) & set(reg.ids_for(b"img-b", 576))
+    assert reg.issued(a[0]) and reg.issued(a[-1]) and not reg.issued(a[-1] - 1) and not reg.issued(5)
+
+
+def test_image_ids_never_shared_by_colliding_digests():
+    """A truncated-hash collision must not give two images the same ids (advisor r3): with ONE bucket
+    pair, the second image is probed into the other bucket; the space, once full, refuses."""
+    reg = ImageIds(n_buckets=2)
+    a, b = reg.ids_for(b"first", 4), reg.ids_for(b"second", 4)
+    assert not set(a) & set(b) and reg.ids_for(b"first", 4) == a
+    with pytest.raises(VisionError):
+        reg.ids_for(b"third", 4)
+
+
+def test_preprocess_rejects_huge_or_thin_canvas(tiny_clip):
+    """A tiny PNG declaring a 1 x 200000 canvas is refused from its header (no 200000^2 padding); a
+    large-but-legal image is downscaled before padding (bounded memory)."""
+    import io as _io
+    from PIL import Image
+    cfg = ClipEncoder(tiny_clip).cfg
+    buf = _io.BytesIO()
+    Image.new("RGB", (1, 20000), (0, 0, 0)).save(buf, format="PNG")
+    data = bytearray(buf.getvalue())
+    # patch the IHDR height field (bytes 20..24) to 200000: the header alone declares the canvas
+    data[20:24] = (200000).to_bytes(4, "big")
+    with pytest.raises(VisionError):
+        preprocess(bytes(data), cfg)
+    buf = _io.BytesIO()
+    Image.new("RGB", (4000, 30), (255, 0, 0)).save(buf, format="PNG")
+    a = preprocess(buf.getvalue(), cfg)
+    assert a.shape == (3, cfg.image_size, cfg.image_size) and np.isfinite(a).all()
 
 
 @pytest.mark.parametrize("backend", ["torch", "native"])
@@ -166,6 +197,14 @@ def test_generate_with_image(llava_client):
     body3 = dict(body, prompt="before [img-0] after")
     d3 = llava_client.post("/api/generate", json=body3).json()
     assert d3["done"]
+    # multi-turn: the returned context (with its image ids) is accepted back...
+    d4 = llava_client.post("/api/generate", json={"model": "tiny-llava", "prompt": " more", "context": ctx,
+                                                  "stream": False, "options": {"num_predict": 2}})
+    assert d4.status_code == 200, d4.text
+    # ...but a negative id this server never issued (another row of the shared ring) is refused
+    bad = llava_client.post("/api/generate", json={"model": "tiny-llava", "prompt": "x", "context": [1, -7],
+                                                   "stream": False, "options": {"num_predict": 2}})
+    assert bad.status_code == 400 and "context" in bad.json()["error"]
 
 
 def test_chat_and_openai_with_image(llava_client):

@@ -158,3 +158,20 @@ def test_overload_keeps_pipelining(runner):
     assert sch._must_drain(rows)  # a free row: admit now
     sch.pending.clear()
     sch.close()
+
+
+def test_bad_request_in_a_burst_fails_alone(runner):
+    """Batched admission validates each request first (advisor r3): a prompt naming an unregistered
+    image id fails by itself; the other requests of the same burst are admitted and decode."""
+    want = solo(runner, [1, 5, 9, 13], SamplingOptions(temperature=0), 6)
+    r = Runner(runner, device="cpu", max_batch=16, max_seqs=8, ctx=256, ext_rows=8)
+    sch = BatchScheduler(r, max_parallel=4)
+    # queue the burst while the scheduler is busy, so all three are admitted together
+    with sch.cv:
+        good1 = sch.submit([1, 5, 9, 13], SamplingOptions(temperature=0), 6)
+        bad = sch.submit([1, -123, 9], SamplingOptions(temperature=0), 6)
+        good2 = sch.submit([1, 5, 9, 13], SamplingOptions(temperature=0), 6)
+    assert list(good1) == want and list(good2) == want
+    with pytest.raises(ValueError):
+        list(bad)
+    sch.close()

@@ -60,6 +60,10 @@ def _run(root, tp, gpu=False):
         opts = {"temperature": 0, "num_predict": 12, "seed": 3}
         a = _post(port, "/api/generate", {"model": "tp", "prompt": "hello there", "stream": False,
                                            "options": opts})
+        # multi-turn: the prompt's cached prefix runs past the first prompt into tokens the batch
+        # scheduler decoded -- every rank must keep (and prefill from) the same position
+        d = _post(port, "/api/generate", {"model": "tp", "prompt": " and then", "context": a["context"],
+                                           "stream": False, "options": opts})
         # stop early on the first character of what it generated -> lockstep must survive
         stop = a["response"][:1] or "x"
         b = _post(port, "/api/generate", {"model": "tp", "prompt": "hello there", "stream": False,
@@ -67,7 +71,7 @@ def _run(root, tp, gpu=False):
         c = _post(port, "/api/generate", {"model": "tp", "prompt": "another prompt", "stream": False,
                                            "options": dict(opts, temperature=0.8, top_k=20)})
         e = _post(port, "/api/embed", {"model": "tp", "input": "embed me"})
-        return a, b, c, e
+        return a, b, c, e, d
     finally:
         p.terminate()
         try:
@@ -77,11 +81,14 @@ def _run(root, tp, gpu=False):
 
 
 def test_tp2_server_matches_tp1(tp_store):
-    a1, b1, c1, e1 = _run(tp_store, 1)
-    a2, b2, c2, e2 = _run(tp_store, 2)
+    a1, b1, c1, e1, d1 = _run(tp_store, 1)
+    a2, b2, c2, e2, d2 = _run(tp_store, 2)
     assert a2["context"] == a1["context"] and a2["eval_count"] == a1["eval_count"] == 12
     assert b2["context"] == b1["context"] and b2["done_reason"] == "stop"
     assert c2["context"] == c1["context"]  # seeded sampling identical across TP degrees
+    assert d2["context"] == d1["context"] and d2["prompt_eval_count"] == d1["prompt_eval_count"]
+    # the cached prefix was reused (the model stayed loaded: its trained context is below num_ctx)
+    assert d1["prompt_eval_count"] < len(a1["context"])
     import numpy as np
     v1, v2 = np.array(e1["embeddings"][0]), np.array(e2["embeddings"][0])
     assert np.linalg.norm(v1 - v2) / np.linalg.norm(v1) < 1e-3
@@ -90,11 +97,12 @@ def test_tp2_server_matches_tp1(tp_store):
 @pytest.mark.gpu
 def test_tp2_server_matches_tp1_gpu(tp_store):
     """Same on the GPU box: native executor on every rank, Megatron shards, HIP kernels."""
-    a1, b1, c1, e1 = _run(tp_store, 1, gpu=True)
-    a2, b2, c2, e2 = _run(tp_store, 2, gpu=True)
+    a1, b1, c1, e1, d1 = _run(tp_store, 1, gpu=True)
+    a2, b2, c2, e2, d2 = _run(tp_store, 2, gpu=True)
     assert a2["eval_count"] == a1["eval_count"] == 12
     # int8-dot GEMV partial sums are reduced in a different order across shards: compare the
     # greedy prefix loosely, the control flow (stop / counts) exactly
     same = sum(x == y for x, y in zip(a1["context"], a2["context"]))
     assert same >= len(a1["context"]) - 6
     assert b2["done_reason"] == "stop" and c2["eval_count"] == c1["eval_count"]
+    assert d2["prompt_eval_count"] == d1["prompt_eval_count"] and d2["eval_count"] == d1["eval_count"]
