@@ -43,10 +43,12 @@ static QMat qmat(py::object o) {
   return m;
 }
 
-static void check_attn(int H, int n_kv, int D) {
+// D: the kernels' head dim = KV cache row stride; Dv: valid dims (a padded head: Orca Mini 100 in 112)
+static void check_attn(int H, int n_kv, int D, int Dv = 0) {
   if (n_kv <= 0 || H % n_kv) throw std::runtime_error("H must be a multiple of n_kv");
   // any group size: decode blocks take a divisor of G in {1, 2, 4, 8} (attention.hip heads_per_block)
-  if (D != 64 && D != 80 && D != 96 && D != 128 && D != 256) throw std::runtime_error("unsupported head dim");
+  if (D != 64 && D != 80 && D != 96 && D != 112 && D != 128 && D != 256) throw std::runtime_error("unsupported head dim");
+  if (Dv && (Dv > D || Dv <= D - 16 || Dv % 4)) throw std::runtime_error("unsupported padded head dim");
 }
 
 static ARParams ar_params(py::dict d) {
@@ -224,6 +226,19 @@ PYBIND11_MODULE(_C, m) {
     P.ld16y = ii("ld16y");
     if ((P.x16 || P.emit16 || P.y16) && !gemv_mb_supported(P))
       throw std::runtime_error("gemv: fp16 chain operands given for a shape the matrix-core GEMV does not take");
+    // batch-1 int8 activation chain (gemv8.hip)
+    P.x8 = Pp<const void>(ip("x8"));
+    P.x8_stat = Pp<const float>(ip("x8_stat"));
+    P.emit8 = Pp<void>(ip("emit8"));
+    P.emit8_nw = Pp<const float>(ip("emit8_nw"));
+    P.emit8_stat = Pp<float>(ip("emit8_stat"));
+    if (qkv.contains("merge_S")) {
+      P.merge_S = ii("merge_S");
+      P.merge_ml = Pp<const float>(ip("merge_ml"));
+      P.merge_D = ii("merge_D");
+    }
+    if ((P.x8 || P.emit8) && !gemv8_supported(P))
+      throw std::runtime_error("gemv: int8 chain operands given for a shape gemv8 does not take");
     if (qkv.contains("expert_ids")) {
       P.expert_ids = Pp<const int>(qkv["expert_ids"].cast<uintptr_t>());
       P.expert_w = Pp<const float>(qkv.contains("expert_w") ? qkv["expert_w"].cast<uintptr_t>() : 0);
@@ -237,10 +252,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("attention", [](uintptr_t q, int ldq, uintptr_t kc, uintptr_t vc, uintptr_t block_table, int max_blocks,
                         uintptr_t q_seq, uintptr_t q_len, int NQ, int H, int n_kv, int D, int bs, float scale,
                         int window, uintptr_t out, int ldo, uintptr_t ws, int n_splits, uintptr_t counters,
-                        uintptr_t stream, int prefill) {
+                        uintptr_t stream, int prefill, int Dv) {
     if (n_splits < 1 || n_splits > 64) throw std::runtime_error("n_splits must be in [1, 64]");
     if (n_splits > 1 && (!ws || !counters)) throw std::runtime_error("split attention needs ws and counters");
-    check_attn(H, n_kv, D);
+    check_attn(H, n_kv, D, Dv);
     AttnParams A{};
     A.q = Pp<const float>(q);
     A.ldq = ldq;
@@ -263,11 +278,12 @@ PYBIND11_MODULE(_C, m) {
     A.n_splits = n_splits;
     A.counters = Pp<int>(counters);
     A.prefill = prefill;
+    A.Dv = Dv;
     attention_decode(A, S(stream));
   }, py::arg("q"), py::arg("ldq"), py::arg("kc"), py::arg("vc"), py::arg("block_table"), py::arg("max_blocks"),
      py::arg("q_seq"), py::arg("q_len"), py::arg("NQ"), py::arg("H"), py::arg("n_kv"), py::arg("D"), py::arg("bs"),
      py::arg("scale"), py::arg("window"), py::arg("out"), py::arg("ldo"), py::arg("ws"), py::arg("n_splits"),
-     py::arg("counters"), py::arg("stream"), py::arg("prefill") = 0);
+     py::arg("counters"), py::arg("stream"), py::arg("prefill") = 0, py::arg("Dv") = 0);
   m.def("attention_ws_floats", &attention_ws_floats);
   m.def("set_attn_tuning", &set_attn_tuning, py::arg("kps"), py::arg("hpb") = -1);
   m.def("gemv_merge_supported", &gemv_merge_supported);
@@ -317,6 +333,34 @@ PYBIND11_MODULE(_C, m) {
                     bs, Pp<int>(host_ring), ring, S(stream));
   });
   m.def("mfma_layout_bytes", &mfma_layout_bytes);
+  m.def("x8_bytes", [](int K) { return x8_bytes(K); });
+  m.def("gemv8_ffn", [](py::object wg, py::object wd, uintptr_t img_in, uintptr_t stat, uintptr_t img_f, uintptr_t h,
+                        uintptr_t resid, uintptr_t nw, uintptr_t img_out, uintptr_t stat_out, uintptr_t sync, int epi,
+                        float eps, uintptr_t stream) {
+    GemvParams G{}, D{};
+    G.w = qmat(wg);
+    G.B = 1;
+    G.n_sel = 1;
+    G.eps = eps;
+    G.epi = epi;
+    G.y = Pp<float>(h);
+    G.ldy = G.w.N / 2;
+    G.x8 = Pp<const void>(img_in);
+    G.x8_stat = Pp<const float>(stat);
+    G.emit8 = Pp<void>(img_f);
+    D.w = qmat(wd);
+    D.B = 1;
+    D.n_sel = 1;
+    D.epi = EPI_ADD;
+    D.y = Pp<float>(resid);
+    D.ldy = D.w.N;
+    D.x8 = Pp<const void>(img_f);
+    D.emit8 = Pp<void>(img_out);
+    D.emit8_nw = Pp<const float>(nw);
+    D.emit8_stat = Pp<float>(stat_out);
+    return gemv8_ffn(G, D, Pp<void>(sync), S(stream));
+  });
+  m.def("x8_slots", [](int K) { return x8_slots(K); });
   m.def("repack_m", [](py::object w, uintptr_t out, uintptr_t stream) {
     QMat q = qmat(w);
     if (!out || !mfma_layout_bytes(q.qtype, q.N, q.K)) throw std::runtime_error("repack_m: no layout M for this matrix");
@@ -392,7 +436,8 @@ PYBIND11_MODULE(_C, m) {
         k.tp = c["tp"].cast<int>();
         k.embed_scale = c.contains("embed_scale") ? c["embed_scale"].cast<float>() : 1.f;
         k.glu_act = c.contains("glu_act") ? c["glu_act"].cast<int>() : 0;
-        check_attn(k.H, k.Hkv, k.D);
+        k.Dc = c.contains("Dc") ? c["Dc"].cast<int>() : k.D;
+        check_attn(k.H, k.Hkv, k.Dc, k.D);
         e.layers.assign(k.n_layer, LayerW{});
       })
       .def("set_globals", [](Executor& e, py::object tok_embd, uintptr_t out_norm, uintptr_t out_norm_b,
@@ -465,7 +510,15 @@ PYBIND11_MODULE(_C, m) {
         w.ld_q = d.contains("ld_q") ? d["ld_q"].cast<int>() : 0;
         w.max_B = d["max_B"].cast<int>();
         w.n_splits = d["n_splits"].cast<int>();
+        w.x8e = Pp<void>(ptr("x8e"));
+        w.x8f = Pp<void>(ptr("x8f"));
+        w.x8st = Pp<float>(ptr("x8st"));
+        w.x8sync = Pp<void>(ptr("x8sync"));
+        w.x8_fuse = d.contains("x8_fuse") ? d["x8_fuse"].cast<int>() : 1;
+        w.x8_ok = (d.contains("x8_ok") ? d["x8_ok"].cast<int>() : 0) && e.x8_capable() ? 1 : 0;
       })
+      .def_property_readonly("x8_on", [](const Executor& e) { return e.ws.x8_ok; })
+      .def("set_segments", [](Executor& e, std::vector<std::pair<int, int>> segs) { e.segments = std::move(segs); })
       .def("set_splits", [](Executor& e, int n, int defer) {
         e.ws.n_splits = n;
         e.ws.defer = defer;

@@ -20,6 +20,9 @@
 //    scope ticket, sc1 write-through partials: MI355X_MICROARCH.md hand-off form, no fences) merges
 //    in the same launch. The grid is fixed, so the launch is hipGraph-capturable for any length.
 // Causal prefill uses the same kernel: each prompt token is a query with length pos + 1.
+#include <stdexcept>
+#include <string>
+
 #include "common.h"
 #include "ops.h"
 
@@ -113,12 +116,16 @@ __global__ __launch_bounds__(ATT_NT) void attn_decode_kernel(AttnParams P) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, tg = lane >> 4, li = lane & 15;
   const int grp = wave * 4 + tg;
 
+  const int Dv = P.Dv > 0 ? P.Dv : D;  // valid dims: q / output head stride; dims >= Dv are padding
   float q[G][DPL];
 #pragma unroll
   for (int g = 0; g < G; ++g) {
-    const float* qp = P.q + (long long)qi * P.ldq + (h0 + g) * D + li * DPL;
+    const float* qp = P.q + (long long)qi * P.ldq + (h0 + g) * Dv;
 #pragma unroll
-    for (int j = 0; j < DPL; ++j) q[g][j] = qp[j] * P.scale;
+    for (int j = 0; j < DPL; ++j) {
+      const int d = li * DPL + j;
+      q[g][j] = d < Dv ? qp[min(d, Dv - 1)] * P.scale : 0.f;  // padded K dims never contribute
+    }
   }
   float m[G], l[G], acc[G][DPL];
 #pragma unroll
@@ -250,14 +257,15 @@ __global__ __launch_bounds__(ATT_NT) void attn_decode_kernel(AttnParams P) {
       }
     }
     const int h = h0 + g;
+    if (d >= Dv) continue;  // padding dims of a padded head (never written)
     if (P.defer) {  // partial slabs [NQ][S][H*D] + [NQ][S][H]{m, l}; the kernel boundary publishes them
       const long long row = (long long)qi * S + split;
       P.ws[row * P.H * D + h * D + d] = A;
       if (d == 0) *(f32x2*)(P.ws + (long long)P.NQ * S * P.H * D + (row * P.H + h) * 2) = (f32x2){M, L};
     } else if (S == 1) {
       const float o = L > 0.f ? A / L : 0.f;
-      P.out[(long long)qi * P.ldo + h * D + d] = o;
-      if (P.out16) ((f16*)P.out16)[(long long)qi * P.ldo + h * D + d] = (f16)o;
+      P.out[(long long)qi * P.ldo + h * Dv + d] = o;
+      if (P.out16) ((f16*)P.out16)[(long long)qi * P.ldo + h * Dv + d] = (f16)o;
     } else {  // write-through (sc1) stores: the hand-off below then needs no release fence
       float* ws = P.ws + (((long long)qi * P.H + h) * gridDim.z + split) * (D + 2);
       __hip_atomic_store(ws + d, A, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -305,14 +313,15 @@ __global__ __launch_bounds__(ATT_NT) void attn_decode_kernel(AttnParams P) {
   __syncthreads();
   for (int i = threadIdx.x; i < G * D; i += ATT_NT) {
     const int g = i / D, d = i % D;
+    if (d >= Dv) continue;
     const float* ws = P.ws + ((long long)qi * P.H + h0 + g) * gridDim.z * (D + 2);
     float A = 0.f;
 #pragma unroll 8
     for (int s = 0; s < S; ++s) A += sw[g][s] * ld1(ws + s * (D + 2) + d);
     const float L = sL[g];
     const float o = L > 0.f ? A / L : 0.f;
-    P.out[(long long)qi * P.ldo + (h0 + g) * D + d] = o;
-    if (P.out16) ((f16*)P.out16)[(long long)qi * P.ldo + (h0 + g) * D + d] = (f16)o;
+    P.out[(long long)qi * P.ldo + (h0 + g) * Dv + d] = o;
+    if (P.out16) ((f16*)P.out16)[(long long)qi * P.ldo + (h0 + g) * Dv + d] = (f16)o;
   }
 }
 
@@ -332,8 +341,11 @@ typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16a __attribute__((ext_vector_type(16)));
 constexpr int PF_BQ = 128, PF_BK = 32;
 
-__device__ __forceinline__ int vswz(int row, int ch) {  // T10 (b): byte offset of 16-B chunk ch
-  return 256 * row + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
+// T10 (b): byte offset of 16-B chunk ch of V row `row`; rows of VROW bytes (256, or 512 for D = 256:
+// each 256-B half swizzled on its own)
+template <int VROW>
+__device__ __forceinline__ int vswz(int row, int ch) {
+  return VROW * row + 256 * (ch >> 4) + 16 * ((ch & 15) ^ (((row & 3) << 2) | ((row >> 2) & 3)));
 }
 
 template <int D>
@@ -342,8 +354,9 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(AttnParams P) {
   constexpr int NDT = (D + 31) / 32;      // 32-row d tiles of O^T
   constexpr int LDK = D + 8;              // K tile row stride (f16): 16-B rows offset by 4 banks
   constexpr int KCH = D / 8;              // 16-B chunks per K/V row
+  constexpr int VROW = D > 128 ? 2 * D : 256;
   __shared__ __attribute__((aligned(16))) f16 Ks[PF_BK * LDK];
-  __shared__ __attribute__((aligned(16))) char Vs[PF_BK * 256];  // [key][256 B] swizzled, zero-padded
+  __shared__ __attribute__((aligned(16))) char Vs[PF_BK * VROW];  // [key][VROW B] swizzled, zero-padded
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h2 = lane >> 5, qc = lane & 31;
   const int head = blockIdx.y, G = P.H / P.n_kv, kvh = head / G;
   const int q0 = blockIdx.x * PF_BQ;
@@ -364,11 +377,15 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(AttnParams P) {
 
   // Q^T fragments (B operand of S^T): lane = query, 8 consecutive d per k-step, scaled
   f16x8 qf[NKS];
+  const int Dv = P.Dv > 0 ? P.Dv : D;  // valid dims (multiple of 4): q / output head stride
   {
-    const float* qp = P.q + (long long)qi * P.ldq + head * D;
+    const float* qp = P.q + (long long)qi * P.ldq + head * Dv;
+    const f32x4 z4 = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int kk = 0; kk < NKS; ++kk) {
-      const f32x4 a = *(const f32x4*)(qp + 16 * kk + 8 * h2), b = *(const f32x4*)(qp + 16 * kk + 8 * h2 + 4);
+      const int d0 = 16 * kk + 8 * h2;  // padded dims load nothing (next head's q / past the row)
+      const f32x4 a = d0 + 4 <= Dv ? *(const f32x4*)(qp + min(d0, Dv - 4)) : z4;
+      const f32x4 b = d0 + 8 <= Dv ? *(const f32x4*)(qp + min(d0 + 4, Dv - 4)) : z4;
       qf[kk] = (f16x8){(f16)(a.x * P.scale), (f16)(a.y * P.scale), (f16)(a.z * P.scale), (f16)(a.w * P.scale),
                        (f16)(b.x * P.scale), (f16)(b.y * P.scale), (f16)(b.z * P.scale), (f16)(b.w * P.scale)};
     }
@@ -384,7 +401,7 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(AttnParams P) {
   if (D < 128) {
     for (int i = tid; i < PF_BK * 16; i += 256) {
       const int row = i >> 4, ch = i & 15;
-      if (ch >= KCH) *(u32x4*)(Vs + vswz(row, ch)) = (u32x4){0u, 0u, 0u, 0u};
+      if (ch >= KCH) *(u32x4*)(Vs + vswz<VROW>(row, ch)) = (u32x4){0u, 0u, 0u, 0u};
     }
   }
   // staging: each thread moves chunks of the K and V tiles (global paged cache -> registers -> LDS)
@@ -410,7 +427,7 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(AttnParams P) {
       if (i < PF_BK * KCH) {
         const int row = i / KCH, ch = i % KCH;
         *(u32x4*)(Ks + row * LDK + 8 * ch) = kr[c];
-        *(u32x4*)(Vs + vswz(row, ch)) = vr[c];
+        *(u32x4*)(Vs + vswz<VROW>(row, ch)) = vr[c];
       }
     }
     __syncthreads();
@@ -460,8 +477,8 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(AttnParams P) {
       for (int i = 0; i < NDT; ++i) {
         const int c0 = (32 * i + 16 * (g & 1)) / 8;  // first 16-B chunk of this group's 16 d columns
         const int r0 = 16 * s2 + 4 * h2;             // element j < 4: keys r0 + 0..3; j >= 4: + 8
-        const int a0 = vswz(r0 + qq, c0 + (pp >> 1)) + 8 * (pp & 1);
-        const int a1 = vswz(r0 + 8 + qq, c0 + (pp >> 1)) + 8 * (pp & 1);
+        const int a0 = vswz<VROW>(r0 + qq, c0 + (pp >> 1)) + 8 * (pp & 1);
+        const int a1 = vswz<VROW>(r0 + 8 + qq, c0 + (pp >> 1)) + 8 * (pp & 1);
         typedef __attribute__((address_space(3))) s16x4 lds_s4;
         // whole-vector bit casts: element-wise extraction from the v4i16 result miscompiled
         // (duplicated pairs), caught by scripts/dbg_prefill_attn.py + scripts/probes/tr16_probe.hip
@@ -476,13 +493,13 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(AttnParams P) {
   const int qo = q0 + wave * 32 + qc;
   if (qo < NQ) {
     const float inv = l > 0.f ? 1.f / l : 0.f;
-    float* out = P.out + (long long)qo * P.ldo + head * D;
+    float* out = P.out + (long long)qo * P.ldo + head * Dv;
 #pragma unroll
     for (int i = 0; i < NDT; ++i)
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const int d = 32 * i + 8 * k + 4 * h2;
-        if (d < D)
+        if (d < Dv)
           *(f32x4*)(out + d) = (f32x4){o[i][4 * k] * inv, o[i][4 * k + 1] * inv, o[i][4 * k + 2] * inv,
                                        o[i][4 * k + 3] * inv};
       }
@@ -524,7 +541,9 @@ void attention_decode(const AttnParams& P0, hipStream_t s) {
       case 64: hipLaunchKernelGGL(attn_prefill_kernel<64>, grid, dim3(256), 0, s, P); return;
       case 80: hipLaunchKernelGGL(attn_prefill_kernel<80>, grid, dim3(256), 0, s, P); return;
       case 96: hipLaunchKernelGGL(attn_prefill_kernel<96>, grid, dim3(256), 0, s, P); return;
+      case 112: hipLaunchKernelGGL(attn_prefill_kernel<112>, grid, dim3(256), 0, s, P); return;  // Orca (100)
       case 128: hipLaunchKernelGGL(attn_prefill_kernel<128>, grid, dim3(256), 0, s, P); return;
+      case 256: hipLaunchKernelGGL(attn_prefill_kernel<256>, grid, dim3(256), 0, s, P); return;  // Gemma
       default: break;
     }
   }
@@ -532,9 +551,11 @@ void attention_decode(const AttnParams& P0, hipStream_t s) {
     case 64: launch_d<64>(P, s); break;
     case 80: launch_d<80>(P, s); break;
     case 96: launch_d<96>(P, s); break;
+    case 112: launch_d<112>(P, s); break;  // Orca Mini (head dim 100 in a 112-wide cache row)
     case 128: launch_d<128>(P, s); break;
-    case 256: launch_d<256>(P, s); break;  // Gemma (prefill too: the MFMA flash kernel covers D <= 128)
-    default: break;
+    case 256: launch_d<256>(P, s); break;  // Gemma
+    default:  // models/config.py rejects any other head dim at load; a direct caller must not no-op
+      throw std::runtime_error("attention: unsupported head dim " + std::to_string(P.D));
   }
 }
 

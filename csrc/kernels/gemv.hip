@@ -29,6 +29,8 @@
 // (reference pkg/model/pod.go:10-12); numerics are checked against quant.py + an fp32 torch GEMV.
 #include "gemv_core.h"
 
+#include <stdexcept>
+
 namespace omx {
 
 
@@ -37,10 +39,10 @@ GemvTuning g_tune;
 void set_gemv_tuning(int blocks_per_cu, int rows, int debug, int ks, int xfirst, int xbar, int stream,
                      int stream_bpc, int pf, int ws) {
   g_tune.debug = debug > 0 ? debug : 0;
-  if (pf == 0 || pf == 1) g_tune.pf = pf;
-  if (ws == 0 || ws == 1) g_tune.ws = ws;
-  if (stream == 0 || stream == 1) g_tune.stream = stream;
-  if (stream_bpc >= 1 && stream_bpc <= 4) g_tune.stream_bpc = stream_bpc;
+  (void)pf;  // cross-launch L2 prefetch: measured slower (profiles/r3_gemv), removed
+  (void)stream;  // the streaming / wave-specialised variants live in experiments/kernels (slower, unbuilt)
+  (void)stream_bpc;
+  (void)ws;
   if (xfirst == 0 || xfirst == 1) g_tune.xfirst = xfirst;
   if (xbar == 0 || xbar == 1) g_tune.xbar = xbar;
   if (ks >= 0 && ks <= 4) g_tune.ks = ks;
@@ -274,8 +276,6 @@ __device__ __forceinline__ void flight_body(const GemvParams& P, const int bx, c
   } else {  // diagnostic: no weight traffic at all (activation latency alone)
     for (int j = 0; j < J; ++j) T[j] = WTile<QT, NSB, R>{};
   }
-  // the next launch's first row tile -> L2, returned behind this block's own tiles (in issue order)
-  const unsigned pfv = *pf_line(P.pf, tid, (const unsigned*)x);
   __builtin_amdgcn_sched_barrier(0);  // every load issued before the prologue's first wait
   if constexpr (MRG > 0) {  // flash-decode merge: splits without keys carry m = -inf, l = 0
 #pragma unroll
@@ -399,7 +399,6 @@ __device__ __forceinline__ void flight_body(const GemvParams& P, const int bx, c
       finish_rows<R, 1>(P, acc, vb * ROWS_B + rbase, N, 0, s);
     }
     stamp(3);
-    asm volatile("" ::"v"(pfv));  // keeps the prefetch load (its value is never used)
     return;
   }
   // 4. consume the tiles in issue order
@@ -427,7 +426,6 @@ __device__ __forceinline__ void flight_body(const GemvParams& P, const int bx, c
     finish_rows<R, 1>(P, acc, t * ROWS_B + rbase, N, 0, s);
   }
   stamp(3);
-  asm volatile("" ::"v"(pfv));  // keeps the prefetch load (its value is never used)
 }
 
 template <int QT, int NSB, int R, int J, int NRM, int DBG = 0, int KS = 1, int MRG = 0, int XB = 0>
@@ -719,15 +717,12 @@ static void launch_nsb(const GemvParams& P, hipStream_t s) {
 template <int QT>
 static void launch_q(const GemvParams& P, hipStream_t s) {
   if (P.merge_S > 0) {  // only the single-chunk B == 1 flight kernel merges (merge_supported())
-    if (gemv_stream(P, s)) return;
     if (launch_flight_xb<QT>(P, 1, s)) return;
     launch_flight<QT, 1, 1>(P, s);
     return;
   }
   if (P.B == 1 || P.expert_ids != nullptr) {  // decode (and MoE: experts differ per batch row)
     const int need = ((P.w.K + 255) / 256 + 15) / 16;
-    if (P.B == 1 && gemv_ws(P, s)) return;      // wave-specialised LDS-DMA kernel (gemv_ws.hip)
-    if (P.B == 1 && gemv_stream(P, s)) return;  // bounded-depth streaming kernel (gemv_stream.hip)
     if (P.B == 1 && need <= 4) {  // whole K in one chunk: all-in-flight kernel
       if (g_tune.rows == 2 && need == 1) { launch_flight<QT, 1, 2>(P, s); return; }
       if (launch_flight_split<QT>(P, need, s)) return;
@@ -816,25 +811,15 @@ static bool launch_dual_a(const GemvParams& A, const GemvParams& Bp, int need, h
   return false;
 }
 
-// the prefetch descriptor stays only where a batch-1 flight launch of a known layout consumes it
-static void pf_filter(GemvParams& P) {
-  const int q = P.pf.qtype;
-  const bool known = q == QT_Q4_K || q == QT_Q5_K || q == QT_Q6_K || q == QT_Q4_0 || q == QT_Q8_0;
-  if (!g_tune.pf || g_tune.debug || P.B != 1 || P.expert_ids || !known || P.pf.s4) P.pf = QMat{};
-}
-
 void gemv2(const GemvParams& A0, const GemvParams& B0, hipStream_t s) {
   if (A0.B > 1 && gemv_mb2(A0, B0, s)) return;  // batched decode chain: q,k + v on the matrix cores
+  if (A0.B == 1 && A0.x8 && gemv8_2(A0, B0, s)) return;  // int8 activation chain (gemv8.hip)
   GemvParams A = A0, Bp = B0;
   A.xfirst = Bp.xfirst = g_tune.xfirst;
-  pf_filter(A);
-  pf_filter(Bp);
   const int need = ((A.w.K + 255) / 256 + 15) / 16;
   const bool ok = A.B == 1 && Bp.B == 1 && A.w.K == Bp.w.K && need <= 2 && A.norm == NORM_RMS &&
                   Bp.norm == NORM_RMS && !A.expert_ids && !Bp.expert_ids && !A.merge_S && !Bp.merge_S &&
                   A.x == Bp.x && g_tune.debug == 0;
-  if (ok && gemv_ws2(A, Bp, s)) return;
-  if (ok && gemv_stream2(A, Bp, s)) return;
   if (ok) {
     bool done = false;
     switch (eff_qtype(A)) {
@@ -857,9 +842,10 @@ bool gemv_merge_supported(int B, int K, int D, int S) {
 }
 
 void gemv(const GemvParams& P0, hipStream_t s) {
+  if (P0.B == 1 && (P0.x8 || P0.emit8) && gemv8(P0, s)) return;  // int8 activation chain (gemv8.hip)
+  if (P0.emit8) throw std::runtime_error("gemv: int8 activation emitter not covered by gemv8");
   GemvParams P = P0;
   P.xfirst = g_tune.xfirst;
-  pf_filter(P);
   if (P.merge_S > 0) {
     // flight grid for K <= 4096 is one chunk, R = 1, no K split: the merge variant covers exactly it
     if (!gemv_merge_supported(P.B, P.w.K, P.merge_D, P.merge_S) || P.norm != NORM_NONE || P.expert_ids) return;

@@ -133,35 +133,6 @@ __device__ __forceinline__ void load_wtile(const QMat& w, long long row_base, in
   }
 }
 
-// Cross-launch prefetch (GemvParams::pf): the address of one 128-byte line of the next launch's row
-// tile blockIdx.x for thread `line`, else `dummy` (an address this launch reads anyway). The tile's
-// regions are contiguous per stream (row-major streams, layout v2); the small scale streams come
-// first, then the codes. One plain load per thread: it allocates the line in this XCD's L2, where
-// block blockIdx.x of the next grid (same XCD) finds it.
-__device__ __forceinline__ const unsigned* pf_line(const QMat& w, int line, const unsigned* dummy) {
-  if (!w.s0) return dummy;
-  const int tile = blockIdx.x, rows0 = 16 * tile;
-  if (rows0 >= w.N) return dummy;
-  const int rows = min(16, w.N - rows0);
-  const long long SB = n_sb(w.K);
-  // bytes per super-block of s1, s2, s3, s0 (quant.py device repack)
-  int b1 = 16, b2 = 0, b3 = 0, b0 = 128;
-  if (w.qtype == QT_Q6_K) { b1 = 64; b2 = 16; b3 = 2; }
-  else if (w.qtype == QT_Q5_K) { b2 = 32; }
-  else if (w.qtype == QT_Q8_0) { b0 = 256; }
-  const uint8_t* base[4] = {w.s1, w.s2, w.s3, w.s0};
-  const int bsb[4] = {b1, b2, b3, b0};
-  long long l = line;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const long long len = (long long)rows * SB * bsb[i];
-    const long long nl = (len + 127) >> 7;
-    if (l < nl) return (const unsigned*)(base[i] + (long long)rows0 * SB * bsb[i] + min(l << 7, len - 4));
-    l -= nl;
-  }
-  return dummy;
-}
-
 // x fragments of one piece for BT batch rows: int8 codes (lo/hi 16 groups) + {scale, sum}
 template <int BT>
 struct XFr {
@@ -476,11 +447,5 @@ __device__ __forceinline__ void finish_rows(const GemvParams& P, float (&acc)[R]
 
 // small-batch decode (gemv_batch.hip): false = shape not covered, caller falls back
 bool gemv_batch(const GemvParams& P, hipStream_t s);
-// bounded-depth streaming batch-1 decode GEMV (gemv_stream.hip): false = not covered
-bool gemv_stream(const GemvParams& P, hipStream_t s);
-bool gemv_stream2(const GemvParams& A, const GemvParams& B, hipStream_t s);
-// wave-specialised LDS-DMA batch-1 decode GEMV (gemv_ws.hip): false = not covered
-bool gemv_ws(const GemvParams& P, hipStream_t s);
-bool gemv_ws2(const GemvParams& A, const GemvParams& B, hipStream_t s);
 
 }  // namespace omx

@@ -271,7 +271,7 @@ __device__ __forceinline__ void mb_epi(const GemvParams& P, int bb, int vn, floa
         P.y[(long long)bb * P.ldy + vn] = out;
       } else {
         const long long blk = slot / P.bs, off = slot % P.bs;
-        const long long idx = ((blk * P.n_kv + hh) * P.bs + off) * D + d;
+        const long long idx = ((blk * P.n_kv + hh) * P.bs + off) * (P.Dc > 0 ? P.Dc : D) + d;
         if (which == 1) ((f16*)P.kc)[idx] = (f16)out;
         else ((f16*)P.vc)[idx] = (f16)out;
       }

@@ -33,6 +33,7 @@ struct GemvParams {
   void* vc;
   const float* inv_freq;       // [n_rot/2]
   int Eq, Ekv, D, n_rot, n_kv, bs;
+  int Dc;                      // KV cache row stride (head dim padded to 16 on the GPU; 0 = D)
   // MoE: blockIdx.z = k-th selected expert of batch row b
   const int* expert_ids;       // [B][n_sel] or null
   const float* expert_w;       // [B][n_sel] routing weights (EPI_ADD scale) or null
@@ -71,11 +72,6 @@ struct GemvParams {
   // prologue done, first tile computed, exit; null in production
   unsigned long long* dbg_ts;
   int xfirst;                  // activations waited for before any weight load (GemvTuning::xfirst)
-  // cross-launch prefetch (B == 1 decode): the matrix the NEXT GEMV of the step streams. Block b
-  // pulls a prefix of that launch's row tile b (16 rows, every stream) into its XCD's L2 behind its
-  // own weight loads, so the bytes move while this launch computes its tail and the next one ramps
-  // (pf.s0 null: off). Block b of both grids sits on XCD b % 8.
-  QMat pf;
   // batched matrix-core decode chain (gemv_mfma.hip, 2 <= B <= 16; null = unused):
   const void* x16;             // consumer: activations already in fp16 [B][ld16] (times norm_w when norm = RMS)
   int ld16;
@@ -88,7 +84,27 @@ struct GemvParams {
   float* emit_stat;            //   and its per-16-row-tile sum-of-squares partials [tiles][16]
   void* y16;                   // EPI_GLU / EPI_GEGLU: fp16 output [B][ld16y] instead of y
   int ld16y;
+  // batch-1 int8 activation chain (gemv8.hip): the producer of a GEMV's input writes it already
+  // int8-quantised per 16-element group, in the consumer's LDS image layout (x8_bytes(K)); an RMSNorm'd
+  // input carries (x * norm_w) and per-group sum-of-squares partials of the un-normed x, and the
+  // consumer scales its outputs by rsqrt(sum / K + eps)
+  const void* x8;              // consumer: activation image (null = fp32 x / merge prologue)
+  const float* x8_stat;        //   RMS partials [K / 16] (null = no norm)
+  void* emit8;                 // producer: image of this GEMV's output (EPI_ADD: new residual * emit8_nw;
+  const float* emit8_nw;       //   EPI_GLU / EPI_GEGLU: the GLU output)
+  float* emit8_stat;           //   EPI_ADD: per-16-row sum-of-squares partials of the new residual
 };
+// int8 activation image of a K-wide row (gemv8.hip): [slots] i32x4 codes + [slots] {scale, scale * sum}
+// with one pad slot per 256-element super-block and a trailing dummy slot (the GEMV's LDS layout)
+inline int x8_slots(int K) { return ((((K + 255) / 256) * 17 + 1) + 1) & ~1; }
+inline size_t x8_bytes(int K) { return (size_t)x8_slots(K) * 24; }
+// batch-1 decode GEMV on the int8 activation chain; false = not covered (caller takes gemv.hip)
+bool gemv8(const GemvParams& P, hipStream_t s);
+bool gemv8_2(const GemvParams& A, const GemvParams& B, hipStream_t s);  // q,k + v rows, one launch
+bool gemv8_supported(const GemvParams& P);
+// gate_up (G: EPI_GLU, emits D's image) -> down (D: EPI_ADD) in one launch with an in-kernel hand-off;
+// sync: 16 zeroed ints of device memory (counters + error word); false = not covered (two launches)
+bool gemv8_ffn(const GemvParams& G, const GemvParams& D, void* sync, hipStream_t s);
 
 // y = epi(W x): the quantised GEMV for small B (decode), the MFMA dequant GEMM for B >= GEMM_MIN_B
 // when an fp16 activation workspace is given (prefill); same epilogues either way.
@@ -131,10 +147,6 @@ struct GemvTuning {
   int ks = 0;             // in-block K split of the flight kernel: 0 = auto, 1 = off, 2..4 = forced
   int xfirst = 0;         // 1: decode GEMVs wait for their activations before streaming weights
   int xbar = 0;           // 1: batch-1 decode GEMVs as x-barrier launches, one block per CU (gemv.hip XB)
-  int stream = 0;         // 1: batch-1 decode GEMVs on the bounded-depth streaming kernel (gemv_stream.hip)
-  int stream_bpc = 1;     // its blocks per CU
-  int pf = 0;             // 1: batch-1 GEMVs prefetch the next GEMV's first row tiles into L2 (GemvParams::pf)
-  int ws = 0;             // 1: batch-1 GEMVs on the wave-specialised LDS-DMA kernel (gemv_ws.hip)
 };
 extern GemvTuning g_tune;
 void set_gemv_tuning(int blocks_per_cu, int rows, int debug, int ks = -1, int xfirst = -1, int xbar = -1,
@@ -156,7 +168,8 @@ struct AttnParams {
   int max_blocks;
   const int* q_seq;            // [NQ] sequence row of each query (null -> identity)
   const int* q_len;            // [NQ] visible keys (= pos + 1)
-  int NQ, H, n_kv, D, bs;
+  int NQ, H, n_kv, D, bs;       // D: KV cache row stride (the kernel's head dim, a multiple of 16)
+  int Dv;                      // valid head dim (<= D; q / out head stride): Orca Mini D = 100 in 112 (0 = D)
   float scale;
   int window;                  // sliding window (0 = none)
   float* out;                  // [NQ][ldo] fp32

@@ -75,6 +75,57 @@ bool Executor::chain_capable() const {
   return ok(lm_head, EPI_STORE, NORM_RMS, true, false);
 }
 
+// Batch-1 int8 activation chain (gemv8.hip): O and down emit the next RMSNorm'd GEMV's input as an int8
+// image (+ sum-of-squares partials), gate_up emits down's; consumers skip the fp32 activation prologue.
+// Layer 0's QKV reads the embedding rows through gemv.hip's prologue.
+bool Executor::x8(const StepInputs& in) const {
+  return ws.x8_ok && in.B == 1 && !in.prefill && cfg.tp == 1 && cfg.arch == 0 && cfg.n_expert == 0;
+}
+
+static void x8_in(GemvParams& P, const void* img, const float* stat) {
+  P.x8 = img;
+  P.x8_stat = stat;
+}
+
+static void x8_emit(GemvParams& P, void* img, const float* nw, float* stat) {
+  P.emit8 = img;
+  P.emit8_nw = nw;
+  P.emit8_stat = stat;
+}
+
+// consumers fall back to gemv.hip's fp32 prologue on their own (the producers keep writing the fp32
+// residual / GLU rows too); an emitter the int8 kernel does not cover would leave its consumer a stale
+// image, so the chain is on only when every emitter is covered
+bool Executor::x8_capable() const {
+  if (cfg.tp != 1 || cfg.arch != 0 || cfg.n_expert != 0 || layers.empty() || !ws.x8e || !ws.x8f || !ws.x8st)
+    return false;
+  static const float dummy[4] = {0.f, 0.f, 0.f, 0.f};
+  for (const LayerW& L : layers) {
+    GemvParams O{};
+    O.w = L.wo;
+    O.B = 1;
+    O.epi = EPI_ADD;
+    O.n_sel = 1;
+    x8_emit(O, (void*)dummy, dummy, (float*)dummy);
+    GemvParams G{};
+    G.w = L.wgu;
+    G.B = 1;
+    G.epi = cfg.glu_act ? EPI_GEGLU : EPI_GLU;
+    G.n_sel = 1;
+    x8_in(G, dummy, dummy);
+    G.emit8 = (void*)dummy;
+    GemvParams D{};
+    D.w = L.wdown;
+    D.B = 1;
+    D.epi = EPI_ADD;
+    D.n_sel = 1;
+    x8_in(D, dummy, nullptr);
+    x8_emit(D, (void*)dummy, dummy, (float*)dummy);
+    if (!gemv8_supported(O) || !gemv8_supported(G) || !gemv8_supported(D)) return false;
+  }
+  return true;
+}
+
 void Executor::embed(const StepInputs& in, hipStream_t s) {
   embed_rows(tok_embd, in.tokens, in.B, ws.resid, cfg.E, s, cfg.embed_scale, ws.ext);
 }
@@ -101,17 +152,18 @@ void Executor::attn_block(int i, const StepInputs& in, hipStream_t s) {
   P.Eq = Eq;
   P.Ekv = Ekv;
   P.D = cfg.D;
+  P.Dc = cfg.Dc;
   P.n_rot = cfg.n_rot;
   P.n_kv = cfg.Hkv;
-  P.bs = in.bs;
-  P.pf = phi ? L.wgu : L.wo;  // the next GEMV of the step (gemv.hip cross-launch prefetch)
+  P.bs = in.bs;  // the next GEMV of the step (gemv.hip cross-launch prefetch)
   const bool ch = chain(in);
+  const bool q8 = x8(in);
   if (ch && i > 0) chain_in(P, ws.xa16, ws.ld_e, ws.st[1], (E + 15) / 16);  // emitted by layer i-1's down
+  if (q8 && i > 0) x8_in(P, ws.x8e, ws.x8st);                                 // emitted by layer i-1's down
   if (!L.qkv_fused) {  // q,k and v rows of different quant types: one dual launch at B == 1
     GemvParams V = P;
     V.w = L.wv;
     V.row_offset = Eq + Ekv;
-    V.pf = QMat{};
     gemv2(P, V, s);
   } else {
     gemv(P, s);
@@ -126,7 +178,6 @@ void Executor::attn_block(int i, const StepInputs& in, hipStream_t s) {
     U.bias = L.bup;
     U.y = ws.hbuf;
     U.ldy = cfg.F;
-    U.pf = L.wo;
     gemv(U, s);
   }
   // --- attention over the paged cache
@@ -142,7 +193,8 @@ void Executor::attn_block(int i, const StepInputs& in, hipStream_t s) {
   A.NQ = B;
   A.H = cfg.H;
   A.n_kv = cfg.Hkv;
-  A.D = cfg.D;
+  A.D = cfg.Dc > 0 ? cfg.Dc : cfg.D;
+  A.Dv = cfg.D;
   A.bs = in.bs;
   A.scale = 1.0f / std::sqrt((float)cfg.D);
   A.window = cfg.window;
@@ -158,7 +210,19 @@ void Executor::attn_block(int i, const StepInputs& in, hipStream_t s) {
     throw std::runtime_error("deferred attention merge: unsupported (K, D, splits)");
   A.defer = defer;
   if (ch) A.out16 = ws.a16;
-  attention_decode(A, s);
+  if (in.prefill && !segments.empty()) {  // several sequences' prompts: flash attention per segment
+    for (const auto& sg : segments) {
+      AttnParams As = A;
+      As.q = A.q + (long long)sg.first * A.ldq;
+      As.out = A.out + (long long)sg.first * A.ldo;
+      As.q_len = A.q_len + sg.first;
+      As.q_seq = A.q_seq ? A.q_seq + sg.first : nullptr;
+      As.NQ = sg.second;
+      attention_decode(As, s);
+    }
+  } else {
+    attention_decode(A, s);
+  }
   // --- output projection (+ residual, or partial sum under TP)
   GemvParams O = base_params(L.wo, B, defer ? ws.attn_ws : ws.abuf, Eq, ws);
   if (defer) {
@@ -167,7 +231,6 @@ void Executor::attn_block(int i, const StepInputs& in, hipStream_t s) {
     O.merge_D = cfg.D;
   }
   O.bias = L.bo;
-  O.pf = phi ? L.wdown : cfg.n_expert > 0 ? L.router : L.wgu;
   if (cfg.tp > 1) {
     O.epi = EPI_STORE;
     O.y = tp_dst(0, B);
@@ -180,6 +243,7 @@ void Executor::attn_block(int i, const StepInputs& in, hipStream_t s) {
     chain_in(O, ws.a16, ws.ld_q, nullptr, 0);
     chain_emit(O, ws.xa16, ws.ld_e, L.ffn_norm, ws.st[0]);  // gate_up's RMSNorm input
   }
+  if (q8) x8_emit(O, ws.x8e, L.ffn_norm, ws.x8st);  // gate_up's RMSNorm input, int8
   gemv(O, s);
 }
 
@@ -194,7 +258,6 @@ void Executor::ffn_block(int i, const StepInputs& in, hipStream_t s) {
     Dn.bias = L.bdown;
     Dn.y = dst;
     Dn.ldy = E;
-    Dn.pf = next_qkv(i);
     gemv(Dn, s);
     return;
   }
@@ -286,6 +349,7 @@ void Executor::ffn_block(int i, const StepInputs& in, hipStream_t s) {
     return;
   }
   const bool ch = chain(in);
+  const bool q8 = x8(in);
   GemvParams G = base_params(L.wgu, B, ws.resid, E, ws);
   G.norm = NORM_RMS;
   G.norm_w = L.ffn_norm;
@@ -293,22 +357,29 @@ void Executor::ffn_block(int i, const StepInputs& in, hipStream_t s) {
   G.epi = cfg.glu_act ? EPI_GEGLU : EPI_GLU;
   G.y = ws.hbuf;
   G.ldy = F;
-  G.pf = L.wdown;
   if (ch) {
     chain_in(G, ws.xa16, ws.ld_e, ws.st[0], (E + 15) / 16);
     G.y16 = ws.h16;
     G.ld16y = ws.ld_f;
   }
-  gemv(G, s);
+  if (q8) {
+    x8_in(G, ws.x8e, ws.x8st);
+    G.emit8 = ws.x8f;  // down's input
+  }
   GemvParams Dn = base_params(L.wdown, B, ws.hbuf, F, ws);
   Dn.epi = dst_epi;
   Dn.y = dst;
   Dn.ldy = E;
-  Dn.pf = next_qkv(i);
   if (ch) {  // the next RMSNorm'd GEMV: layer i+1's QKV, or the LM head
     chain_in(Dn, ws.h16, ws.ld_f, nullptr, 0);
     chain_emit(Dn, ws.xa16, ws.ld_e, i + 1 < (int)layers.size() ? layers[i + 1].attn_norm : out_norm, ws.st[1]);
   }
+  if (q8) {
+    x8_in(Dn, ws.x8f, nullptr);
+    x8_emit(Dn, ws.x8e, i + 1 < (int)layers.size() ? layers[i + 1].attn_norm : out_norm, ws.x8st);
+    if (ws.x8_fuse && gemv8_ffn(G, Dn, ws.x8sync, s)) return;  // one launch, in-kernel hand-off
+  }
+  gemv(G, s);
   gemv(Dn, s);
 }
 
@@ -331,12 +402,8 @@ void Executor::head(const StepInputs& in, hipStream_t s) {
   P.ldy = lm_head.N;
   if (chain(in) && x == ws.resid && in.n_logits == in.B && cfg.n_layer > 0)
     chain_in(P, ws.xa16, ws.ld_e, ws.st[1], (E + 15) / 16);
+  if (x8(in) && x == ws.resid && in.n_logits == 1 && cfg.n_layer > 0) x8_in(P, ws.x8e, ws.x8st);
   gemv(P, s);
-}
-
-// the first GEMV after layer i's FFN: layer i+1's QKV, or the LM head
-QMat Executor::next_qkv(int i) const {
-  return i + 1 < (int)layers.size() ? layers[i + 1].wqk : lm_head;
 }
 
 float* Executor::tp_dst(int slab, int B) const {

@@ -15,6 +15,7 @@ namespace omx {
 struct ExecConfig {
   int arch = 0;          // 0 llama-family (llama/mistral/mixtral), 1 phi2
   int E = 0, H = 0, Hkv = 0, D = 0, n_rot = 0, F = 0, n_layer = 0, V = 0;  // per-rank (TP) sizes
+  int Dc = 0;            // KV cache row stride (head dim padded to a multiple of 16; 0 = D)
   float eps = 1e-5f;
   int n_expert = 0, n_expert_used = 0;
   int window = 0;
@@ -83,6 +84,14 @@ struct Workspace {
   void* a16 = nullptr;       // fp16 attention output [17][ld_q]
   float* st[2] = {nullptr, nullptr};  // sum-of-squares partials [E / 16][16] (after O / after down)
   int ld_e = 0, ld_f = 0, ld_q = 0;
+  // batch-1 int8 activation chain (gemv8.hip): images of the E-wide (QKV / gate_up / LM head input)
+  // and F-wide (down input) activations, RMS partials [E / 16]; x8_ok once every emitter is covered
+  void* x8e = nullptr;
+  void* x8f = nullptr;
+  float* x8st = nullptr;
+  void* x8sync = nullptr;    // 16 zeroed ints: in-launch hand-off counters + error word (gemv8_ffn)
+  int x8_ok = 0;
+  int x8_fuse = 1;           // gate_up -> down in one launch (gemv8_ffn) when covered
 };
 constexpr int MB_CHAIN_MAX = 16;
 
@@ -124,12 +133,17 @@ class Executor {
   void forward_tp(const StepInputs& in, hipStream_t s);  // tp > 1, custom all-reduce (graph-capturable)
   bool ar_fits(int B) const;                             // decode batch B fits the AR slabs
   bool chain_capable() const;                            // every projection takes the fp16 matrix-core chain
+  bool x8_capable() const;                               // every emitter of the int8 chain takes gemv8
   StepInputs bound{};                                    // pre-bound step inputs (set_inputs)
+  // batched admission (Runner.admit_many): the rows of a prefill step are several sequences' contiguous
+  // prompt segments {first row, rows}; attention runs the MFMA flash kernel once per segment. Empty: one
+  // sequence (or a decode step). Host-side: admission steps are never graph-captured.
+  std::vector<std::pair<int, int>> segments;
 
  private:
   float* tp_dst(int slab, int B) const;  // where a row-parallel projection leaves its partial sums
   bool chain(const StepInputs& in) const;  // this step runs the fp16 matrix-core decode chain
-  QMat next_qkv(int i) const;          // the matrix the GEMV after layer i's FFN streams (prefetch target)
+  bool x8(const StepInputs& in) const;     // this step runs the batch-1 int8 activation chain
   int ar_active_ = 0;
 };
 

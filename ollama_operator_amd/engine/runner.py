@@ -22,6 +22,7 @@ from typing import Callable, Iterator
 import numpy as np
 import torch
 
+from ..models.config import cache_head_dim
 from ..ops import native, stream_handle
 from ..ops.reference import TorchExecutor
 from ..utils.trace import trace_range
@@ -44,7 +45,7 @@ class NativeExec:
         w, loc, cfg = r.w, r.w.local, r.w.cfg
         self.r = r
         self.exe = e = C.Executor()
-        e.configure(dict(arch=1 if cfg.arch == "phi2" else 0, E=loc["E"], H=loc["H"], Hkv=loc["Hkv"], D=loc["D"],
+        e.configure(dict(arch=1 if cfg.arch == "phi2" else 0, E=loc["E"], H=loc["H"], Hkv=loc["Hkv"], D=loc["D"], Dc=r.Dc,
                          n_rot=cfg.n_rot, F=loc["F"], n_layer=cfg.n_layer, V=loc["V"], eps=float(cfg.norm_eps),
                          n_expert=cfg.n_expert, n_expert_used=cfg.n_expert_used, window=cfg.sliding_window,
                          tp=r.tp_size, embed_scale=float(cfg.embed_scale), glu_act=int(cfg.gelu_glu)))
@@ -68,7 +69,7 @@ class NativeExec:
                              gws_elems=r.gws.numel(), max_B=r.max_batch, ld_logits=r.logits.shape[1],
                              ext=p(r.ext), w16=p(r.w16), w16_elems=r.w16.numel() if r.w16 is not None else 0,
                              yws=p(r.yws), yws_elems=r.yws.numel() if r.yws is not None else 0,
-                             n_splits=1, **self._chain_ws(r)))
+                             n_splits=1, **self._chain_ws(r), **self._x8_ws(r)))
         # step buffers bound once: every stage call below passes integers only
         e.set_inputs(dict(tokens=p(r.d_tokens), pos=p(r.d_pos), slot=p(r.d_slot), q_len=p(r.d_qlen),
                           q_seq=p(r.d_qseq), block_table=p(r.d_block_table), max_blocks=r.max_blocks,
@@ -89,6 +90,16 @@ class NativeExec:
         d = {k: v.data_ptr() for k, v in mb.items()}
         d.update(mb_ok=1, ld_e=mb["xa16"].shape[1], ld_f=mb["h16"].shape[1], ld_q=mb["a16"].shape[1])
         return d
+
+    @staticmethod
+    def _x8_ws(r) -> dict:
+        """The batch-1 int8 activation chain buffers (gemv8.hip; the executor turns the chain on only
+        when every emitter is covered: Executor::x8_capable)."""
+        b = getattr(r, "x8_bufs", None)
+        if not b:
+            return {}
+        return dict(x8e=b["x8e"].data_ptr(), x8f=b["x8f"].data_ptr(), x8st=b["x8st"].data_ptr(),
+                    x8sync=b["x8sync"].data_ptr(), x8_ok=1, x8_fuse=int(os.environ.get("OMX_X8_FUSE", "1") != "0"))
 
     def ar_fits(self, B: int) -> bool:
         return self.exe.ar_fits(B)
@@ -129,14 +140,6 @@ class Runner:
                 native().set_gemv_tuning(xfirst=int(os.environ["OMX_GEMV_XFIRST"]))
             if os.environ.get("OMX_GEMV_XBAR") in ("0", "1"):  # x-barrier one-block-per-CU decode GEMVs
                 native().set_gemv_tuning(xbar=int(os.environ["OMX_GEMV_XBAR"]))
-            if os.environ.get("OMX_GEMV_STREAM") in ("0", "1"):  # bounded-depth streaming decode GEMV
-                native().set_gemv_tuning(stream=int(os.environ["OMX_GEMV_STREAM"]))
-            if os.environ.get("OMX_GEMV_PF") in ("0", "1"):  # cross-launch L2 prefetch of the next GEMV
-                native().set_gemv_tuning(pf=int(os.environ["OMX_GEMV_PF"]))
-            if os.environ.get("OMX_GEMV_WS") in ("0", "1"):  # wave-specialised LDS-DMA decode GEMV
-                native().set_gemv_tuning(ws=int(os.environ["OMX_GEMV_WS"]))
-            if os.environ.get("OMX_GEMV_STREAM_BPC"):
-                native().set_gemv_tuning(stream_bpc=int(os.environ["OMX_GEMV_STREAM_BPC"]))
         self.tp_rank, self.tp_size, self.tp_group = tp_rank, tp_size, tp_group
         self._closed = False
         # TP serving (parallel/tp.py): rank 0 signals each decode step, followers mirror it
@@ -163,9 +166,12 @@ class Runner:
         # CPU: the cache stays untouched (and out of RSS) until blocks are written -- every slot is
         # written by its QKV step before any attention reads it
         kv_alloc = torch.zeros if self.is_gpu else torch.empty
-        self.kc = [kv_alloc(n_blocks, loc["Hkv"], block_size, loc["D"], device=dev, dtype=torch.float16)
+        # GPU cache rows are as wide as an attention kernel's head dim (Orca Mini's 100 -> 112, zero pad);
+        # the CPU backends keep the model's head dim
+        self.Dc = cache_head_dim(loc["D"]) if self.is_gpu else loc["D"]
+        self.kc = [kv_alloc(n_blocks, loc["Hkv"], block_size, self.Dc, device=dev, dtype=torch.float16)
                    for _ in range(cfg.n_layer)]
-        self.vc = [kv_alloc(n_blocks, loc["Hkv"], block_size, loc["D"], device=dev, dtype=torch.float16)
+        self.vc = [kv_alloc(n_blocks, loc["Hkv"], block_size, self.Dc, device=dev, dtype=torch.float16)
                    for _ in range(cfg.n_layer)]
         self.resid = torch.zeros(max_batch, E, **f32)
         self.qbuf = torch.zeros(max_batch, Eq, **f32)
@@ -187,6 +193,14 @@ class Runner:
             self.mb_bufs = dict(xa16=torch.zeros(17, r256(E), **h16), h16=torch.zeros(17, r256(Fl), **h16),
                                 a16=torch.zeros(17, r256(Eq), **h16), st0=torch.zeros((E + 15) // 16 * 16, **f32),
                                 st1=torch.zeros((E + 15) // 16 * 16, **f32))
+        # batch-1 int8 activation chain (csrc/kernels/gemv8.hip): zeroed images (pad slots stay zero)
+        self.x8_bufs = None
+        if self.is_gpu and os.environ.get("OMX_X8", "1") != "0":
+            C = native()
+            u8 = dict(device=dev, dtype=torch.uint8)
+            self.x8_bufs = dict(x8e=torch.zeros(C.x8_bytes(E), **u8), x8f=torch.zeros(C.x8_bytes(Fl), **u8),
+                                x8st=torch.zeros((E + 15) // 16 + 4, **f32),
+                                x8sync=torch.zeros(16, device=dev, dtype=torch.int32))
         # MoE prefill grouping (csrc/kernels/moe.hip moe_sort -> grouped MFMA GEMM)
         n_pairs = max_batch * ksel
         self.moe_rows = torch.zeros(n_pairs, **i32)
@@ -322,7 +336,7 @@ class Runner:
     def _ws_floats(self, B: int) -> int:
         loc = self.w.local
         S = self.n_splits(B)
-        return B * loc["H"] * S * (loc["D"] + 2) if S > 1 else 0
+        return B * loc["H"] * S * (self.Dc + 2) if S > 1 else 0
 
     # ------------------------------------------------------------------ forward
     def _all_reduce_add(self, B: int):
@@ -638,6 +652,12 @@ class Runner:
         finally:
             self._decode_S = 0
 
+    def x8_error(self) -> int:
+        """Nonzero when an in-launch hand-off of the int8 chain timed out (gemv8.hip ffn8_kernel): the
+        step's results are invalid. Reads device memory (a sync)."""
+        b = self.x8_bufs
+        return int(b["x8sync"][2].item()) if b else 0
+
     def set_tokens(self, tokens: list[int]) -> None:
         """Host -> d_tokens[:len(tokens)] (batch recomposition: rows' next inputs)."""
         self._upload(np.zeros((5, 0), np.int32), np.asarray(tokens, np.int32))
@@ -713,8 +733,21 @@ class Runner:
         lidx[:n] = last
         arr = np.stack([pos, np.asarray(slot_l, np.int32), pos + 1, np.asarray(row_l, np.int32), lidx])
         self._upload(arr.astype(np.int32), self._device_tokens(toks))
+        # each admitted prompt is one sequence's contiguous positions: flash (MFMA) attention per segment
+        segs, at = [], 0
+        for _sid, _k, tokens, _o, _h, _sd in items:
+            segs.append((at, len(tokens)))
+            at += len(tokens)
+        seg_exe = getattr(getattr(self.exe, "exe", None), "set_segments", None) if self.is_gpu else None
         with trace_range(f"admit_many rows={B} seqs={n}"):
-            self.forward(B, n, use_idx=True, prefill=False)
+            if seg_exe is not None:
+                seg_exe(segs)
+                try:
+                    self.forward(B, n, use_idx=True, prefill=True)
+                finally:
+                    seg_exe([])
+            else:  # torch twin / CPU backend: their attention serves any row -> sequence mapping
+                self.forward(B, n, use_idx=True, prefill=False)
         for i, (sid, _k, tokens, opts, history, seed) in enumerate(items):
             self.kv.seqs[sid].tokens.extend(tokens)
             self._set_sampler(i, opts, history, seed, 0)

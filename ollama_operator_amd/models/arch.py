@@ -43,8 +43,18 @@ def _matrix_type(ftype: FileType, role: str, layer: int, n_layer: int) -> GGMLTy
     raise NotImplementedError(f"file type {ftype!r}")
 
 
+# llama.cpp cannot k-quantise a row whose length is not a multiple of the 256-weight super-block
+# (llama_tensor_get_type): it falls back to a 32-block type. Q4_K's fallback there is Q5_0, which this
+# framework does not implement; Q4_0 stands in (same 32-block family).
+_KQ_FALLBACK = {GGMLType.Q4_K: GGMLType.Q4_0, GGMLType.Q5_K: GGMLType.Q8_0, GGMLType.Q6_K: GGMLType.Q8_0}
+
+
 def tensor_specs(cfg: ModelConfig, ftype: FileType) -> list[tuple[str, tuple[int, ...], GGMLType]]:
     """[(name, ggml shape (ne0 first), type)] for every tensor of the model."""
+    return [(n, sh, _KQ_FALLBACK.get(t, t) if sh[0] % 256 else t) for n, sh, t in _tensor_specs(cfg, ftype)]
+
+
+def _tensor_specs(cfg: ModelConfig, ftype: FileType) -> list[tuple[str, tuple[int, ...], GGMLType]]:
     E, F, V, L = cfg.n_embd, cfg.n_ff, cfg.n_vocab, cfg.n_layer
     Ekv = cfg.n_embd_kv
     f32 = GGMLType.F32

@@ -95,6 +95,7 @@ class ModelConfig:
         head = int(g("attention.key_length", n_embd // n_head))
         if int(g("attention.value_length", head)) != head:
             raise UnsupportedArchitecture("attention.value_length != attention.key_length")
+        check_head_dim(head)
         cfg = cls(
             arch=SUPPORTED_ARCHS[arch],
             n_vocab=int(g("vocab_size", len(tokens) if tokens is not None else 32000)),
@@ -146,6 +147,28 @@ class ModelConfig:
         return md
 
 
+# attention kernels (csrc/kernels/attention.hip) exist for these KV row widths; a head dim that is not
+# one of them runs in the next one up (zero-padded cache rows, masked q / output): Orca Mini's 100 -> 112
+ATTN_ROW_DIMS = (64, 80, 96, 112, 128, 256)
+
+
+def cache_head_dim(head: int) -> int:
+    """KV cache row width on the GPU for head dim `head` (the CPU backends keep `head`)."""
+    for d in ATTN_ROW_DIMS:
+        if head <= d:
+            return d
+    raise UnsupportedArchitecture(f"head dim {head} exceeds the largest attention kernel ({ATTN_ROW_DIMS[-1]})")
+
+
+def check_head_dim(head: int) -> None:
+    """Refuse at load what the GPU attention kernels cannot serve, instead of loading a model whose
+    attention would silently not run (a head dim without a kernel used to no-op)."""
+    if head <= 0 or head % 4 or cache_head_dim(head) - head >= 16:
+        raise UnsupportedArchitecture(
+            f"unsupported attention head dim {head} (supported: {', '.join(map(str, ATTN_ROW_DIMS))}, "
+            "or a multiple of 4 up to 15 below one of them)")
+
+
 PRESETS: dict[str, ModelConfig] = {
     # BASELINE headline: Llama-2-7B Q4_K_M
     "llama2-7b": ModelConfig(name="llama2-7b"),
@@ -157,6 +180,10 @@ PRESETS: dict[str, ModelConfig] = {
                               rope_base=1000000.0),
     "mixtral-8x7b": ModelConfig(name="mixtral-8x7b", n_head_kv=8, n_ff=14336, ctx_len=32768,
                                 rope_base=1000000.0, n_expert=8, n_expert_used=2),
+    # Orca Mini 3B (reference README.md:55): OpenLLaMA-3B shapes, head dim 100; Q4_0 (its E = 3200 is not a
+    # multiple of the 256-weight K-quant super-block)
+    "orca-mini-3b": ModelConfig(name="orca-mini-3b", n_embd=3200, n_layer=26, n_head=32, n_head_kv=32,
+                                n_ff=8640, n_rot=100, ctx_len=2048),
     "phi2": ModelConfig(name="phi2", arch="phi2", n_vocab=51200, n_embd=2560, n_layer=32, n_head=32,
                         n_head_kv=32, n_ff=10240, n_rot=32, rope_mode=ROPE_NEOX, norm_eps=1e-5,
                         ctx_len=2048, bos_id=50256, eos_id=50256),
@@ -174,6 +201,9 @@ PRESETS: dict[str, ModelConfig] = {
                               norm_eps=1e-6, ctx_len=256, bos_id=2, eos_id=1),
     "tiny-llama": ModelConfig(name="tiny-llama", n_vocab=512, n_embd=256, n_layer=2, n_head=4,
                               n_head_kv=2, n_ff=512, n_rot=64, ctx_len=256),
+    # head dim 100 (Orca Mini), E not a multiple of 256: Q4_0 / Q8_0 files
+    "tiny-orca": ModelConfig(name="tiny-orca", n_vocab=512, n_embd=800, n_layer=2, n_head=8, n_head_kv=8,
+                             n_ff=2176, n_rot=100, ctx_len=256),
     "tiny-mixtral": ModelConfig(name="tiny-mixtral", n_vocab=512, n_embd=256, n_layer=2, n_head=4,
                                 n_head_kv=2, n_ff=512, n_rot=64, ctx_len=256, n_expert=4,
                                 n_expert_used=2),

@@ -39,7 +39,8 @@ def tiny_models(tmp_path_factory):
     for name, ft in [("tiny-llama", FileType.MOSTLY_Q4_K_M), ("tiny-mixtral", FileType.MOSTLY_Q4_K_M),
                      ("tiny-phi2", FileType.MOSTLY_Q4_0), ("tiny-llama-q8", FileType.MOSTLY_Q8_0),
                      ("tiny-llama-q40", FileType.MOSTLY_Q4_0), ("tiny-llama-q5km", FileType.MOSTLY_Q5_K_M),
-                     ("tiny-mixtral-q5ks", FileType.MOSTLY_Q5_K_S), ("tiny-gemma", FileType.MOSTLY_Q4_K_M)]:
+                     ("tiny-mixtral-q5ks", FileType.MOSTLY_Q5_K_S), ("tiny-gemma", FileType.MOSTLY_Q4_K_M),
+                     ("tiny-orca", FileType.MOSTLY_Q4_0)]:
         base = name.replace("-q8", "").replace("-q40", "").replace("-q5km", "").replace("-q5ks", "")
         p = str(d / f"{name}.gguf")
         write_random_gguf(p, preset(base), ft, seed=zlib.crc32(name.encode()) % 1000, quantize_from_float=True)

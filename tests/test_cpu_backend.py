@@ -53,7 +53,8 @@ PROMPT = [1, 17, 42, 99, 7, 300, 12, 5, 77, 3, 250, 11]
 
 @pytest.mark.parametrize("name,ft", [("tiny-llama", FileType.MOSTLY_Q4_K_M), ("tiny-llama", FileType.MOSTLY_Q5_K_M),
                                      ("tiny-phi2", FileType.MOSTLY_Q4_0), ("tiny-mixtral", FileType.MOSTLY_Q8_0),
-                                     ("tiny-llama", FileType.MOSTLY_Q6_K), ("tiny-gemma", FileType.MOSTLY_Q4_K_M)])
+                                     ("tiny-llama", FileType.MOSTLY_Q6_K), ("tiny-gemma", FileType.MOSTLY_Q4_K_M),
+                                     ("tiny-orca", FileType.MOSTLY_Q4_0)])
 def test_native_cpu_runner_matches_torch_twin(tmp_path, name, ft):
     from ollama_operator_amd.engine.runner import Runner
     from ollama_operator_amd.engine.sampling import SamplingOptions

@@ -15,7 +15,7 @@ def rel(a, b):
 
 
 @pytest.mark.parametrize("name", ["tiny-llama", "tiny-mixtral", "tiny-phi2", "tiny-llama-q8", "tiny-llama-q40",
-                                  "tiny-llama-q5km", "tiny-mixtral-q5ks", "tiny-gemma"])
+                                  "tiny-llama-q5km", "tiny-mixtral-q5ks", "tiny-gemma", "tiny-orca"])
 def test_native_vs_torch_teacher_forced(tiny_models, name):
     path = tiny_models[name]
     g = Runner(path, device="cuda", max_batch=8, max_seqs=2, ctx=128)
@@ -58,7 +58,7 @@ def test_long_context_splits(tiny_models):
 
 
 @pytest.mark.parametrize("name", ["tiny-llama", "tiny-mixtral", "tiny-phi2", "tiny-llama-q8", "tiny-llama-q40",
-                                  "tiny-llama-q5km", "tiny-mixtral-q5ks", "tiny-gemma"])
+                                  "tiny-llama-q5km", "tiny-mixtral-q5ks", "tiny-gemma", "tiny-orca"])
 def test_prefill_gemm_path_vs_torch(tiny_models, name):
     """Prompts >= GEMM_MIN_B take the MFMA GEMM path (and, for Mixtral, the device-sorted grouped
     expert GEMM with the routing-weighted scatter); logits must match the torch twin."""

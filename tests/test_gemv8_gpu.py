@@ -1,0 +1,218 @@
+"""Batch-1 int8 activation chain (csrc/kernels/gemv8.hip) against fp32 PyTorch references: the
+consumer reads a producer-written int8 image (+ RMS partials) and must equal the fp32 GEMV of the
+normed input; producers (residual-add, GLU) must write the same outputs as the fp32 path AND an image
+that decodes to the next input. The int8 activation rounding (per 16 elements) bounds the error."""
+import numpy as np
+import pytest
+import torch
+
+from ollama_operator_amd.gguf import GGMLType
+
+from test_kernels_gpu import QM, C, S, rel
+
+pytestmark = pytest.mark.gpu
+
+EPI_STORE, EPI_ADD, EPI_GLU, EPI_QKV, EPI_GEGLU = 0, 1, 2, 4, 5
+
+
+def make_image(x: torch.Tensor, nw: torch.Tensor | None = None):
+    """Host-side reference encoder of the image layout (ops.h x8_bytes): int8(x * nw) per 16-group,
+    {d, d * sum(q)} per slot, pad slot 16 of every super-block, trailing dummy; + RMS partials of x."""
+    K = x.numel()
+    xs = (x * nw if nw is not None else x).float().cpu().numpy()
+    SB = (K + 255) // 256
+    slots = C().x8_slots(K)
+    q = np.zeros((slots, 16), np.int8)
+    f = np.zeros((slots, 2), np.float32)
+    for gi in range(K // 16):
+        v = xs[16 * gi:16 * gi + 16]
+        amax = np.abs(v).max()
+        d = np.float32(amax / 127.0)
+        qq = np.rint(v * (127.0 / amax)).astype(np.int32) if amax > 0 else np.zeros(16, np.int32)
+        slot = (gi // 16) * 17 + gi % 16
+        q[slot] = qq.astype(np.int8)
+        f[slot] = (d, d * qq.sum())
+    img = np.concatenate([q.reshape(-1).view(np.uint8), f.reshape(-1).view(np.uint8)])
+    assert img.nbytes == C().x8_bytes(K) and SB * 17 < slots
+    st = (x.float().reshape(-1, 16) ** 2).sum(1).cpu()
+    return torch.from_numpy(img).cuda(), torch.cat([st, torch.zeros(4)]).cuda()
+
+
+def decode_image(img: torch.Tensor, K: int) -> torch.Tensor:
+    slots = C().x8_slots(K)
+    a = img.cpu().numpy()
+    q = a[:slots * 16].view(np.int8).reshape(slots, 16).astype(np.float32)
+    f = a[slots * 16:].view(np.float32).reshape(slots, 2)
+    out = np.zeros(K, np.float32)
+    for gi in range(K // 16):
+        slot = (gi // 16) * 17 + gi % 16
+        out[16 * gi:16 * gi + 16] = q[slot] * f[slot, 0]
+    return torch.from_numpy(out)
+
+
+def call(m, B, x, y, epi, ops, ldy=None):
+    C().gemv(m.tup, B, x.data_ptr() if x is not None else 0, m.tup[5], 0, 0, 0, 1e-5, epi, y.data_ptr(),
+             ldy or y.shape[-1], 0, 0, ops, S())
+
+
+@pytest.mark.parametrize("qt", [GGMLType.Q4_K, GGMLType.Q6_K, GGMLType.Q4_0, GGMLType.Q8_0, GGMLType.Q5_K])
+@pytest.mark.parametrize("K", [4096, 11008])
+def test_consumer_rms_store(qt, K):
+    """K = 4096: an RMSNorm'd input (QKV / gate_up / LM head shape); K = 11008: the un-normed GLU output
+    (down's input, in-block K split over 3 wave groups)."""
+    N = 1024 if K == 4096 else 512
+    m = QM(qt, N, K, seed=K + int(qt))
+    x = torch.randn(K, device="cuda") * 2
+    rms = K == 4096
+    nw = torch.rand(K, device="cuda") + 0.5 if rms else None
+    img, st = make_image(x, nw)
+    y = torch.zeros(1, N, device="cuda")
+    ops = {"x8": img.data_ptr()}
+    if rms:
+        ops["x8_stat"] = st.data_ptr()
+    call(m, 1, None, y, EPI_STORE, ops)
+    xn = x * torch.rsqrt(x.pow(2).mean() + 1e-5) * nw if rms else x
+    ref = (xn @ m.w.T)[None]
+    assert rel(y, ref) < 1.5e-2
+
+
+@pytest.mark.parametrize("qt", [GGMLType.Q4_K, GGMLType.Q6_K])
+def test_residual_producer_emits_next_input(qt):
+    """O / down shape: EPI_ADD into the residual, image of (new resid * next norm w) + partials."""
+    N, K = 4096, 11008
+    m = QM(qt, N, K, seed=5)
+    h = torch.randn(K, device="cuda")
+    img_in, _ = make_image(h)
+    resid0 = torch.randn(1, N, device="cuda") * 4
+    resid = resid0.clone()
+    nw = torch.rand(N, device="cuda") + 0.5
+    out = torch.zeros(C().x8_bytes(N), dtype=torch.uint8, device="cuda")
+    st = torch.zeros(N // 16 + 4, device="cuda")
+    call(m, 1, None, resid, EPI_ADD, {"x8": img_in.data_ptr(), "emit8": out.data_ptr(),
+                                      "emit8_nw": nw.data_ptr(), "emit8_stat": st.data_ptr()})
+    ref = resid0 + (h @ m.w.T)[None]
+    assert rel(resid - resid0, ref - resid0) < 1.5e-2
+    # the emitted image decodes to (new resid * nw) within int8 rounding, partials = group sums of squares
+    dec = decode_image(out, N)
+    want = (resid[0] * nw).cpu()
+    assert rel(dec, want) < 1e-2
+    assert torch.allclose(st[:N // 16].cpu(), (resid[0].cpu().reshape(-1, 16) ** 2).sum(1), rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("act", [EPI_GLU, EPI_GEGLU])
+def test_glu_producer_emits_down_input(act):
+    """gate_up shape (interleaved gate/up rows): h written to y and emitted as down's image."""
+    F, K = 11008, 4096
+    m = QM(GGMLType.Q4_K, 2 * F, K, seed=9)
+    x = torch.randn(K, device="cuda")
+    nw = torch.rand(K, device="cuda") + 0.5
+    img, st = make_image(x, nw)
+    y = torch.zeros(1, F, device="cuda")
+    out = torch.zeros(C().x8_bytes(F), dtype=torch.uint8, device="cuda")
+    call(m, 1, None, y, act, {"x8": img.data_ptr(), "x8_stat": st.data_ptr(), "emit8": out.data_ptr()})
+    xn = x * torch.rsqrt(x.pow(2).mean() + 1e-5) * nw
+    gu = xn @ m.w.T
+    g, u = gu[0::2], gu[1::2]
+    hact = torch.nn.functional.silu(g) if act == EPI_GLU else torch.nn.functional.gelu(g, approximate="tanh")
+    ref = hact * u
+    assert rel(y[0], ref) < 2e-2
+    assert rel(decode_image(out, F), y[0].cpu()) < 1e-2
+
+
+@pytest.mark.parametrize("S_", [1, 2, 4])
+def test_merge_producer(S_):
+    """O projection: deferred flash-decode partial slabs (or a plain fp32 row) in, residual + image out."""
+    N, K, D = 4096, 4096, 128
+    m = QM(GGMLType.Q4_K, N, K, seed=11)
+    nh = K // D
+    acc = torch.randn(S_, K, device="cuda")
+    mx = torch.randn(S_, nh, device="cuda")
+    l = torch.rand(S_, nh, device="cuda") + 0.5
+    if S_ > 1:
+        ml = torch.stack([mx, l], -1).contiguous()
+        wgt = torch.exp(mx - mx.max(0).values)  # [S, nh]
+        x = (acc.view(S_, nh, D) * wgt[..., None]).sum(0) / (wgt * l).sum(0)[:, None]
+        x = x.reshape(K)
+        ops = {"merge_S": S_, "merge_ml": ml.data_ptr(), "merge_D": D}
+    else:
+        x = acc[0]
+        ops = {}
+    resid0 = torch.randn(1, N, device="cuda")
+    resid = resid0.clone()
+    nw = torch.rand(N, device="cuda") + 0.5
+    out = torch.zeros(C().x8_bytes(N), dtype=torch.uint8, device="cuda")
+    st = torch.zeros(N // 16 + 4, device="cuda")
+    ops.update(emit8=out.data_ptr(), emit8_nw=nw.data_ptr(), emit8_stat=st.data_ptr())
+    call(m, 1, acc, resid, EPI_ADD, ops)
+    ref = resid0 + (x @ m.w.T)[None]
+    assert rel(resid - resid0, ref - resid0) < 1.5e-2
+    assert rel(decode_image(out, N), (resid[0] * nw).cpu()) < 1e-2
+
+
+def test_engine_x8_chain_on_and_matches_torch(tmp_path):
+    """Llama Q4_K_M batch-1 decode through the executor: the chain is on (every emitter covered) and
+    teacher-forced decode steps (graph replays of the decode path, where the chain runs) track the fp32
+    torch twin's logits."""
+    from ollama_operator_amd.engine.runner import Runner
+    from ollama_operator_amd.gguf.constants import FileType
+    from ollama_operator_amd.models.config import preset
+    from ollama_operator_amd.models.random_init import write_random_gguf
+    p = str(tmp_path / "m.gguf")
+    write_random_gguf(p, preset("tiny-llama"), FileType.MOSTLY_Q4_K_M, seed=4, quantize_from_float=True)
+    g = Runner(p, device="cuda:0", max_batch=16, max_seqs=1, ctx=256)
+    assert g.exe.exe.x8_on == 1
+    c = Runner(p, device="cpu", max_batch=16, max_seqs=1, ctx=256, cpu_backend="torch")
+    prompt = [1, 17, 33, 49, 65]
+    sg, sc = g.new_sequence(), c.new_sequence()
+    g.prefill(sg, prompt)
+    c.prefill(sc, prompt)
+    V = g.cfg.n_vocab
+    for t in [8, 9, 10, 11, 12]:
+        g.set_tokens([t])
+        g.decode_step(sg)
+        torch.cuda.synchronize()
+        g.kv.seqs[sg].tokens.append(t)
+        c.prefill(sc, [t])
+        assert rel(g.logits[0, :V].cpu(), c.logits[0, :V]) < 3e-2
+
+
+@pytest.mark.parametrize("qd", [GGMLType.Q4_K, GGMLType.Q6_K])
+def test_fused_ffn_matches_two_launches(qd):
+    """gate_up -> down in one launch (ffn8_kernel, in-kernel hand-off): the residual, h and the emitted
+    next-layer image equal the two-launch path; repeated launches re-arm the counters; no timeout."""
+    E, F = 4096, 11008
+    mg = QM(GGMLType.Q4_K, 2 * F, E, seed=21)
+    md = QM(qd, E, F, seed=22)
+    x = torch.randn(E, device="cuda")
+    nw = torch.rand(E, device="cuda") + 0.5
+    nw2 = torch.rand(E, device="cuda") + 0.5
+    img, st = make_image(x, nw)
+    sync = torch.zeros(16, dtype=torch.int32, device="cuda")
+    outs = []
+    for fused in (False, True):
+        resid0 = torch.randn(1, E, device="cuda", generator=torch.Generator("cuda").manual_seed(3))
+        resid = resid0.clone()
+        h = torch.zeros(1, F, device="cuda")
+        img_f = torch.zeros(C().x8_bytes(F), dtype=torch.uint8, device="cuda")
+        img_o = torch.zeros(C().x8_bytes(E), dtype=torch.uint8, device="cuda")
+        st_o = torch.zeros(E // 16 + 4, device="cuda")
+        if fused:
+            for _ in range(3):  # counters re-arm between launches
+                resid.copy_(resid0)
+                assert C().gemv8_ffn(mg.tup, md.tup, img.data_ptr(), st.data_ptr(), img_f.data_ptr(), h.data_ptr(),
+                                     resid.data_ptr(), nw2.data_ptr(), img_o.data_ptr(), st_o.data_ptr(),
+                                     sync.data_ptr(), EPI_GLU, 1e-5, S())
+        else:
+            call(mg, 1, None, h, EPI_GLU, {"x8": img.data_ptr(), "x8_stat": st.data_ptr(), "emit8": img_f.data_ptr()})
+            call(md, 1, None, resid, EPI_ADD, {"x8": img_f.data_ptr(), "emit8": img_o.data_ptr(),
+                                                "emit8_nw": nw2.data_ptr(), "emit8_stat": st_o.data_ptr()})
+        torch.cuda.synchronize()
+        outs.append((resid.clone(), h.clone(), img_o.clone(), st_o.clone(), resid0))
+    assert int(sync[2].item()) == 0 and int(sync[0].item()) == 0 and int(sync[1].item()) == 0
+    (r1, h1, i1, s1, r0), (r2, h2, i2, s2, _) = outs
+    assert torch.equal(h1, h2) and torch.equal(r1, r2) and torch.equal(i1, i2) and torch.equal(s1, s2)
+    xn = x * torch.rsqrt(x.pow(2).mean() + 1e-5) * nw
+    gu = xn @ mg.w.T
+    hr = torch.nn.functional.silu(gu[0::2]) * gu[1::2]
+    ref = r0[0] + hr @ md.w.T
+    assert rel(r2[0] - r0[0], ref - r0[0]) < 2e-2

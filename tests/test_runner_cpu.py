@@ -9,7 +9,7 @@ from ollama_operator_amd.engine.sampling import SamplingOptions
 from ollama_operator_amd.gguf import read_gguf
 from ollama_operator_amd.models.reference import KVCacheRef, ReferenceModel
 
-MODELS = ["tiny-llama", "tiny-mixtral", "tiny-phi2", "tiny-llama-q8", "tiny-llama-q40", "tiny-llama-q5km"]
+MODELS = ["tiny-llama", "tiny-mixtral", "tiny-phi2", "tiny-llama-q8", "tiny-llama-q40", "tiny-llama-q5km", "tiny-orca"]
 
 
 @pytest.mark.parametrize("name", MODELS)
@@ -82,3 +82,16 @@ def test_admit_many_matches_sequential_admits(tiny_models):
         assert firsts[i] == tok
     for sid, p in zip(sids, prompts):
         assert r.kv.seqs[sid].tokens == p
+
+
+def test_unsupported_head_dim_fails_at_load(tmp_path):
+    """A head dim no attention kernel serves is refused when the model loads (it used to load and then
+    skip attention on the GPU): 132 is past 128 and far below 256."""
+    from ollama_operator_amd.gguf.constants import FileType
+    from ollama_operator_amd.models.config import UnsupportedArchitecture, preset
+    from ollama_operator_amd.models.random_init import write_random_gguf
+    p = str(tmp_path / "bad.gguf")
+    write_random_gguf(p, preset("tiny-llama", n_embd=264, n_head=2, n_head_kv=2, n_rot=132, n_embd_head=132),
+                      FileType.MOSTLY_Q8_0, seed=1)
+    with pytest.raises(UnsupportedArchitecture):
+        Runner(p, device="cpu", max_batch=4, max_seqs=1, ctx=32)
