@@ -186,6 +186,7 @@ PYBIND11_MODULE(_C, m) {
     P.row_offset = row_offset;
     P.n_sel = 1;
     if (qkv.contains("xws")) P.xws = Pp<void>(qkv["xws"].cast<uintptr_t>());  // enables the GEMM path
+    if (qkv.contains("xws_elems")) P.xws_elems = qkv["xws_elems"].cast<long long>();
     if (qkv.contains("dbg_ts")) P.dbg_ts = Pp<unsigned long long>(qkv["dbg_ts"].cast<uintptr_t>());
     if (qkv.contains("gws")) {  // split-K slabs for small-M GEMMs
       P.gws = Pp<float>(qkv["gws"].cast<uintptr_t>());
@@ -295,6 +296,8 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("set_gemm_lib_min_m", &set_gemm_lib_min_m, "prefill rows from which the hipBLASLt path runs (0 = off)");
   m.def("gemm_lib_min_m", &gemm_lib_min_m);
+  m.def("set_dq_gemm", &set_dq_gemm, "1: prefill GEMMs from 128 rows on the stream-order dequant kernel (gemm_dq.hip)");
+  m.def("dq_gemm_enabled", &dq_gemm_enabled);
   m.def("gemm_lib_prepare", [](int N, int K, int min_M, int max_M, size_t ws_bytes) {
     blas_prepare(N, K, min_M, max_M, ws_bytes);
   });
@@ -514,15 +517,19 @@ PYBIND11_MODULE(_C, m) {
         w.x8f = Pp<void>(ptr("x8f"));
         w.x8st = Pp<float>(ptr("x8st"));
         w.x8sync = Pp<void>(ptr("x8sync"));
+        w.x8q = Pp<void>(ptr("x8q"));
         w.x8_fuse = d.contains("x8_fuse") ? d["x8_fuse"].cast<int>() : 1;
         w.x8_ok = (d.contains("x8_ok") ? d["x8_ok"].cast<int>() : 0) && e.x8_capable() ? 1 : 0;
       })
       .def_property_readonly("x8_on", [](const Executor& e) { return e.ws.x8_ok; })
+      .def_property_readonly("n_attn8", [](const Executor& e) { return e.n_attn8; })
+      .def_property_readonly("n_ffn8", [](const Executor& e) { return e.n_ffn8; })
       .def("set_segments", [](Executor& e, std::vector<std::pair<int, int>> segs) { e.segments = std::move(segs); })
-      .def("set_splits", [](Executor& e, int n, int defer) {
+      .def("set_splits", [](Executor& e, int n, int defer, int fuse) {
         e.ws.n_splits = n;
         e.ws.defer = defer;
-      }, py::arg("n"), py::arg("defer") = 0)
+        e.ws.attn_fuse = fuse;
+      }, py::arg("n"), py::arg("defer") = 0, py::arg("fuse") = 0)
       .def("run", [](Executor& e, const std::string& what, int layer, py::dict d, uintptr_t stream) {
         static const std::pair<const char*, int> names[] = {{"forward", ST_FORWARD}, {"embed", ST_EMBED},
             {"attn", ST_ATTN}, {"ffn", ST_FFN}, {"head", ST_HEAD}, {"forward_tp", ST_FORWARD_TP}};

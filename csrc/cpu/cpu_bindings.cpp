@@ -124,7 +124,7 @@ PYBIND11_MODULE(_cpu, m) {
         b.max_B = d["max_B"].cast<int>();
         b.ld_logits = d.contains("ld_logits") ? d["ld_logits"].cast<int>() : e.cfg.V;
       })
-      .def("set_splits", [](Engine&, int, int) {}, py::arg("n"), py::arg("defer") = 0)
+      .def("set_splits", [](Engine&, int, int, int) {}, py::arg("n"), py::arg("defer") = 0, py::arg("fuse") = 0)
       .def("set_inputs", [](Engine& e, py::dict d) {
         auto ptr = [&](const char* k) -> uintptr_t { return d.contains(k) ? d[k].cast<uintptr_t>() : 0; };
         Buffers& b = e.buf;

@@ -456,6 +456,10 @@ static int split_k(const GemvParams& P, int tiles, int nks) {
   return sk;
 }
 
+void gemm_finalize(const GemvParams& P, int sk, hipStream_t s) {
+  hipLaunchKernelGGL(gemm_finalize_kernel, finalize_grid(P.B, P.w.N), dim3(256), 0, s, P, sk, (const int*)nullptr);
+}
+
 template <int QT>
 static void launch_gemm(const GemvParams& P, const f16* x16, hipStream_t s) {
   const int nt = (P.w.N + GM_BN - 1) / GM_BN, mt = (P.B + GM_BM - 1) / GM_BM;
@@ -536,7 +540,7 @@ static int g_lib_min_m = -1;  // -1: OMX_GEMM_LIB_MIN_M (default 256), read once
 int gemm_lib_min_m() {
   if (g_lib_min_m < 0) {
     const char* e = getenv("OMX_GEMM_LIB_MIN_M");
-    g_lib_min_m = e ? atoi(e) : 256;
+    g_lib_min_m = e ? atoi(e) : 0;
   }
   return g_lib_min_m;
 }
@@ -564,8 +568,16 @@ static bool gemm_lib(const GemvParams& P, const f16* x16, hipStream_t s) {
 
 void gemm(const GemvParams& P, hipStream_t s) {
   f16* x16 = (f16*)P.xws;
-  hipLaunchKernelGGL(prep_x16_kernel, dim3(P.B), dim3(256), 0, s, P, x16);
-  if (gemm_lib(P, x16, s)) return;
+  // hipBLASLt only when asked for (OMX_GEMM_LIB_MIN_M / set_gemm_lib_min_m: the test oracle and A/B
+  // baseline); from 128 rows the stream-order kernel (gemm_dq.hip), below that the 128 x 128 tile here
+  const int lm = gemm_lib_min_m();
+  const bool lib = lm > 0 && P.B >= lm;
+  if (lib) {
+    hipLaunchKernelGGL(prep_x16_kernel, dim3(P.B), dim3(256), 0, s, P, x16);
+    if (gemm_lib(P, x16, s)) return;
+  }
+  if (dq_gemm(P, s)) return;
+  if (!lib) hipLaunchKernelGGL(prep_x16_kernel, dim3(P.B), dim3(256), 0, s, P, x16);
   switch (P.w.qtype) {
     case QT_Q4_K: launch_gemm<QT_Q4_K>(P, x16, s); break;
     case QT_Q6_K: launch_gemm<QT_Q6_K>(P, x16, s); break;

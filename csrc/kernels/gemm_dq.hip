@@ -1,0 +1,433 @@
+// Prefill dequant GEMM, stream-order edition: Y[M][N] = epi(X[M][K] . W[N][K]^T)
+// for M = prompt tokens, W in the resident layout v2 (no second weight copy, no fp16 weight scratch).
+//
+// MI355X-first design:
+//  * K in STORAGE order. Layout v2 keeps each row's codes piece-major (piece t of super-block sb at
+//    byte (t * SB + sb) * piece_bytes), so the row's code stream is one contiguous run. A dot product
+//    is invariant under a common permutation of K, so this kernel walks K in exactly that stream
+//    order: K step ks is the 32 (64 for Q8_0) contiguous code bytes of pieces 2 ks, 2 ks + 1 of every
+//    weight row -- no gather, each 128-B line is consumed over 4 consecutive K steps from L2. The
+//    activations are written once per GEMM in the same order by `prep_xp_kernel` (RMSNorm / LayerNorm
+//    fused there), so the X tile is a plain row-major [M][Kp] fp16 slab.
+//  * Inside a piece the packed-fp16 dequant produces weights in the order lo(0,2,1,3, 4,6,5,7, ...),
+//    hi(same): `(q >> {0,8,4,12}) & 0x000F000F | 0x64006400` is two exact halves 1024 + n per VALU op,
+//    then one v_pk_add (remove 1024) + one v_pk_fma (scale, zero point) -- ~2.5 VALU per 2 weights,
+//    paid once per weight per 256-token M tile (the decode GEMVs pay it once per token).
+//  * Block tile BM (tokens) x BN (weight rows) x 64 K, 8 waves (WM x WN), each a (BM/WM) x (BN/WN)
+//    sub-tile of `v_mfma_f32_16x16x32_f16` accumulators (128 fp32 per lane at 256 x 256). Both
+//    operands are staged in LDS as [rows][64 + 8] fp16: 144-B rows put the 16-B fragment reads of 16
+//    consecutive rows on distinct bank groups (conflict-free), and both A (X rows) and B (W rows) read
+//    "8 consecutive K of one row" per lane, so one image format serves both.
+//  * Software pipeline, one register stage (the guide's T14 form): after the barrier that publishes
+//    K step ks, every thread dequantises step ks + 1 (loaded a whole step ago) into the other LDS
+//    buffer, issues the loads of step ks + 2, then runs the MFMAs of step ks -- one barrier per K step,
+//    HBM/L2 latency covered by a full step of matrix work, VALU dequant of one wave overlapping the
+//    MFMAs of the other wave on its SIMD.
+//  * Grid: XCD-aware bijective remap; blocks that share an XCD (and its L2) walk the M tiles of the
+//    same N tile, so each weight tile is fetched from HBM about once per XCD. Grids that cannot fill
+//    256 CUs split K (fp32 slabs + the deterministic finalize of gemm.hip).
+//  * Epilogue straight from the accumulators: the C fragment holds weight rows n on lanes 16 apart
+//    and the row pair (n, n ^ 1) on adjacent lanes (one DPP swap), so SiLU-GLU / RoPE + KV scatter /
+//    residual add / bias run through the shared epi_apply (epilogue.h) with no LDS round trip.
+// Parity: replaces llama.cpp's prefill matmul inside `ollama/ollama` (reference pkg/model/pod.go:10-12);
+// numerics vs fp32 torch on the dequantised weights in tests/test_gemm_gpu.py (dq cases).
+#include <stdexcept>
+
+#include "common.h"
+#include "epilogue.h"
+#include "ops.h"
+
+namespace omx {
+
+namespace {
+
+constexpr int DQ_NT = 512;        // 8 waves
+constexpr int DQ_BK = 64;         // K per step (two 32-code pieces per weight row)
+constexpr int DQ_LDR = DQ_BK + 8; // fp16 LDS row stride (144 B)
+constexpr unsigned DQ_MAGIC = 0x64006400u;
+
+typedef _Float16 dh2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ dh2 dq_h2(unsigned v) { return __builtin_bit_cast(dh2, v); }
+__device__ __forceinline__ unsigned dq_u(dh2 v) { return __builtin_bit_cast(unsigned, v); }
+__device__ __forceinline__ dh2 dq_splat(float f) { return (dh2){(f16)f, (f16)f}; }
+// (n + 1024) pairs -> (n - off') * s + c  (off' = 1024 + zero point)
+__device__ __forceinline__ unsigned dq2(unsigned p, dh2 off, dh2 sc, dh2 c) {
+  return dq_u((dq_h2(p) - off) * sc + c);
+}
+__device__ __forceinline__ unsigned dsel(const u32x4& v, int i) { return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w; }
+
+// weight offsets (natural K) of the lo / hi 16-weight halves of piece t of super-block sb
+template <int QT>
+__host__ __device__ __forceinline__ int piece_off(int t, int sb, int g) {
+  if constexpr (QT == QT_Q4_K || QT == QT_Q5_K) return 256 * sb + 64 * (t >> 1) + 16 * (t & 1) + 32 * g;
+  else if constexpr (QT == QT_Q6_K) return 256 * sb + 128 * (t >> 2) + 16 * (t & 3) + 64 * g;
+  else return 256 * sb + 32 * t + 16 * g;  // Q4_0 / Q8_0
+}
+
+// ------------------------------------------------------------------------------------------------
+// activations: x fp32 [B][ldx] -> (norm) -> fp16 [B][Kp] in storage order; one block per row.
+// Stream position kp: piece P = kp / 32 (t = P / SB, sb = P % SB), slot p = kp % 32: half g = p / 16,
+// byte i = 4 ((p & 15) / 4) + (0, 2, 1, 3)[p & 3] -> natural k = piece_off(t, sb, g) + i
+template <int QT>
+__global__ __launch_bounds__(256) void prep_xp_kernel(GemvParams P, f16* out, int Kp) {
+  __shared__ float red[4];
+  const int b = blockIdx.x, K = P.w.K, SB = Kp >> 8;
+  const float* x = P.x + (long long)b * P.ldx;
+  float mean = 0.f, rstd = 1.f;
+  if (P.norm != NORM_NONE) {
+    float s = 0.f, ss = 0.f;
+    for (int i = threadIdx.x; i < K / 4; i += 256) {
+      const f32x4 v = *(const f32x4*)(x + 4 * i);
+      s += v.x + v.y + v.z + v.w;
+      ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+    }
+    ss = block_sum<256>(ss, red);
+    if (P.norm == NORM_LAYER) {
+      s = block_sum<256>(s, red);
+      mean = s / K;
+      rstd = rsqrtf(fmaxf(ss / K - mean * mean, 0.f) + P.eps);
+    } else {
+      rstd = rsqrtf(ss / K + P.eps);
+    }
+  }
+  f16* o = out + (long long)b * Kp;
+  for (int c = threadIdx.x; c < Kp / 8; c += 256) {
+    const int kp = 8 * c, pc = kp >> 5, p0 = kp & 31;
+    const int t = pc / SB, sb = pc - t * SB;
+    const int base = piece_off<QT>(t, sb, p0 >> 4) + 4 * ((p0 & 15) >> 2);
+    f16x8 v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int r = j & 3;
+      const int k = base + 4 * (j >> 2) + (r == 1 ? 2 : r == 2 ? 1 : r);
+      float e = 0.f;
+      if (k < K) {
+        e = x[k];
+        if (P.norm != NORM_NONE) {
+          e = (e - mean) * rstd * P.norm_w[k];
+          if (P.norm == NORM_LAYER && P.norm_b) e += P.norm_b[k];
+        }
+      }
+      v[j] = (f16)e;
+    }
+    *(f16x8*)(o + kp) = v;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// one weight-row piece (32 codes) in registers: codes + the scale bytes it needs
+template <int QT>
+struct Piece {
+  u32x4 a;                                   // 16 code bytes (Q8_0: first 16)
+  u32x4 b;                                   // Q8_0: last 16 code bytes
+  u32x4 m;                                   // Q4_K / Q5_K meta (d, dmin, scales12); Q6_K int8 scales
+  u32x2 h;                                   // Q6_K high-bit pairs
+  unsigned e;                                // Q5_K 5th bits; Q6_K / Q4_0 / Q8_0: fp16 d (low half)
+};
+
+template <int QT>
+__device__ __forceinline__ void load_piece(const QMat& w, long long row, int SB, int pc, Piece<QT>& R) {
+  const int t = pc / SB, sb = pc - t * SB;
+  if constexpr (QT == QT_Q8_0) {
+    const uint8_t* q = w.s0 + row * SB * 256 + 32LL * pc;
+    R.a = *(const u32x4*)q;
+    R.b = *(const u32x4*)(q + 16);
+    R.e = *(const uint16_t*)(w.s1 + row * SB * 16 + 16LL * sb + 2 * t);
+  } else {
+    R.a = *(const u32x4*)(w.s0 + row * SB * 128 + 16LL * pc);
+    if constexpr (QT == QT_Q4_K || QT == QT_Q5_K) R.m = *(const u32x4*)(w.s1 + row * SB * 16 + 16LL * sb);
+    if constexpr (QT == QT_Q5_K) R.e = *(const unsigned*)(w.s2 + row * SB * 32 + 4LL * pc);
+    if constexpr (QT == QT_Q6_K) {
+      R.h = *(const u32x2*)(w.s1 + row * SB * 64 + 8LL * pc);
+      R.m = *(const u32x4*)(w.s2 + row * SB * 16 + 16LL * sb);
+      R.e = *(const uint16_t*)(w.s3 + row * SB * 2 + 2LL * sb);
+    }
+    if constexpr (QT == QT_Q4_0) R.e = *(const uint16_t*)(w.s1 + row * SB * 16 + 16LL * sb + 2 * t);
+  }
+}
+
+// Q4_K / Q5_K 6-bit scale and min of sub-block j
+__device__ __forceinline__ void k_scale(const u32x4& m, int j, float& sc, float& mn) {
+  const float d = h2f(m.x & 0xFFFF), dmin = h2f(m.x >> 16);
+  const int sh = 8 * (j & 3);
+  const unsigned a = (m.y >> sh) & 0xFF, b = (m.z >> sh) & 0xFF, e = (m.w >> sh) & 0xFF;
+  const unsigned s = j < 4 ? (a & 63) : ((e & 0xF) | ((a >> 6) << 4));
+  const unsigned mm = j < 4 ? (b & 63) : ((e >> 4) | ((b >> 6) << 4));
+  sc = d * (float)s;
+  mn = -dmin * (float)mm;
+}
+
+// dequantise a piece to 32 fp16 in stream order: o[0..7] = lo half pairs, o[8..15] = hi half pairs
+template <int QT>
+__device__ __forceinline__ void dq_piece(const Piece<QT>& R, int t, unsigned (&o)[16]) {
+  if constexpr (QT == QT_Q4_K || QT == QT_Q5_K) {
+    const int c = t >> 1;
+    float s0, c0, s1, c1;
+    k_scale(R.m, 2 * c, s0, c0);
+    k_scale(R.m, 2 * c + 1, s1, c1);
+    const dh2 off = dq_splat(1024.f), S0 = dq_splat(s0), S1 = dq_splat(s1), C0 = dq_splat(c0), C1 = dq_splat(c1);
+    const u32x4 q = QT == QT_Q4_K ? (R.a ^ 0x80808080u) : R.a;  // Q4_K: undo the signed-high-nibble repack
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const unsigned w = dsel(q, e);
+      unsigned l0 = (w & 0x000F000Fu) | DQ_MAGIC, l1 = ((w >> 8) & 0x000F000Fu) | DQ_MAGIC;
+      unsigned g0 = ((w >> 4) & 0x000F000Fu) | DQ_MAGIC, g1 = ((w >> 12) & 0x000F000Fu) | DQ_MAGIC;
+      if constexpr (QT == QT_Q5_K) {  // 5th bit of weight 4e + j: byte j of H, bit e (lo) / 4 + e (hi)
+        const unsigned H = R.e;
+        l0 |= (H << (4 - e)) & 0x00100010u;
+        l1 |= (H >> (4 + e)) & 0x00100010u;
+        g0 |= (H >> e) & 0x00100010u;
+        g1 |= (H >> (8 + e)) & 0x00100010u;
+      }
+      o[2 * e] = dq2(l0, off, S0, C0);
+      o[2 * e + 1] = dq2(l1, off, S0, C0);
+      o[8 + 2 * e] = dq2(g0, off, S1, C1);
+      o[8 + 2 * e + 1] = dq2(g1, off, S1, C1);
+    }
+  } else if constexpr (QT == QT_Q6_K) {
+    const int n = t >> 2, sub = t & 3;
+    const float d = h2f((uint16_t)R.e);
+    // int8 scales 8 n + sub (lo codes) and 8 n + sub + 4 (hi codes): dwords 2 n / 2 n + 1, byte sub
+    const unsigned mlo = n ? R.m.z : R.m.x, mhi = n ? R.m.w : R.m.y;
+    const float slo = d * (float)(int8_t)((mlo >> (8 * sub)) & 0xFF);
+    const float shi = d * (float)(int8_t)((mhi >> (8 * sub)) & 0xFF);
+    const dh2 off = dq_splat(1056.f), S0 = dq_splat(slo), S1 = dq_splat(shi), z = dq_splat(0.f);  // 1024 + 32
+    const unsigned H0 = R.h.x, H1 = R.h.y;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const unsigned q = dsel(R.a, e);
+      // high 2 bits of weight 4e + j: byte j, bits 2e..2e+1 of H0 (lo) / H1 (hi) -> bits 4..5
+      const int sl = 4 - 2 * e;
+      const unsigned hl0 = (sl >= 0 ? (H0 << sl) : (H0 >> -sl)) & 0x00300030u;
+      const unsigned hl1 = (H0 >> (4 + 2 * e)) & 0x00300030u;
+      const unsigned hh0 = (sl >= 0 ? (H1 << sl) : (H1 >> -sl)) & 0x00300030u;
+      const unsigned hh1 = (H1 >> (4 + 2 * e)) & 0x00300030u;
+      o[2 * e] = dq2((q & 0x000F000Fu) | hl0 | DQ_MAGIC, off, S0, z);
+      o[2 * e + 1] = dq2(((q >> 8) & 0x000F000Fu) | hl1 | DQ_MAGIC, off, S0, z);
+      o[8 + 2 * e] = dq2(((q >> 4) & 0x000F000Fu) | hh0 | DQ_MAGIC, off, S1, z);
+      o[8 + 2 * e + 1] = dq2(((q >> 12) & 0x000F000Fu) | hh1 | DQ_MAGIC, off, S1, z);
+    }
+  } else if constexpr (QT == QT_Q4_0) {
+    const dh2 sd = dq_splat(h2f((uint16_t)R.e)), z = dq_splat(0.f), off = dq_splat(1032.f);  // 1024 + 8
+    const u32x4 q = R.a ^ 0x80808080u;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const unsigned w = dsel(q, e);
+      o[2 * e] = dq2((w & 0x000F000Fu) | DQ_MAGIC, off, sd, z);
+      o[2 * e + 1] = dq2(((w >> 8) & 0x000F000Fu) | DQ_MAGIC, off, sd, z);
+      o[8 + 2 * e] = dq2(((w >> 4) & 0x000F000Fu) | DQ_MAGIC, off, sd, z);
+      o[8 + 2 * e + 1] = dq2(((w >> 12) & 0x000F000Fu) | DQ_MAGIC, off, sd, z);
+    }
+  } else {  // Q8_0: bytes are offset-binary after ^ 0x80
+    const dh2 sd = dq_splat(h2f((uint16_t)R.e)), z = dq_splat(0.f), off = dq_splat(1152.f);  // 1024 + 128
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const unsigned qa = dsel(R.a, e), qb = dsel(R.b, e);
+      o[2 * e] = dq2(((qa & 0x00FF00FFu) | DQ_MAGIC) ^ 0x00800080u, off, sd, z);
+      o[2 * e + 1] = dq2((((qa >> 8) & 0x00FF00FFu) | DQ_MAGIC) ^ 0x00800080u, off, sd, z);
+      o[8 + 2 * e] = dq2(((qb & 0x00FF00FFu) | DQ_MAGIC) ^ 0x00800080u, off, sd, z);
+      o[8 + 2 * e + 1] = dq2((((qb >> 8) & 0x00FF00FFu) | DQ_MAGIC) ^ 0x00800080u, off, sd, z);
+    }
+  }
+}
+
+// C fragment -> fused epilogue: weight row n = nb + 16 j, token row = mb + 16 i + r; the row pair
+// partner n ^ 1 sits on the adjacent lane
+template <int E, int TM, int TN>
+__device__ __forceinline__ void dq_out(const GemvParams& P, const f32x4 (&acc)[TM][TN], int mb, int nb, int M, int N) {
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float v = acc[i][j][r];
+        const float pv = __shfl_xor(v, 1);
+        const int gm = mb + 16 * i + r, gn = nb + 16 * j;
+        if (gm < M && gn < N) epi_apply_t<E>(P, gm, gn + P.row_offset, v, pv, 0);
+      }
+}
+
+// ------------------------------------------------------------------------------------------------
+template <int QT, int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__(DQ_NT, 1) void dq_gemm_kernel(GemvParams P, const f16* __restrict__ X, int Kp, int mt,
+                                                           int sk) {
+  static_assert(WM * WN == 8, "8 waves");
+  constexpr int TM = BM / WM / 16, TN = BN / WN / 16;  // 16 x 16 accumulator tiles per wave
+  constexpr int XS = BM * DQ_LDR, WS = BN * DQ_LDR;    // halves per LDS buffer
+  constexpr int XL = BM / 64;                          // 16-B X chunks per thread per K step
+  static_assert(TM >= 1 && TN >= 1 && BN * 2 <= DQ_NT && XL >= 1, "tile shape");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  f16* Xs = (f16*)smem;  // [2][BM][LDR]
+  f16* Ws = Xs + 2 * XS;  // [2][BN][LDR]
+
+  const QMat& w = P.w;
+  const int M = P.B, N = w.N, SB = Kp >> 8, nks = SB * 4;
+  // XCD-aware bijective remap: the blocks one XCD runs are a contiguous range of (tile, split) ids
+  const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int z = wg % sk, tile = wg / sk;
+  const int m0 = (tile % mt) * BM, n0 = (tile / mt) * BN;
+  const int ks0 = (int)((long long)z * nks / sk), ks1 = (int)((long long)(z + 1) * nks / sk);
+
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  // staging roles: X chunk (row xr + 64 i, 16 B at column xc), W piece (row wr, piece 2 ks + wh)
+  const int xr = tid >> 3, xc = tid & 7;
+  const int wr = tid >> 1, wh = tid & 1;
+  const bool wact = wr < BN;
+  const long long wrow = min(n0 + wr, N - 1);
+  const f16* xsrc[XL];
+#pragma unroll
+  for (int i = 0; i < XL; ++i) xsrc[i] = X + (long long)min(m0 + xr + 64 * i, M - 1) * Kp + 8 * xc;
+
+  u32x4 xreg[XL];
+  Piece<QT> wreg;
+  auto issue = [&](int ks) {
+#pragma unroll
+    for (int i = 0; i < XL; ++i) xreg[i] = *(const u32x4*)(xsrc[i] + ks * DQ_BK);
+    if (wact) load_piece<QT>(w, wrow, SB, 2 * ks + wh, wreg);
+  };
+  auto stage = [&](int ks, int buf) {
+    f16* xd = Xs + buf * XS;
+#pragma unroll
+    for (int i = 0; i < XL; ++i) *(u32x4*)(xd + (xr + 64 * i) * DQ_LDR + 8 * xc) = xreg[i];
+    if (wact) {
+      unsigned o[16];
+      dq_piece<QT>(wreg, (2 * ks + wh) / SB, o);
+      f16* wd = Ws + buf * WS + wr * DQ_LDR + 32 * wh;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) *(u32x4*)(wd + 8 * i) = (u32x4){o[4 * i], o[4 * i + 1], o[4 * i + 2], o[4 * i + 3]};
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int wm = wave / WN, wn = wave % WN;
+  const int fr = lane & 15, fk = 8 * (lane >> 4);
+  auto compute = [&](int buf) {
+    const f16* xb = Xs + buf * XS + (wm * (BM / WM) + fr) * DQ_LDR + fk;
+    const f16* wb = Ws + buf * WS + (wn * (BN / WN) + fr) * DQ_LDR + fk;
+#pragma unroll
+    for (int kk = 0; kk < DQ_BK / 32; ++kk) {
+      f16x8 a[TM], b[TN];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) b[j] = *(const f16x8*)(wb + j * 16 * DQ_LDR + 32 * kk);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) a[i] = *(const f16x8*)(xb + i * 16 * DQ_LDR + 32 * kk);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  issue(ks0);
+  stage(ks0, 0);
+  if (ks0 + 1 < ks1) issue(ks0 + 1);
+  for (int ks = ks0; ks < ks1; ++ks) {
+    const int cur = (ks - ks0) & 1;
+    __syncthreads();  // step ks staged by every thread; the other buffer's reads (step ks - 1) done
+    if (ks + 1 < ks1) {
+      stage(ks + 1, cur ^ 1);
+      if (ks + 2 < ks1) issue(ks + 2);
+    }
+    compute(cur);
+  }
+
+  // C fragment: weight row n = lane & 15 (+ 16 j), token row = 4 (lane >> 4) + r (+ 16 i)
+  const int nb = n0 + wn * (BN / WN) + fr;
+  const int mb = m0 + wm * (BM / WM) + 4 * (lane >> 4);
+  if (sk > 1) {
+    float* slab = P.gws + (long long)z * M * N;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int gm = mb + 16 * i + r, gn = nb + 16 * j;
+          if (gm < M && gn < N) __builtin_nontemporal_store(acc[i][j][r], slab + (long long)gm * N + gn);
+        }
+    return;
+  }
+  switch (P.epi) {  // one epilogue kind per unrolled body (the generic switch x 128 outputs spills)
+    case EPI_STORE: dq_out<EPI_STORE, TM, TN>(P, acc, mb, nb, M, N); break;
+    case EPI_ADD: dq_out<EPI_ADD, TM, TN>(P, acc, mb, nb, M, N); break;
+    case EPI_GELU: dq_out<EPI_GELU, TM, TN>(P, acc, mb, nb, M, N); break;
+    case EPI_GLU: dq_out<EPI_GLU, TM, TN>(P, acc, mb, nb, M, N); break;
+    case EPI_GEGLU: dq_out<EPI_GEGLU, TM, TN>(P, acc, mb, nb, M, N); break;
+    default: dq_out<EPI_QKV, TM, TN>(P, acc, mb, nb, M, N); break;
+  }
+}
+
+template <int BM, int BN>
+constexpr size_t dq_lds() { return (size_t)2 * (BM + BN) * DQ_LDR * sizeof(f16); }
+
+int g_dq_enable = -1;  // -1: OMX_GEMM_DQ (default on), read once
+
+}  // namespace
+
+bool dq_gemm_enabled() {
+  if (g_dq_enable < 0) {
+    const char* e = getenv("OMX_GEMM_DQ");
+    g_dq_enable = e ? atoi(e) != 0 : 1;
+  }
+  return g_dq_enable != 0;
+}
+
+void set_dq_gemm(int on) { g_dq_enable = on ? 1 : 0; }
+
+template <int QT, int BM, int BN, int WM, int WN>
+static void launch_dq(const GemvParams& P, const f16* xp, int Kp, int sk, hipStream_t s) {
+  const int mt = (P.B + BM - 1) / BM, nt = (P.w.N + BN - 1) / BN;
+  const size_t lds = dq_lds<BM, BN>();
+  hipLaunchKernelGGL((dq_gemm_kernel<QT, BM, BN, WM, WN>), dim3(mt * nt * sk), dim3(DQ_NT), lds, s, P, xp, Kp, mt, sk);
+}
+
+template <int QT>
+static void run_dq(const GemvParams& P, f16* xp, int Kp, hipStream_t s) {
+  hipLaunchKernelGGL(prep_xp_kernel<QT>, dim3(P.B), dim3(256), 0, s, P, xp, Kp);
+  const int M = P.B, N = P.w.N, nks = Kp / DQ_BK;
+  // tile: 256 x 256 when the grid fills the chip, else narrower N tiles, then 128-token M tiles
+  int cfg;
+  long long tiles;
+  auto ntl = [&](int bm, int bn) { return (long long)((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
+  if (M >= 256 && ntl(256, 256) >= 240) cfg = 0, tiles = ntl(256, 256);
+  else if (M >= 256) cfg = 1, tiles = ntl(256, 128);
+  else if (ntl(128, 256) >= 240) cfg = 2, tiles = ntl(128, 256);
+  else cfg = 3, tiles = ntl(128, 128);
+  int sk = 1;
+  if (P.gws && P.gws_elems > 0)
+    while (sk < 8 && tiles * sk < 240 && nks / (2 * sk) >= 8 && (long long)(2 * sk) * M * N <= P.gws_elems) sk *= 2;
+  switch (cfg) {
+    case 0: launch_dq<QT, 256, 256, 2, 4>(P, xp, Kp, sk, s); break;
+    case 1: launch_dq<QT, 256, 128, 4, 2>(P, xp, Kp, sk, s); break;
+    case 2: launch_dq<QT, 128, 256, 2, 4>(P, xp, Kp, sk, s); break;
+    default: launch_dq<QT, 128, 128, 2, 4>(P, xp, Kp, sk, s); break;
+  }
+  if (sk > 1) gemm_finalize(P, sk, s);
+}
+
+bool dq_gemm(const GemvParams& P, hipStream_t s) {
+  if (!dq_gemm_enabled() || P.B < 128 || !P.xws || P.expert_ids || P.moe_tiles) return false;
+  const int qt = P.w.qtype;
+  if (qt != QT_Q4_K && qt != QT_Q5_K && qt != QT_Q6_K && qt != QT_Q4_0 && qt != QT_Q8_0) return false;
+  const int Kp = ((P.w.K + 255) >> 8) * 256;
+  const long long cap = P.xws_elems ? P.xws_elems : (long long)P.B * P.w.K;
+  if ((long long)P.B * Kp > cap) return false;
+  f16* xp = (f16*)P.xws;
+  switch (qt) {
+    case QT_Q4_K: run_dq<QT_Q4_K>(P, xp, Kp, s); break;
+    case QT_Q5_K: run_dq<QT_Q5_K>(P, xp, Kp, s); break;
+    case QT_Q6_K: run_dq<QT_Q6_K>(P, xp, Kp, s); break;
+    case QT_Q4_0: run_dq<QT_Q4_0>(P, xp, Kp, s); break;
+    default: run_dq<QT_Q8_0>(P, xp, Kp, s); break;
+  }
+  return true;
+}
+
+}  // namespace omx

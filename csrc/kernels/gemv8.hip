@@ -22,60 +22,9 @@
 // The O projection keeps the deferred flash-decode merge input (IN_MERGE) and emits like down.
 // Reference parity: the decode GEMVs of llama.cpp inside `ollama/ollama` (reference
 // pkg/model/pod.go:10-12); numerics checked against an fp32 torch GEMV (tests/test_gemv8_gpu.py).
-#include "gemv_core.h"
+#include "gemv8_core.h"
 
 namespace omx {
-
-enum { IN_X8 = 0, IN_X8_RMS = 1, IN_MERGE = 2 };
-enum { EM_NONE = 0, EM_ADD = 1, EM_GLU = 2 };
-
-__device__ __forceinline__ int x8_slots_dev(int K) { return ((n_sb(K) * XPAD + 1) + 1) & ~1; }
-
-constexpr int X8_NWI = 3;   // 16-byte image words per thread (K <= 16384 at 256 threads x KS)
-constexpr int X8_NSTW = 2;  // f32x4 RMS partials per lane (K <= 8192)
-
-// quantise the 16 staged values of group G into the consumer image (one lane). WT: write-through (sc1)
-// dword stores -- the image is handed to another workgroup of the SAME launch (ffn8_kernel)
-template <bool WT = false>
-__device__ __forceinline__ void emit_group(void* img, int Kc, int G, const float* v, const float* sq,
-                                           float* stat) {
-  float amax = 0.f;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) amax = fmaxf(amax, fabsf(v[i]));
-  const float d = amax / 127.f, id = amax > 0.f ? 127.f / amax : 0.f;
-  int qsum = 0;
-  i32x4 pk;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    int word = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int q = (int)rintf(v[4 * j + k] * id);
-      qsum += q;
-      word |= (q & 0xFF) << (8 * k);
-    }
-    pk[j] = word;
-  }
-  const int XSP = x8_slots_dev(Kc);
-  const int slot = (G >> 4) * XPAD + (G & 15);
-  if constexpr (WT) {
-    unsigned* q = (unsigned*)img + 4 * slot;
-    unsigned* f = (unsigned*)((char*)img + (size_t)XSP * 16) + 2 * slot;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) __hip_atomic_store(q + j, (unsigned)pk[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(f, __float_as_uint(d), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(f + 1, __float_as_uint(d * (float)qsum), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  } else {
-    ((i32x4*)img)[slot] = pk;
-    ((f32x2*)((char*)img + (size_t)XSP * 16))[slot] = (f32x2){d, d * (float)qsum};
-  }
-  if (stat) {
-    float ss = 0.f;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) ss += sq[i];
-    stat[G] = ss;
-  }
-}
 
 // One block = KS groups of 4 waves on the same 16-row tiles (group kg owns super-blocks
 // [kg * CH, (kg + 1) * CH)); J consecutive tiles per block, every weight load issued up front.
@@ -295,37 +244,6 @@ __global__ __launch_bounds__(GEMV_NT) void qgemv8_dual_kernel(GemvParams PA, Gem
 // loads after its poll matched, the other waves after the barrier it joins; every byte stored and
 // loaded sc1). Deadlock freedom: waiting blocks never exceed the grid's residency minus the other
 // blocks' slots (host check), and a wait gives up after 2 ms (error word; the runner raises).
-struct Handoff {
-  unsigned* count;  // phase-A arrivals
-  unsigned* done;   // phase-B passes; the last one re-arms both (the next launch starts from zero)
-  int* err;         // 1: a wait timed out (results of that step are invalid)
-  int n_prod, n_cons;
-};
-
-__device__ __forceinline__ void handoff_arrive(const Handoff& H) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its sc1 stores are done
-  __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_fetch_add(H.count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__device__ __forceinline__ void handoff_wait(const Handoff& H) {
-  if (threadIdx.x == 0) {
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
-    while (__hip_atomic_load(H.count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)H.n_prod) {
-      if (__builtin_amdgcn_s_memrealtime() - t0 > 200000ull) {  // 2 ms: never in a healthy step
-        __hip_atomic_store(H.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-    if (__hip_atomic_fetch_add(H.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)H.n_cons - 1) {
-      __hip_atomic_store(H.count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(H.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  __syncthreads();
-}
-
 constexpr int FFN_IMG_DW = 20;  // image dwords per thread (K <= 13568 at 256 threads)
 
 // phase B: one 16-row down tile, input image handed off in this launch, EPI_ADD + emission

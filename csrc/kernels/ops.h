@@ -105,6 +105,11 @@ bool gemv8_supported(const GemvParams& P);
 // gate_up (G: EPI_GLU, emits D's image) -> down (D: EPI_ADD) in one launch with an in-kernel hand-off;
 // sync: 16 zeroed ints of device memory (counters + error word); false = not covered (two launches)
 bool gemv8_ffn(const GemvParams& G, const GemvParams& D, void* sync, hipStream_t s);
+struct AttnParams;
+// QKV (A: q,k rows or all rows; B: v rows or B.w.s0 null) + paged attention + O projection (O.x8 = the
+// attention image, EPI_ADD + emission) in one launch (attn8.hip); false = not covered
+bool attn8(const GemvParams& A, const GemvParams& B, const GemvParams& O, const AttnParams& At, void* sync,
+           hipStream_t s);
 
 // y = epi(W x): the quantised GEMV for small B (decode), the MFMA dequant GEMM for B >= GEMM_MIN_B
 // when an fp16 activation workspace is given (prefill); same epilogues either way.
@@ -138,6 +143,11 @@ size_t mfma_layout_bytes(int qtype, int N, int K);  // 0 = no layout M for this 
 void repack_m(const QMat& w, void* out, hipStream_t s);
 bool gemm_eligible(const GemvParams& P);
 void gemm(const GemvParams& P, hipStream_t s);
+// stream-order dequant MFMA GEMM (gemm_dq.hip): M >= 128, dense v2 matrices; false = not covered
+bool dq_gemm(const GemvParams& P, hipStream_t s);
+bool dq_gemm_enabled();
+void set_dq_gemm(int on);
+void gemm_finalize(const GemvParams& P, int sk, hipStream_t s);  // sums sk split-K slabs + epilogue
 
 // launch-shape knobs for the decode GEMV (tuned on MI355X; see scripts/bench_gemv.py)
 struct GemvTuning {

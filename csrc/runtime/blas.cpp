@@ -56,11 +56,17 @@ void destroy(Plan& p) {
   p = Plan{};
 }
 
+// M buckets: 128, 256, then every multiple of 256. A prompt of M rows runs its bucket's plan over
+// padded rows whenever the caller's buffers hold them (no exact-M query: hipBLASLt's algorithm check
+// cost ~0.3 s on its first call per shape, which landed in the first TTFT of every new burst size --
+// the 4-client bench's ~0.4 s stall); at most 255 padded rows past 256.
 int bucket_of(int M) {
-  int b = 128;
-  while (b < M) b <<= 1;
-  return b;
+  if (M <= 128) return 128;
+  if (M <= 256) return 256;
+  return (M + 255) / 256 * 256;
 }
+
+int next_bucket(int b) { return b < 256 ? b * 2 : b + 256; }
 
 bool layouts(Plan& p, int M, int N, int K) {
   if (hipblasLtMatmulDescCreate(&p.op, HIPBLAS_COMPUTE_32F, HIP_R_32F) != HIPBLAS_STATUS_SUCCESS) return false;
@@ -127,6 +133,10 @@ Plan plan_for(hipblasLtHandle_t h, int dev, int M, int N, int K, size_t ws_bytes
   if (M == Mb) {
     p = bt->second;
     p.m_run = Mb;
+  } else if (bt->second.ok && m_cap >= Mb) {  // padded rows: the bucket's plan as is (not cached: m_cap)
+    Plan q = bt->second;
+    q.m_run = Mb;
+    return q;
   } else if (bt->second.ok && !g_rejected.count(key) && layouts(p, M, N, K)) {
     hipblasLtMatmulAlgo_t algo = bt->second.algo;
     size_t need = 0;
@@ -197,7 +207,7 @@ void blas_prepare(int N, int K, int min_M, int max_M, size_t ws_bytes) {
   std::lock_guard<std::mutex> lk(g_mu);
   hipblasLtHandle_t h = handle(dev);
   if (!h) return;
-  for (int Mb = bucket_of(min_M); Mb <= bucket_of(max_M); Mb <<= 1) (void)plan_for(h, dev, Mb, N, K, ws_bytes, 0);
+  for (int Mb = bucket_of(min_M); Mb <= bucket_of(max_M); Mb = next_bucket(Mb)) (void)plan_for(h, dev, Mb, N, K, ws_bytes, 0);
 }
 
 }  // namespace omx

@@ -160,6 +160,42 @@ void Executor::attn_block(int i, const StepInputs& in, hipStream_t s) {
   const bool q8 = x8(in);
   if (ch && i > 0) chain_in(P, ws.xa16, ws.ld_e, ws.st[1], (E + 15) / 16);  // emitted by layer i-1's down
   if (q8 && i > 0) x8_in(P, ws.x8e, ws.x8st);                                 // emitted by layer i-1's down
+  if (q8 && i > 0 && ws.attn_fuse && ws.x8q && !phi) {  // QKV + attention + O in one launch (attn8.hip)
+    GemvParams V{};
+    if (!L.qkv_fused) {
+      V = P;
+      V.w = L.wv;
+      V.row_offset = Eq + Ekv;
+    }
+    GemvParams O = base_params(L.wo, B, ws.abuf, Eq, ws);
+    O.bias = L.bo;
+    O.epi = EPI_ADD;
+    O.y = ws.resid;
+    O.ldy = E;
+    x8_in(O, ws.x8q, nullptr);
+    x8_emit(O, ws.x8e, L.ffn_norm, ws.x8st);
+    AttnParams A{};
+    A.q = ws.qbuf;
+    A.ldq = Eq;
+    A.kc = L.kc;
+    A.vc = L.vc;
+    A.block_table = in.block_table;
+    A.max_blocks = in.max_blocks;
+    A.q_seq = in.q_seq;
+    A.q_len = in.q_len;
+    A.NQ = B;
+    A.H = cfg.H;
+    A.n_kv = cfg.Hkv;
+    A.D = cfg.Dc > 0 ? cfg.Dc : cfg.D;
+    A.Dv = cfg.D;
+    A.bs = in.bs;
+    A.scale = 1.0f / std::sqrt((float)cfg.D);
+    A.window = cfg.window;
+    if (attn8(P, V, O, A, ws.x8sync, s)) {
+      ++n_attn8;
+      return;
+    }
+  }
   if (!L.qkv_fused) {  // q,k and v rows of different quant types: one dual launch at B == 1
     GemvParams V = P;
     V.w = L.wv;
@@ -377,7 +413,10 @@ void Executor::ffn_block(int i, const StepInputs& in, hipStream_t s) {
   if (q8) {
     x8_in(Dn, ws.x8f, nullptr);
     x8_emit(Dn, ws.x8e, i + 1 < (int)layers.size() ? layers[i + 1].attn_norm : out_norm, ws.x8st);
-    if (ws.x8_fuse && gemv8_ffn(G, Dn, ws.x8sync, s)) return;  // one launch, in-kernel hand-off
+    if (ws.x8_fuse && gemv8_ffn(G, Dn, ws.x8sync, s)) {  // one launch, in-kernel hand-off
+      ++n_ffn8;
+      return;
+    }
   }
   gemv(G, s);
   gemv(Dn, s);

@@ -98,8 +98,8 @@ class NativeExec:
         b = getattr(r, "x8_bufs", None)
         if not b:
             return {}
-        return dict(x8e=b["x8e"].data_ptr(), x8f=b["x8f"].data_ptr(), x8st=b["x8st"].data_ptr(),
-                    x8sync=b["x8sync"].data_ptr(), x8_ok=1, x8_fuse=int(os.environ.get("OMX_X8_FUSE", "1") != "0"))
+        return dict(x8e=b["x8e"].data_ptr(), x8f=b["x8f"].data_ptr(), x8st=b["x8st"].data_ptr(), x8q=b["x8q"].data_ptr(),
+                    x8sync=b["x8sync"].data_ptr(), x8_ok=1, x8_fuse=int(os.environ.get("OMX_X8_FUSE", "0") != "0"))
 
     def ar_fits(self, B: int) -> bool:
         return self.exe.ar_fits(B)
@@ -107,7 +107,10 @@ class NativeExec:
     def run(self, stage: str, layer: int, B: int, n_logits: int = 0, use_idx: bool = False,
             prefill: bool = False):
         S, defer = self.r.split_plan(B)
-        self.exe.set_splits(S, defer)
+        # batch-1 decode over <= 512 keys: QKV + attention + O in one launch (attn8.hip), when the
+        # executor covers the shapes (it falls back to the split attention kernel otherwise)
+        fuse = int(B == 1 and self.r._decode_S in (1, 2, 4) and self.r.attn_fuse)
+        self.exe.set_splits(S, defer, fuse)
         self.exe.step(self.stages[stage], layer, B, n_logits, use_idx, prefill, stream_handle() if self.on_gpu else 0)
 
 
@@ -195,12 +198,15 @@ class Runner:
                                 st1=torch.zeros((E + 15) // 16 * 16, **f32))
         # batch-1 int8 activation chain (csrc/kernels/gemv8.hip): zeroed images (pad slots stay zero)
         self.x8_bufs = None
+        self.attn_fuse = False
         if self.is_gpu and os.environ.get("OMX_X8", "1") != "0":
             C = native()
             u8 = dict(device=dev, dtype=torch.uint8)
             self.x8_bufs = dict(x8e=torch.zeros(C.x8_bytes(E), **u8), x8f=torch.zeros(C.x8_bytes(Fl), **u8),
                                 x8st=torch.zeros((E + 15) // 16 + 4, **f32),
-                                x8sync=torch.zeros(16, device=dev, dtype=torch.int32))
+                                x8q=torch.zeros(C.x8_bytes(Eq), **u8),
+                                x8sync=torch.zeros(128, device=dev, dtype=torch.int32))
+        self.attn_fuse = os.environ.get("OMX_ATTN_FUSE", "0") != "0"
         # MoE prefill grouping (csrc/kernels/moe.hip moe_sort -> grouped MFMA GEMM)
         n_pairs = max_batch * ksel
         self.moe_rows = torch.zeros(n_pairs, **i32)
@@ -213,10 +219,11 @@ class Runner:
         self._ext_next = 0
         # split-K partial slabs of small-M prefill GEMMs (the kernel picks splits that fit)
         self.gws = torch.zeros(GEMM_SPLIT_WS_FLOATS if str(dev).startswith("cuda") else 1, **f32)
-        # large-M prefill on hipBLASLt (gemm.hip gemm_lib): fp16 dequantised-weight scratch sized for the
-        # largest dense layer matrix and its fp32 output slab at max_batch rows (OMX_GEMM_LIB=0: off)
+        # hipBLASLt prefill (gemm.hip gemm_lib), only when asked for (OMX_GEMM_LIB_MIN_M > 0: the A/B
+        # baseline of the hand-written stream-order GEMM, gemm_dq.hip): fp16 dequantised-weight scratch
+        # sized for the largest dense layer matrix and its fp32 output slab at max_batch rows
         self.w16 = self.yws = None
-        if self.is_gpu and os.environ.get("OMX_GEMM_LIB", "1") != "0" and max_batch >= 16:
+        if self.is_gpu and native().gemm_lib_min_m() > 0 and max_batch >= 16:
             # expert stacks count per expert (DevQMat.N = rows of one expert): moe_gemm_lib
             mats = [v for L in self.w.layers for k, v in L.items() if isinstance(v, DevQMat) and k != "router"]
             if mats:
@@ -581,9 +588,9 @@ class Runner:
         lens = [min(self.max_batch, 32)]
         if self.w16 is not None and native().gemm_lib_min_m() > 0:
             m = native().gemm_lib_min_m()
-            while m <= min(self.max_batch, self.ctx - 1):
+            while m <= min(self.max_batch, self.ctx - 1):  # every hipBLASLt M bucket (blas.cpp bucket_of)
                 lens.append(m)
-                m *= 2
+                m = m * 2 if m < 256 else m + 256
         V = self.cfg.n_vocab
         toks = lambda n, k=0: [self.cfg.bos_id] + [3 + (i * 7919 + k) % max(1, V - 3) for i in range(n - 1)]  # noqa: E731
         for n in lens:  # varied tokens: MoE routing spreads over the experts (per-expert row buckets)
@@ -656,7 +663,7 @@ class Runner:
         """Nonzero when an in-launch hand-off of the int8 chain timed out (gemv8.hip ffn8_kernel): the
         step's results are invalid. Reads device memory (a sync)."""
         b = self.x8_bufs
-        return int(b["x8sync"][2].item()) if b else 0
+        return int(b["x8sync"][2].item() or b["x8sync"][16 + 66].item()) if b else 0
 
     def set_tokens(self, tokens: list[int]) -> None:
         """Host -> d_tokens[:len(tokens)] (batch recomposition: rows' next inputs)."""

@@ -201,6 +201,11 @@ PRESETS: dict[str, ModelConfig] = {
                               norm_eps=1e-6, ctx_len=256, bos_id=2, eos_id=1),
     "tiny-llama": ModelConfig(name="tiny-llama", n_vocab=512, n_embd=256, n_layer=2, n_head=4,
                               n_head_kv=2, n_ff=512, n_rot=64, ctx_len=256),
+    # head dim 128 (the fused batch-1 attention half, attn8.hip): MHA and GQA 4
+    "tiny-llama-d128": ModelConfig(name="tiny-llama-d128", n_vocab=512, n_embd=512, n_layer=3, n_head=4,
+                                   n_head_kv=4, n_ff=768, n_rot=128, ctx_len=512),
+    "tiny-llama-d128-gqa": ModelConfig(name="tiny-llama-d128-gqa", n_vocab=512, n_embd=512, n_layer=3, n_head=4,
+                                       n_head_kv=1, n_ff=768, n_rot=128, ctx_len=512),
     # head dim 100 (Orca Mini), E not a multiple of 256: Q4_0 / Q8_0 files
     "tiny-orca": ModelConfig(name="tiny-orca", n_vocab=512, n_embd=800, n_layer=2, n_head=8, n_head_kv=8,
                              n_ff=2176, n_rot=100, ctx_len=256),

@@ -1,7 +1,8 @@
-"""Prefill GEMM microbenchmark, fused MFMA dequant GEMM (csrc/kernels/gemm.hip) vs the hipBLASLt path
-(dequant to fp16 + library GEMM + epilogue; csrc/runtime/blas.cpp) on Llama-2-7B Q4_K_M shapes:
-time per call and achieved TFLOP/s vs M (prompt tokens). Run on the GPU box:
-  python scripts/bench_gemm.py            (OMX_BENCH_SHAPES / OMX_BENCH_M filter for PMC runs)"""
+"""Prefill GEMM microbenchmark on Llama-2-7B Q4_K_M shapes: the stream-order dequant GEMM
+(csrc/kernels/gemm_dq.hip, "dq", the default), the 128 x 128 natural-order tile (gemm.hip, "tile") and
+the hipBLASLt path (prep + dequant to fp16 + library GEMM + epilogue pass; csrc/runtime/blas.cpp):
+time per call (everything the path launches) and TFLOP/s vs M (prompt tokens). On the GPU box:
+  python scripts/bench_gemm.py   (OMX_BENCH_SHAPES / OMX_BENCH_M / OMX_BENCH_PATHS filter, e.g. for PMC runs)"""
 import os
 import sys
 
@@ -33,15 +34,19 @@ def main():
         for M in ms:
             x = torch.randn(M, K, device="cuda")
             y = torch.zeros(M, N, device="cuda")
-            xws = torch.empty(M * K, device="cuda", dtype=torch.float16)
+            xws = torch.empty(M * ((K + 255) // 256 * 256), device="cuda", dtype=torch.float16)
             gws = torch.empty(8 << 20, device="cuda")  # the runner's split-K workspace
             w16 = torch.empty(N * K, device="cuda", dtype=torch.float16)
             yws = torch.empty(M * N, device="cuda")
-            ws = {"xws": xws.data_ptr(), "gws": gws.data_ptr(), "gws_elems": gws.numel(), "w16ws": w16.data_ptr(),
+            ws = {"xws": xws.data_ptr(), "xws_elems": xws.numel(), "gws": gws.data_ptr(), "gws_elems": gws.numel(), "w16ws": w16.data_ptr(),
                   "w16_elems": w16.numel(), "yws": yws.data_ptr(), "yws_elems": yws.numel()}
             fn = lambda: C.gemv(tup, M, x.data_ptr(), K, 0, 0, 0, 1e-5, 0, y.data_ptr(), N, 0, 0, ws, s)  # noqa: E731
-            for path, min_m in (("fused", 0), ("hipblaslt", 1)):
+            paths = os.environ.get("OMX_BENCH_PATHS", "dq,tile,hipblaslt").split(",")
+            for path, min_m, dq in (("dq", 0, 1), ("tile", 0, 0), ("hipblaslt", 1, 0)):
+                if path not in paths:
+                    continue
                 C.set_gemm_lib_min_m(min_m)
+                C.set_dq_gemm(dq)
                 for _ in range(3):
                     fn()
                 torch.cuda.synchronize()

@@ -77,6 +77,28 @@ def test_prefill_gemm_path_vs_torch(tiny_models, name):
     assert rel(g.logits[0, :V].cpu(), c.logits[0, :V]) < 3e-2
 
 
+@pytest.mark.parametrize("name", ["tiny-llama", "tiny-mixtral", "tiny-phi2", "tiny-llama-q8", "tiny-llama-q40",
+                                  "tiny-llama-q5km", "tiny-gemma", "tiny-orca"])
+def test_prefill_dq_path_vs_torch(tiny_models, name):
+    """Prompts >= 128 tokens take the stream-order dequant GEMM (gemm_dq.hip) for every dense matrix:
+    logits must match the torch twin, before and after a decode step on the KV it wrote."""
+    C = native()
+    assert C.dq_gemm_enabled() and C.gemm_lib_min_m() == 0
+    path = tiny_models[name]
+    g = Runner(path, device="cuda", max_batch=256, max_seqs=2, ctx=256)
+    c = Runner(path, device="cpu", max_batch=256, max_seqs=2, ctx=256)
+    rng = np.random.default_rng(4)
+    toks = [1] + [int(x) for x in rng.integers(3, 500, 229)]
+    sg, sc = g.new_sequence(), c.new_sequence()
+    g.prefill(sg, toks)
+    c.prefill(sc, toks)
+    V = g.cfg.n_vocab
+    assert rel(g.logits[0, :V].cpu(), c.logits[0, :V]) < 3e-2
+    g.prefill(sg, [5])
+    c.prefill(sc, [5])
+    assert rel(g.logits[0, :V].cpu(), c.logits[0, :V]) < 3e-2
+
+
 @pytest.mark.parametrize("name", ["tiny-llama", "tiny-mixtral", "tiny-gemma", "tiny-phi2"])
 def test_prefill_library_path_vs_torch(tiny_models, name):
     """The hipBLASLt prefill path (gemm.hip gemm_lib; for Mixtral per-expert GEMMs over the sorted
