@@ -121,10 +121,15 @@ __global__ __launch_bounds__(ATT_NT) void attn_decode_kernel(AttnParams P) {
 #pragma unroll
   for (int g = 0; g < G; ++g) {
     const float* qp = P.q + (long long)qi * P.ldq + (h0 + g) * Dv;
+    if (Dv == D) {  // unpadded head: plain loads (a per-element select makes hipcc wait per load)
 #pragma unroll
-    for (int j = 0; j < DPL; ++j) {
-      const int d = li * DPL + j;
-      q[g][j] = d < Dv ? qp[min(d, Dv - 1)] * P.scale : 0.f;  // padded K dims never contribute
+      for (int j = 0; j < DPL; ++j) q[g][j] = qp[li * DPL + j] * P.scale;
+    } else {
+#pragma unroll
+      for (int j = 0; j < DPL; ++j) {
+        const int d = li * DPL + j;  // clamped load, then zero: padded K dims never contribute
+        q[g][j] = qp[min(d, Dv - 1)] * (d < Dv ? P.scale : 0.f);
+      }
     }
   }
   float m[G], l[G], acc[G][DPL];

@@ -14,7 +14,8 @@
 //    then one v_pk_add (remove 1024) + one v_pk_fma (scale, zero point) -- ~2.5 VALU per 2 weights,
 //    paid once per weight per 256-token M tile (the decode GEMVs pay it once per token).
 //  * Block tile BM (tokens) x BN (weight rows) x 64 K, 8 waves (WM x WN), each a (BM/WM) x (BN/WN)
-//    sub-tile of `v_mfma_f32_16x16x32_f16` accumulators (128 fp32 per lane at 256 x 256). Both
+//    sub-tile of `v_mfma_f32_32x32x16_f16` accumulators (128 fp32 per lane at 256 x 256; the 32-row
+//    shape needs half the fragment registers per MFMA batch of the 16 x 16 one at the same rate). Both
 //    operands are staged in LDS as [rows][64 + 8] fp16: 144-B rows put the 16-B fragment reads of 16
 //    consecutive rows on distinct bank groups (conflict-free), and both A (X rows) and B (W rows) read
 //    "8 consecutive K of one row" per lane, so one image format serves both.
@@ -43,10 +44,15 @@ namespace {
 
 constexpr int DQ_NT = 512;        // 8 waves
 constexpr int DQ_BK = 64;         // K per step (two 32-code pieces per weight row)
-constexpr int DQ_LDR = DQ_BK + 8; // fp16 LDS row stride (144 B)
+// LDS operand image: [rows][64] fp16 (128-B rows), 16-B chunk c of row r at physical chunk
+// c ^ ((r >> 1) & 7): the fragment reads of 16 consecutive rows at one chunk then cover 16 distinct
+// bank slots (rows 2p, 2p + 1 share a chunk in opposite 128-B halves), and each wave's X DMA writes
+// whole rows lane-linearly (the swizzle is applied to the global source address instead)
+__device__ __forceinline__ int swz(int r, int c) { return r * 64 + 8 * (c ^ ((r >> 1) & 7)); }
 constexpr unsigned DQ_MAGIC = 0x64006400u;
 
 typedef _Float16 dh2 __attribute__((ext_vector_type(2)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
 __device__ __forceinline__ dh2 dq_h2(unsigned v) { return __builtin_bit_cast(dh2, v); }
 __device__ __forceinline__ unsigned dq_u(dh2 v) { return __builtin_bit_cast(unsigned, v); }
 __device__ __forceinline__ dh2 dq_splat(float f) { return (dh2){(f16)f, (f16)f}; }
@@ -231,19 +237,19 @@ __device__ __forceinline__ void dq_piece(const Piece<QT>& R, int t, unsigned (&o
   }
 }
 
-// C fragment -> fused epilogue: weight row n = nb + 16 j, token row = mb + 16 i + r; the row pair
-// partner n ^ 1 sits on the adjacent lane
+// C fragment -> fused epilogue: weight row n = nb + 32 j, token row = mb + 32 i + (r & 3) + 8 (r >> 2);
+// the row pair partner n ^ 1 sits on the adjacent lane
 template <int E, int TM, int TN>
-__device__ __forceinline__ void dq_out(const GemvParams& P, const f32x4 (&acc)[TM][TN], int mb, int nb, int M, int N) {
+__device__ __forceinline__ void dq_out(const GemvParams& P, const f32x16 (&acc)[TM][TN], int mb, int nb, int M, int N) {
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
+      for (int r = 0; r < 16; ++r) {
         const float v = acc[i][j][r];
         const float pv = __shfl_xor(v, 1);
-        const int gm = mb + 16 * i + r, gn = nb + 16 * j;
+        const int gm = mb + 32 * i + (r & 3) + 8 * (r >> 2), gn = nb + 32 * j;
         if (gm < M && gn < N) epi_apply_t<E>(P, gm, gn + P.row_offset, v, pv, 0);
       }
 }
@@ -253,8 +259,8 @@ template <int QT, int BM, int BN, int WM, int WN>
 __global__ __launch_bounds__(DQ_NT, 1) void dq_gemm_kernel(GemvParams P, const f16* __restrict__ X, int Kp, int mt,
                                                            int sk) {
   static_assert(WM * WN == 8, "8 waves");
-  constexpr int TM = BM / WM / 16, TN = BN / WN / 16;  // 16 x 16 accumulator tiles per wave
-  constexpr int XS = BM * DQ_LDR, WS = BN * DQ_LDR;    // halves per LDS buffer
+  constexpr int TM = BM / WM / 32, TN = BN / WN / 32;  // 32 x 32 accumulator tiles per wave
+  constexpr int XS = BM * DQ_BK, WS = BN * DQ_BK;      // halves per LDS buffer (128-B rows, swizzled)
   constexpr int XL = BM / 64;                          // 16-B X chunks per thread per K step
   static_assert(TM >= 1 && TN >= 1 && BN * 2 <= DQ_NT && XL >= 1, "tile shape");
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -263,6 +269,7 @@ __global__ __launch_bounds__(DQ_NT, 1) void dq_gemm_kernel(GemvParams P, const f
 
   const QMat& w = P.w;
   const int M = P.B, N = w.N, SB = Kp >> 8, nks = SB * 4;
+  const unsigned sbinv = (0xFFFFFFFFu / (unsigned)SB) + 1u;  // pc / SB = umulhi(pc, sbinv) for pc < 8 SB
   // XCD-aware bijective remap: the blocks one XCD runs are a contiguous range of (tile, split) ids
   const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
   const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
@@ -272,75 +279,104 @@ __global__ __launch_bounds__(DQ_NT, 1) void dq_gemm_kernel(GemvParams P, const f
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   // staging roles: X chunk (row xr + 64 i, 16 B at column xc), W piece (row wr, piece 2 ks + wh)
-  const int xr = tid >> 3, xc = tid & 7;
   const int wr = tid >> 1, wh = tid & 1;
-  const bool wact = wr < BN;
+  const bool wact = BN * 2 >= DQ_NT || wr < BN;  // compile-time true when every thread stages a piece
   const long long wrow = min(n0 + wr, N - 1);
+  // X rows by LDS DMA: wave w's i-th global_load_lds fills rows 64 i + 8 w .. + 7 (1 KiB, lane-linear);
+  // lane l lands in physical chunk l & 7 of its row, so it fetches the logical chunk that swizzles there
   const f16* xsrc[XL];
 #pragma unroll
-  for (int i = 0; i < XL; ++i) xsrc[i] = X + (long long)min(m0 + xr + 64 * i, M - 1) * Kp + 8 * xc;
+  for (int i = 0; i < XL; ++i) {
+    const int r = 64 * i + 8 * wave + (lane >> 3);
+    xsrc[i] = X + (long long)min(m0 + r, M - 1) * Kp + 8 * ((lane & 7) ^ ((r >> 1) & 7));
+  }
+  typedef __attribute__((address_space(3))) void lds_void;
+  typedef __attribute__((address_space(1))) void glb_void;
 
-  u32x4 xreg[XL];
   Piece<QT> wreg;
-  auto issue = [&](int ks) {
-#pragma unroll
-    for (int i = 0; i < XL; ++i) xreg[i] = *(const u32x4*)(xsrc[i] + ks * DQ_BK);
+  auto issue_w = [&](int ks) {
     if (wact) load_piece<QT>(w, wrow, SB, 2 * ks + wh, wreg);
   };
-  auto stage = [&](int ks, int buf) {
-    f16* xd = Xs + buf * XS;
+  auto issue_x = [&](int ks, int buf) {
 #pragma unroll
-    for (int i = 0; i < XL; ++i) *(u32x4*)(xd + (xr + 64 * i) * DQ_LDR + 8 * xc) = xreg[i];
+    for (int i = 0; i < XL; ++i)
+      __builtin_amdgcn_global_load_lds((glb_void*)(xsrc[i] + ks * DQ_BK), (lds_void*)(Xs + buf * XS + (64 * i + 8 * wave) * DQ_BK),
+                                       16, 0, 0);
+  };
+  auto stage_w = [&](int ks, int buf) {
     if (wact) {
+      const int pc = 2 * ks + wh;
       unsigned o[16];
-      dq_piece<QT>(wreg, (2 * ks + wh) / SB, o);
-      f16* wd = Ws + buf * WS + wr * DQ_LDR + 32 * wh;
+      dq_piece<QT>(wreg, (int)__umulhi((unsigned)pc, sbinv), o);  // t = pc / SB
+      f16* wd = Ws + buf * WS;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) *(u32x4*)(wd + 8 * i) = (u32x4){o[4 * i], o[4 * i + 1], o[4 * i + 2], o[4 * i + 3]};
+      for (int i = 0; i < 4; ++i)
+        *(u32x4*)(wd + swz(wr, 4 * wh + i)) = (u32x4){o[4 * i], o[4 * i + 1], o[4 * i + 2], o[4 * i + 3]};
     }
   };
 
-  f32x4 acc[TM][TN];
+  f32x16 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   const int wm = wave / WN, wn = wave % WN;
-  const int fr = lane & 15, fk = 8 * (lane >> 4);
+  const int fr = lane & 31, fq = lane >> 5;
   auto compute = [&](int buf) {
-    const f16* xb = Xs + buf * XS + (wm * (BM / WM) + fr) * DQ_LDR + fk;
-    const f16* wb = Ws + buf * WS + (wn * (BN / WN) + fr) * DQ_LDR + fk;
+    const f16* xb = Xs + buf * XS;
+    const f16* wb = Ws + buf * WS;
 #pragma unroll
-    for (int kk = 0; kk < DQ_BK / 32; ++kk) {
+    for (int kk = 0; kk < DQ_BK / 16; ++kk) {
       f16x8 a[TM], b[TN];
 #pragma unroll
-      for (int j = 0; j < TN; ++j) b[j] = *(const f16x8*)(wb + j * 16 * DQ_LDR + 32 * kk);
+      for (int j = 0; j < TN; ++j) b[j] = *(const f16x8*)(wb + swz(wn * (BN / WN) + 32 * j + fr, 2 * kk + fq));
 #pragma unroll
-      for (int i = 0; i < TM; ++i) a[i] = *(const f16x8*)(xb + i * 16 * DQ_LDR + 32 * kk);
+      for (int i = 0; i < TM; ++i) a[i] = *(const f16x8*)(xb + swz(wm * (BM / WM) + 32 * i + fr, 2 * kk + fq));
+      __builtin_amdgcn_s_setprio(1);  // T5: the MFMA cluster first while the other wave dequantises
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[i], b[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[i], b[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
     }
   };
 
-  issue(ks0);
-  stage(ks0, 0);
-  if (ks0 + 1 < ks1) issue(ks0 + 1);
-  for (int ks = ks0; ks < ks1; ++ks) {
-    const int cur = (ks - ks0) & 1;
-    __syncthreads();  // step ks staged by every thread; the other buffer's reads (step ks - 1) done
-    if (ks + 1 < ks1) {
-      stage(ks + 1, cur ^ 1);
-      if (ks + 2 < ks1) issue(ks + 2);
-    }
-    compute(cur);
+  // Two K steps per trip with literal buffer indices and no branches in between: the compiler sees the
+  // staging writes (other buffer) and the fragment reads (this buffer) as disjoint, so it can interleave
+  // the dequant VALU / LDS writes of step ks + 1 with the MFMAs of step ks. Order inside a step: the
+  // dequant consumes the weight registers BEFORE the X DMA is issued (hipcc would otherwise wait for
+  // the DMA at the first use of an ordinary load), the weight loads of step ks + 2 follow, and the wait
+  // hipcc places before the next barrier retires both. Steps past the end are clamped to the last one
+  // (a redundant load / a write into the buffer nobody reads again).
+  const int kl = ks1 - 1;
+  issue_w(ks0);
+  stage_w(ks0, 0);
+  issue_x(ks0, 0);
+  issue_w(min(ks0 + 1, kl));
+  int ks = ks0;
+  for (; ks + 1 < ks1; ks += 2) {
+    __syncthreads();  // buffer 0 holds step ks; buffer 1's readers (step ks - 1) are done
+    stage_w(ks + 1, 1);
+    issue_x(ks + 1, 1);
+    issue_w(min(ks + 2, kl));
+    compute(0);
+    __syncthreads();  // buffer 1 holds step ks + 1; buffer 0's readers are done
+    stage_w(min(ks + 2, kl), 0);
+    issue_x(min(ks + 2, kl), 0);
+    issue_w(min(ks + 3, kl));
+    compute(1);
+  }
+  if (ks < ks1) {  // odd step count: the last step sits in buffer 0
+    __syncthreads();
+    compute(0);
   }
 
-  // C fragment: weight row n = lane & 15 (+ 16 j), token row = 4 (lane >> 4) + r (+ 16 i)
+  // C fragment (32 x 32): weight row n = lane & 31 (+ 32 j), token row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
   const int nb = n0 + wn * (BN / WN) + fr;
-  const int mb = m0 + wm * (BM / WM) + 4 * (lane >> 4);
+  const int mb = m0 + wm * (BM / WM) + 4 * fq;
   if (sk > 1) {
     float* slab = P.gws + (long long)z * M * N;
 #pragma unroll
@@ -348,8 +384,8 @@ __global__ __launch_bounds__(DQ_NT, 1) void dq_gemm_kernel(GemvParams P, const f
 #pragma unroll
       for (int j = 0; j < TN; ++j)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int gm = mb + 16 * i + r, gn = nb + 16 * j;
+        for (int r = 0; r < 16; ++r) {
+          const int gm = mb + 32 * i + (r & 3) + 8 * (r >> 2), gn = nb + 32 * j;
           if (gm < M && gn < N) __builtin_nontemporal_store(acc[i][j][r], slab + (long long)gm * N + gn);
         }
     return;
@@ -365,9 +401,10 @@ __global__ __launch_bounds__(DQ_NT, 1) void dq_gemm_kernel(GemvParams P, const f
 }
 
 template <int BM, int BN>
-constexpr size_t dq_lds() { return (size_t)2 * (BM + BN) * DQ_LDR * sizeof(f16); }
+constexpr size_t dq_lds() { return (size_t)2 * (BM + BN) * DQ_BK * sizeof(f16); }
 
 int g_dq_enable = -1;  // -1: OMX_GEMM_DQ (default on), read once
+int g_dq_cfg = -1;     // OMX_DQ_CFG: force tile config 0..3 (microbenchmarks)
 
 }  // namespace
 
@@ -375,6 +412,8 @@ bool dq_gemm_enabled() {
   if (g_dq_enable < 0) {
     const char* e = getenv("OMX_GEMM_DQ");
     g_dq_enable = e ? atoi(e) != 0 : 1;
+    const char* c = getenv("OMX_DQ_CFG");
+    g_dq_cfg = c ? atoi(c) : -1;
   }
   return g_dq_enable != 0;
 }
@@ -400,6 +439,11 @@ static void run_dq(const GemvParams& P, f16* xp, int Kp, hipStream_t s) {
   else if (M >= 256) cfg = 1, tiles = ntl(256, 128);
   else if (ntl(128, 256) >= 240) cfg = 2, tiles = ntl(128, 256);
   else cfg = 3, tiles = ntl(128, 128);
+  if (g_dq_cfg >= 0 && g_dq_cfg <= 3) {  // microbenchmark override (OMX_DQ_CFG)
+    cfg = g_dq_cfg;
+    const int bm[4] = {256, 256, 128, 128}, bn[4] = {256, 128, 256, 128};
+    tiles = ntl(bm[cfg], bn[cfg]);
+  }
   int sk = 1;
   if (P.gws && P.gws_elems > 0)
     while (sk < 8 && tiles * sk < 240 && nks / (2 * sk) >= 8 && (long long)(2 * sk) * M * N <= P.gws_elems) sk *= 2;

@@ -7,7 +7,8 @@ forked or exec'ed from a GPU-initialised parent). All ranks then join:
   * the compute group (RCCL = backend "nccl" on ROCm, over xGMI): the runner's all-reduce of the
     row-parallel partial sums and the all-gather of vocab-sharded logits (engine/runner.py);
   * a gloo control group: rank 0 broadcasts every runner call (load / new_sequence / generate /
-    embed / ...) to the workers, and one continue/stop flag per decode step.
+    embed / ...) to the workers as int32 frames (no pickling; `TPControl`), and a host shared-memory
+    doorbell carries the continue/stop flag of each single-stream decode step (`Doorbell`).
 Sampling needs no token broadcast: every rank holds the all-gathered full logits and the same
 sampler state with the same resolved seed, so every rank samples the same token; only the stop
 decision (taken by the server on detokenised text) crosses the control group, which keeps the
@@ -42,30 +43,192 @@ def _free_port() -> int:
     return p
 
 
-class TPControl:
-    """Leader -> follower command / step-flag channel over a gloo group."""
+# ---- control channel -------------------------------------------------------------------------------
+# Commands travel as int32 frames over the gloo group -- no pickling: the per-step ops (decode_batch,
+# evict, new/free_sequence) are ONE fixed-size tensor broadcast; the rare structured ones (load, admit,
+# set_ext, ...) add one uint8 broadcast of a JSON document (numpy arrays and SamplingOptions encoded
+# explicitly, nothing executable). The per-token continue/stop flag of single-stream generation does not
+# use the group at all: a host shared-memory doorbell (all TP ranks of a pod share one node).
+FRAME_ROWS = 128                     # decode_batch rows carried inline
+_FRAME = 2 + 2 * FRAME_ROWS          # [op, n, sids..., poss...]
+_OPS = {"decode_batch": 1, "evict": 2, "new_sequence": 3, "free_sequence": 4, "warmup": 5, "unload": 6, "exit": 7}
+_OP_JSON = 100
+_NAMES = {v: k for k, v in _OPS.items()}
+ENV_DOORBELL = "OMX_TP_DOORBELL"
 
-    def __init__(self, group, leader: bool):
+
+def _enc(o):
+    import numpy as np
+    from ..engine.sampling import SamplingOptions
+    if isinstance(o, SamplingOptions):
+        return {"__opts__": dataclasses.asdict(o)}
+    if isinstance(o, np.ndarray):
+        import base64
+        a = np.ascontiguousarray(o)
+        return {"__nd__": [a.dtype.str, list(a.shape), base64.b64encode(a.tobytes()).decode("ascii")]}
+    if isinstance(o, (np.integer,)):
+        return int(o)
+    if isinstance(o, (np.floating,)):
+        return float(o)
+    raise TypeError(f"TP control: cannot encode {type(o).__name__}")
+
+
+def _dec(d):
+    if "__opts__" in d:
+        from ..engine.sampling import SamplingOptions
+        return SamplingOptions(**d["__opts__"])
+    if "__nd__" in d:
+        import base64
+
+        import numpy as np
+        dt, shape, b = d["__nd__"]
+        return np.frombuffer(base64.b64decode(b), dtype=np.dtype(dt)).reshape(shape).copy()
+    return d
+
+
+def encode_cmd(cmd: dict) -> bytes:
+    import json
+    return json.dumps(cmd, default=_enc, separators=(",", ":")).encode()
+
+
+def decode_cmd(blob: bytes) -> dict:
+    import json
+    return json.loads(blob.decode(), object_hook=_dec)
+
+
+class Doorbell:
+    """Leader -> follower step flags in host shared memory: a 64-slot ring of values plus a sequence
+    number (x86 stores are not reordered with other stores, so a follower that sees the sequence sees the
+    value); followers publish the last sequence they consumed so the leader never overwrites an unread
+    slot. Replaces one gloo broadcast per generated token."""
+    SLOTS = 64
+
+    def __init__(self, name: str, create: bool, rank: int = 0, world: int = 1):
+        import numpy as np
+        from multiprocessing import shared_memory
+        self.shm = shared_memory.SharedMemory(name=name, create=create, size=8 * (2 + self.SLOTS + 64))
+        if not create:  # the creator owns the segment (Python 3.10 would unlink it at a follower's exit)
+            try:
+                from multiprocessing import resource_tracker
+                resource_tracker.unregister(self.shm._name, "shared_memory")  # noqa: SLF001
+            except Exception:  # noqa: BLE001
+                pass
+        self.a = np.ndarray((2 + self.SLOTS + 64,), dtype=np.int64, buffer=self.shm.buf)
+        if create:
+            self.a[:] = 0
+        self.rank, self.world = rank, world
+        self.seen = int(self.a[0])
+
+    def ring(self, value: int) -> None:
+        seq = int(self.a[0]) + 1
+        # the slowest follower must have consumed seq - SLOTS before its slot is reused
+        while self.world > 1 and seq - min(int(self.a[2 + self.SLOTS + r]) for r in range(1, self.world)) > self.SLOTS:
+            time.sleep(0)
+        self.a[2 + seq % self.SLOTS] = value
+        self.a[0] = seq
+
+    def wait(self, alive=lambda: True) -> int:
+        target = self.seen + 1
+        spins, t0 = 0, time.monotonic()
+        while int(self.a[0]) < target:
+            spins += 1
+            if spins > 2000:
+                time.sleep(50e-6)
+                if time.monotonic() - t0 > 5.0:
+                    if not alive():
+                        raise RuntimeError("TP doorbell: leader gone")
+                    t0 = time.monotonic()
+        v = int(self.a[2 + target % self.SLOTS])
+        self.seen = target
+        self.a[2 + self.SLOTS + self.rank] = target
+        return v
+
+    def close(self, unlink: bool = False) -> None:
+        self.a = None
+        try:
+            self.shm.close()
+            if unlink:
+                self.shm.unlink()
+        except Exception:  # noqa: BLE001
+            pass
+
+
+class TPControl:
+    """Leader -> follower command / step-flag channel: int32 frames over a gloo group (commands) and a
+    shared-memory doorbell (step flags; gloo broadcast when no doorbell is configured)."""
+
+    def __init__(self, group, leader: bool, doorbell: "Doorbell | None" = None):
         self.group = group
         self.leader = leader
+        self.bell = doorbell
         self._flag = torch.zeros(1, dtype=torch.int32)
+        self._frame = torch.zeros(_FRAME, dtype=torch.int32)
 
     def send_cmd(self, cmd: dict) -> None:
         assert self.leader
-        dist.broadcast_object_list([cmd], src=0, group=self.group)
+        op = cmd["op"]
+        code = _OPS.get(op)
+        f = self._frame
+        f.zero_()
+        fast = code is not None and set(cmd) <= {"op", "sid", "sids", "poss"}
+        if fast and code == 1 and len(cmd["sids"]) > FRAME_ROWS:
+            fast = False
+        if fast:
+            f[0] = code
+            if code == 1:
+                n = len(cmd["sids"])
+                f[1] = n
+                f[2:2 + n] = torch.tensor(cmd["sids"], dtype=torch.int32)
+                f[2 + FRAME_ROWS:2 + FRAME_ROWS + n] = torch.tensor(cmd["poss"], dtype=torch.int32)
+            elif "sid" in cmd:
+                f[1] = 1
+                f[2] = int(cmd["sid"])
+            dist.broadcast(f, src=0, group=self.group)
+            return
+        blob = encode_cmd(cmd)
+        f[0] = _OP_JSON
+        f[1] = len(blob)
+        dist.broadcast(f, src=0, group=self.group)
+        dist.broadcast(torch.frombuffer(bytearray(blob), dtype=torch.uint8), src=0, group=self.group)
 
     def recv_cmd(self) -> dict:
-        box = [None]
-        dist.broadcast_object_list(box, src=0, group=self.group)
-        return box[0]
+        f = self._frame
+        dist.broadcast(f, src=0, group=self.group)
+        code, n = int(f[0]), int(f[1])
+        if code == _OP_JSON:
+            t = torch.empty(n, dtype=torch.uint8)
+            dist.broadcast(t, src=0, group=self.group)
+            return decode_cmd(t.numpy().tobytes())
+        op = _NAMES.get(code)
+        if op is None:
+            raise RuntimeError(f"TP control: unknown frame op {code}")
+        cmd = {"op": op}
+        if code == 1:
+            cmd["sids"] = f[2:2 + n].tolist()
+            cmd["poss"] = f[2 + FRAME_ROWS:2 + FRAME_ROWS + n].tolist()
+        elif n:
+            cmd["sid"] = int(f[2])
+        return cmd
 
     def signal(self, go: bool) -> None:  # leader: one decode step will follow (1) / generation over (0)
+        if self.bell is not None:
+            self.bell.ring(1 if go else 0)
+            return
         self._flag[0] = 1 if go else 0
         dist.broadcast(self._flag, src=0, group=self.group)
 
     def wait(self) -> bool:  # follower
+        if self.bell is not None:
+            return bool(self.bell.wait(alive=_parent_alive))
         dist.broadcast(self._flag, src=0, group=self.group)
         return bool(self._flag[0])
+
+
+_PPID = os.getppid()
+
+
+def _parent_alive() -> bool:
+    return os.getppid() == _PPID
 
 
 @dataclasses.dataclass
@@ -109,9 +272,11 @@ def start_leader(size: int) -> TPWorld:
     addr, port = "127.0.0.1", _free_port()
     workers = []
     pkg_root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    bell_name = f"omx_tp_{os.getpid()}_{port}"
+    bell = Doorbell(bell_name, create=True, rank=0, world=size)
     for r in range(1, size):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(size), MASTER_ADDR=addr,
-                   MASTER_PORT=str(port),
+                   MASTER_PORT=str(port), **{ENV_DOORBELL: bell_name},
                    PYTHONPATH=pkg_root + os.pathsep + os.environ.get("PYTHONPATH", ""))
         workers.append(subprocess.Popen([sys.executable, "-m", "ollama_operator_amd.parallel.tp_worker"], env=env))
     world = TPWorld(0, size, "", None, None, workers)
@@ -119,7 +284,7 @@ def start_leader(size: int) -> TPWorld:
     # leader blocked in init_process_group
     threading.Thread(target=_watchdog, args=(world,), name="tp-watchdog", daemon=True).start()
     dev, compute, ctrl = _init_groups(0, size, addr, port)
-    world.device, world.compute_group, world.ctrl = dev, compute, TPControl(ctrl, leader=True)
+    world.device, world.compute_group, world.ctrl = dev, compute, TPControl(ctrl, leader=True, doorbell=bell)
     return world
 
 
@@ -164,6 +329,8 @@ def shutdown_leader(world: TPWorld) -> None:
             p.wait(timeout=30)
         except subprocess.TimeoutExpired:
             p.kill()
+    if world.ctrl is not None and world.ctrl.bell is not None:
+        world.ctrl.bell.close(unlink=True)
 
 
 class TPRunnerProxy:
@@ -258,7 +425,8 @@ def load_tp_runner(world: TPWorld, path: str, max_batch: int, max_seqs: int, ctx
 def worker_main() -> None:
     rank, size = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     dev, compute, ctrl_group = _init_groups(rank, size, os.environ["MASTER_ADDR"], int(os.environ["MASTER_PORT"]))
-    ctrl = TPControl(ctrl_group, leader=False)
+    bell = Doorbell(os.environ[ENV_DOORBELL], create=False, rank=rank, world=size) if os.environ.get(ENV_DOORBELL) else None
+    ctrl = TPControl(ctrl_group, leader=False, doorbell=bell)
     from ..engine.runner import Runner
     runner = None
     while True:
