@@ -457,6 +457,8 @@ def main():
     if a.batch_extra > 1 and gpu:
         batched = bench_batched(runner, a, rank, world, sync)
     served = None
+    # resident weight bytes: the GGUF tensors (layout v2) plus the batched-decode layout M copies
+    layout_m_gb = getattr(runner, "mfma_bytes", 0) / 1e9
     if server is not None:
         weights_gb = runner.w.nbytes / 1e9
         n_vocab = runner.cfg.n_vocab
@@ -492,7 +494,8 @@ def main():
                        "sampling": "temperature 0.8, top_k 40, top_p 0.9, repeat_penalty 1.1 (on device)"},
             "extra": {"ttft_ms": round(ttft * 1e3, 2), f"ttft_{a.ttft_long}_ms": ttft_long, "prefill_chunk": a.chunk,
                       "load_s": round(load_s, 2),
-                      "weights_gb": round(weights_gb, 3),
+                      "weights_gb": round(weights_gb, 3), "layout_m_gb": round(layout_m_gb, 3),
+                      "resident_weights_gb": round(weights_gb + layout_m_gb, 3),
                       "continuous_batching": batched, "server": served},
         }), flush=True)
     if world > 1:

@@ -36,9 +36,10 @@ static QMat qmat(py::object o) {
   m.s4 = t.size() >= 8 ? Pp<const uint8_t>(t[7].cast<uintptr_t>()) : nullptr;
   m.mt = t.size() == 9 ? Pp<const uint8_t>(t[8].cast<uintptr_t>()) : nullptr;
   if (m.s4 && m.qtype != QT_Q6_K) throw std::runtime_error("widened codes are for Q6_K only");
-  if (m.qtype != QT_Q4_0 && m.qtype != QT_Q8_0 && m.qtype != QT_Q4_K && m.qtype != QT_Q5_K && m.qtype != QT_Q6_K)
+  if (m.qtype != QT_Q4_0 && m.qtype != QT_Q8_0 && m.qtype != QT_Q4_K && m.qtype != QT_Q5_K && m.qtype != QT_Q6_K &&
+      m.qtype != QT_F16)
     throw std::runtime_error("unsupported device quant type " + std::to_string(m.qtype));
-  const int blk = (m.qtype == QT_Q4_K || m.qtype == QT_Q5_K || m.qtype == QT_Q6_K) ? 256 : 32;
+  const int blk = (m.qtype == QT_Q4_K || m.qtype == QT_Q5_K || m.qtype == QT_Q6_K) ? 256 : m.qtype == QT_F16 ? 1 : 32;
   if (m.K % blk || m.K <= 0 || m.N <= 0) throw std::runtime_error("bad qmat geometry");
   return m;
 }

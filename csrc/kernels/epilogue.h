@@ -24,6 +24,12 @@ __device__ __forceinline__ void epi_apply_t(const GemvParams& P, int bb, int vn,
   } else if constexpr (E == EPI_GELU) {
     if (P.bias) v += P.bias[vn];
     P.y[(long long)bb * P.ldy + vn] = gelu_tanh(v);
+  } else if constexpr (E == EPI_GELU_ERF) {
+    if (P.bias) v += P.bias[vn];
+    P.y[(long long)bb * P.ldy + vn] = 0.5f * v * (1.f + erff(v * 0.70710678f));
+  } else if constexpr (E == EPI_QGELU) {
+    if (P.bias) v += P.bias[vn];
+    P.y[(long long)bb * P.ldy + vn] = v / (1.f + __expf(-1.702f * v));
   } else if constexpr (E == EPI_GLU) {
     if ((vn & 1) == 0)  // even row = gate, odd row = up
       P.y[(long long)bb * P.ldy + (long long)zsel * P.y_sel_stride + vn / 2] = silu(v) * pv;
@@ -66,6 +72,8 @@ __device__ __forceinline__ void epi_apply(const GemvParams& P, int bb, int vn, f
     case EPI_GLU: epi_apply_t<EPI_GLU>(P, bb, vn, v, pv, zsel); break;
     case EPI_GEGLU: epi_apply_t<EPI_GEGLU>(P, bb, vn, v, pv, zsel); break;
     case EPI_QKV: epi_apply_t<EPI_QKV>(P, bb, vn, v, pv, zsel); break;
+    case EPI_GELU_ERF: epi_apply_t<EPI_GELU_ERF>(P, bb, vn, v, pv, zsel); break;
+    case EPI_QGELU: epi_apply_t<EPI_QGELU>(P, bb, vn, v, pv, zsel); break;
   }
 }
 

@@ -24,9 +24,10 @@
 //    buffer, issues the loads of step ks + 2, then runs the MFMAs of step ks -- one barrier per K step,
 //    HBM/L2 latency covered by a full step of matrix work, VALU dequant of one wave overlapping the
 //    MFMAs of the other wave on its SIMD.
-//  * Grid: XCD-aware bijective remap; blocks that share an XCD (and its L2) walk the M tiles of the
-//    same N tile, so each weight tile is fetched from HBM about once per XCD. Grids that cannot fill
-//    256 CUs split K (fp32 slabs + the deterministic finalize of gemm.hip).
+//  * Grid: XCD-aware bijective remap, M-major: the blocks that share an XCD (and its 4 MB L2) work on
+//    the same activation tile and different weight tiles, so X lines come from L2 (each weight tile is
+//    read once per M tile, from HBM / the Infinity Cache). Grids that cannot fill 256 CUs split K
+//    (fp32 slabs + the deterministic finalize of gemm.hip).
 //  * Epilogue straight from the accumulators: the C fragment holds weight rows n on lanes 16 apart
 //    and the row pair (n, n ^ 1) on adjacent lanes (one DPP swap), so SiLU-GLU / RoPE + KV scatter /
 //    residual add / bias run through the shared epi_apply (epilogue.h) with no LDS round trip.
@@ -65,6 +66,7 @@ __device__ __forceinline__ unsigned dsel(const u32x4& v, int i) { return i == 0 
 // weight offsets (natural K) of the lo / hi 16-weight halves of piece t of super-block sb
 template <int QT>
 __host__ __device__ __forceinline__ int piece_off(int t, int sb, int g) {
+  static_assert(QT != QT_F16, "F16 rows are in natural order (prep_xp copies them straight)");
   if constexpr (QT == QT_Q4_K || QT == QT_Q5_K) return 256 * sb + 64 * (t >> 1) + 16 * (t & 1) + 32 * g;
   else if constexpr (QT == QT_Q6_K) return 256 * sb + 128 * (t >> 2) + 16 * (t & 3) + 64 * g;
   else return 256 * sb + 32 * t + 16 * g;  // Q4_0 / Q8_0
@@ -97,26 +99,46 @@ __global__ __launch_bounds__(256) void prep_xp_kernel(GemvParams P, f16* out, in
     }
   }
   f16* o = out + (long long)b * Kp;
-  for (int c = threadIdx.x; c < Kp / 8; c += 256) {
-    const int kp = 8 * c, pc = kp >> 5, p0 = kp & 31;
-    const int t = pc / SB, sb = pc - t * SB;
-    const int base = piece_off<QT>(t, sb, p0 >> 4) + 4 * ((p0 & 15) >> 2);
-    f16x8 v;
+  if constexpr (QT == QT_F16) {  // natural order: the weight rows are plain fp16
+    for (int c = threadIdx.x; c < Kp / 8; c += 256) {
+      f16x8 v;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int r = j & 3;
-      const int k = base + 4 * (j >> 2) + (r == 1 ? 2 : r == 2 ? 1 : r);
-      float e = 0.f;
-      if (k < K) {
-        e = x[k];
-        if (P.norm != NORM_NONE) {
-          e = (e - mean) * rstd * P.norm_w[k];
-          if (P.norm == NORM_LAYER && P.norm_b) e += P.norm_b[k];
+      for (int j = 0; j < 8; ++j) {
+        const int k = 8 * c + j;
+        float e = 0.f;
+        if (k < K) {
+          e = x[k];
+          if (P.norm != NORM_NONE) {
+            e = (e - mean) * rstd * P.norm_w[k];
+            if (P.norm == NORM_LAYER && P.norm_b) e += P.norm_b[k];
+          }
         }
+        v[j] = (f16)e;
       }
-      v[j] = (f16)e;
+      *(f16x8*)(o + 8 * c) = v;
     }
-    *(f16x8*)(o + kp) = v;
+  } else {
+    for (int c = threadIdx.x; c < Kp / 8; c += 256) {
+      const int kp = 8 * c, pc = kp >> 5, p0 = kp & 31;
+      const int t = pc / SB, sb = pc - t * SB;
+      const int base = piece_off<QT>(t, sb, p0 >> 4) + 4 * ((p0 & 15) >> 2);
+      f16x8 v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int r = j & 3;
+        const int k = base + 4 * (j >> 2) + (r == 1 ? 2 : r == 2 ? 1 : r);
+        float e = 0.f;
+        if (k < K) {
+          e = x[k];
+          if (P.norm != NORM_NONE) {
+            e = (e - mean) * rstd * P.norm_w[k];
+            if (P.norm == NORM_LAYER && P.norm_b) e += P.norm_b[k];
+          }
+        }
+        v[j] = (f16)e;
+      }
+      *(f16x8*)(o + kp) = v;
+    }
   }
 }
 
@@ -129,10 +151,19 @@ struct Piece {
   u32x4 m;                                   // Q4_K / Q5_K meta (d, dmin, scales12); Q6_K int8 scales
   u32x2 h;                                   // Q6_K high-bit pairs
   unsigned e;                                // Q5_K 5th bits; Q6_K / Q4_0 / Q8_0: fp16 d (low half)
+  u32x4 f[QT == QT_F16 ? 2 : 1];             // F16: halves 16..31 of the piece
 };
 
 template <int QT>
 __device__ __forceinline__ void load_piece(const QMat& w, long long row, int SB, int pc, Piece<QT>& R) {
+  if constexpr (QT == QT_F16) {  // natural order: piece pc = halves 32 pc .. + 31 of the row
+    const uint8_t* q = w.s0 + row * SB * 512 + 64LL * pc;
+    R.a = *(const u32x4*)q;
+    R.b = *(const u32x4*)(q + 16);
+    R.f[0] = *(const u32x4*)(q + 32);
+    R.f[1] = *(const u32x4*)(q + 48);
+    return;
+  }
   const int t = pc / SB, sb = pc - t * SB;
   if constexpr (QT == QT_Q8_0) {
     const uint8_t* q = w.s0 + row * SB * 256 + 32LL * pc;
@@ -166,7 +197,11 @@ __device__ __forceinline__ void k_scale(const u32x4& m, int j, float& sc, float&
 // dequantise a piece to 32 fp16 in stream order: o[0..7] = lo half pairs, o[8..15] = hi half pairs
 template <int QT>
 __device__ __forceinline__ void dq_piece(const Piece<QT>& R, int t, unsigned (&o)[16]) {
-  if constexpr (QT == QT_Q4_K || QT == QT_Q5_K) {
+  if constexpr (QT == QT_F16) {
+    const u32x4 v[4] = {R.a, R.b, R.f[0], R.f[1]};
+#pragma unroll
+    for (int i = 0; i < 16; ++i) o[i] = dsel(v[i >> 2], i & 3);
+  } else if constexpr (QT == QT_Q4_K || QT == QT_Q5_K) {
     const int c = t >> 1;
     float s0, c0, s1, c1;
     k_scale(R.m, 2 * c, s0, c0);
@@ -256,8 +291,7 @@ __device__ __forceinline__ void dq_out(const GemvParams& P, const f32x16 (&acc)[
 
 // ------------------------------------------------------------------------------------------------
 template <int QT, int BM, int BN, int WM, int WN>
-__global__ __launch_bounds__(DQ_NT, 1) void dq_gemm_kernel(GemvParams P, const f16* __restrict__ X, int Kp, int mt,
-                                                           int sk) {
+__global__ __launch_bounds__(DQ_NT, 1) void dq_gemm_kernel(GemvParams P, const f16* __restrict__ X, int Kp, int sk) {
   static_assert(WM * WN == 8, "8 waves");
   constexpr int TM = BM / WM / 32, TN = BN / WN / 32;  // 32 x 32 accumulator tiles per wave
   constexpr int XS = BM * DQ_BK, WS = BN * DQ_BK;      // halves per LDS buffer (128-B rows, swizzled)
@@ -269,12 +303,17 @@ __global__ __launch_bounds__(DQ_NT, 1) void dq_gemm_kernel(GemvParams P, const f
 
   const QMat& w = P.w;
   const int M = P.B, N = w.N, SB = Kp >> 8, nks = SB * 4;
-  const unsigned sbinv = (0xFFFFFFFFu / (unsigned)SB) + 1u;  // pc / SB = umulhi(pc, sbinv) for pc < 8 SB
+  // pc / SB = umulhi(pc, ceil(2^32 / SB)) for pc < 8 SB (SB = 1 would overflow: taken apart)
+  const unsigned sbinv = (0xFFFFFFFFu / (unsigned)SB) + 1u;
   // XCD-aware bijective remap: the blocks one XCD runs are a contiguous range of (tile, split) ids
   const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
   const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
   const int z = wg % sk, tile = wg / sk;
-  const int m0 = (tile % mt) * BM, n0 = (tile / mt) * BN;
+  // M-major: the blocks of one XCD share an activation tile (BM x K fp16, 2-6 MB) and walk the weight
+  // tiles, advancing through K roughly together -- each X line is fetched into that XCD's L2 once and
+  // hit by every block there (N-major order streamed X from the Infinity Cache at full latency)
+  const int nt = (N + BN - 1) / BN;
+  const int m0 = (tile / nt) * BM, n0 = (tile % nt) * BN;
   const int ks0 = (int)((long long)z * nks / sk), ks1 = (int)((long long)(z + 1) * nks / sk);
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -307,7 +346,7 @@ __global__ __launch_bounds__(DQ_NT, 1) void dq_gemm_kernel(GemvParams P, const f
     if (wact) {
       const int pc = 2 * ks + wh;
       unsigned o[16];
-      dq_piece<QT>(wreg, (int)__umulhi((unsigned)pc, sbinv), o);  // t = pc / SB
+      dq_piece<QT>(wreg, SB == 1 ? pc : (int)__umulhi((unsigned)pc, sbinv), o);  // t = pc / SB
       f16* wd = Ws + buf * WS;
 #pragma unroll
       for (int i = 0; i < 4; ++i)
@@ -396,6 +435,8 @@ __global__ __launch_bounds__(DQ_NT, 1) void dq_gemm_kernel(GemvParams P, const f
     case EPI_GELU: dq_out<EPI_GELU, TM, TN>(P, acc, mb, nb, M, N); break;
     case EPI_GLU: dq_out<EPI_GLU, TM, TN>(P, acc, mb, nb, M, N); break;
     case EPI_GEGLU: dq_out<EPI_GEGLU, TM, TN>(P, acc, mb, nb, M, N); break;
+    case EPI_GELU_ERF: dq_out<EPI_GELU_ERF, TM, TN>(P, acc, mb, nb, M, N); break;
+    case EPI_QGELU: dq_out<EPI_QGELU, TM, TN>(P, acc, mb, nb, M, N); break;
     default: dq_out<EPI_QKV, TM, TN>(P, acc, mb, nb, M, N); break;
   }
 }
@@ -404,7 +445,7 @@ template <int BM, int BN>
 constexpr size_t dq_lds() { return (size_t)2 * (BM + BN) * DQ_BK * sizeof(f16); }
 
 int g_dq_enable = -1;  // -1: OMX_GEMM_DQ (default on), read once
-int g_dq_cfg = -1;     // OMX_DQ_CFG: force tile config 0..3 (microbenchmarks)
+int g_dq_cfg = -2;     // OMX_DQ_CFG: force tile config 0..3 (microbenchmarks); -2 = not read yet
 
 }  // namespace
 
@@ -412,6 +453,8 @@ bool dq_gemm_enabled() {
   if (g_dq_enable < 0) {
     const char* e = getenv("OMX_GEMM_DQ");
     g_dq_enable = e ? atoi(e) != 0 : 1;
+  }
+  if (g_dq_cfg == -2) {
     const char* c = getenv("OMX_DQ_CFG");
     g_dq_cfg = c ? atoi(c) : -1;
   }
@@ -424,7 +467,7 @@ template <int QT, int BM, int BN, int WM, int WN>
 static void launch_dq(const GemvParams& P, const f16* xp, int Kp, int sk, hipStream_t s) {
   const int mt = (P.B + BM - 1) / BM, nt = (P.w.N + BN - 1) / BN;
   const size_t lds = dq_lds<BM, BN>();
-  hipLaunchKernelGGL((dq_gemm_kernel<QT, BM, BN, WM, WN>), dim3(mt * nt * sk), dim3(DQ_NT), lds, s, P, xp, Kp, mt, sk);
+  hipLaunchKernelGGL((dq_gemm_kernel<QT, BM, BN, WM, WN>), dim3(mt * nt * sk), dim3(DQ_NT), lds, s, P, xp, Kp, sk);
 }
 
 template <int QT>
@@ -459,7 +502,7 @@ static void run_dq(const GemvParams& P, f16* xp, int Kp, hipStream_t s) {
 bool dq_gemm(const GemvParams& P, hipStream_t s) {
   if (!dq_gemm_enabled() || P.B < 128 || !P.xws || P.expert_ids || P.moe_tiles) return false;
   const int qt = P.w.qtype;
-  if (qt != QT_Q4_K && qt != QT_Q5_K && qt != QT_Q6_K && qt != QT_Q4_0 && qt != QT_Q8_0) return false;
+  if (qt != QT_Q4_K && qt != QT_Q5_K && qt != QT_Q6_K && qt != QT_Q4_0 && qt != QT_Q8_0 && qt != QT_F16) return false;
   const int Kp = ((P.w.K + 255) >> 8) * 256;
   const long long cap = P.xws_elems ? P.xws_elems : (long long)P.B * P.w.K;
   if ((long long)P.B * Kp > cap) return false;
@@ -469,6 +512,7 @@ bool dq_gemm(const GemvParams& P, hipStream_t s) {
     case QT_Q5_K: run_dq<QT_Q5_K>(P, xp, Kp, s); break;
     case QT_Q6_K: run_dq<QT_Q6_K>(P, xp, Kp, s); break;
     case QT_Q4_0: run_dq<QT_Q4_0>(P, xp, Kp, s); break;
+    case QT_F16: run_dq<QT_F16>(P, xp, Kp, s); break;
     default: run_dq<QT_Q8_0>(P, xp, Kp, s); break;
   }
   return true;

@@ -844,6 +844,10 @@ bool gemv_merge_supported(int B, int K, int D, int S) {
 void gemv(const GemvParams& P0, hipStream_t s) {
   if (P0.B == 1 && (P0.x8 || P0.emit8) && gemv8(P0, s)) return;  // int8 activation chain (gemv8.hip)
   if (P0.emit8) throw std::runtime_error("gemv: int8 activation emitter not covered by gemv8");
+  if (P0.w.qtype == QT_F16) {  // fp16 weights (vision tower): the stream-order GEMM only
+    if (!dq_gemm(P0, s)) throw std::runtime_error("gemv: F16 weights need >= 128 rows and an fp16 workspace");
+    return;
+  }
   GemvParams P = P0;
   P.xfirst = g_tune.xfirst;
   if (P.merge_S > 0) {

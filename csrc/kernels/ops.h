@@ -10,7 +10,9 @@
 namespace omx {
 
 enum { NORM_NONE = 0, NORM_RMS = 1, NORM_LAYER = 2 };
-enum { EPI_STORE = 0, EPI_ADD = 1, EPI_GLU = 2, EPI_GELU = 3, EPI_QKV = 4, EPI_GEGLU = 5 };
+// EPI_GELU: tanh approximation (Phi-2 / Gemma); EPI_GELU_ERF: exact erf GELU (LLaVA projector, CLIP with
+// use_gelu); EPI_QGELU: x * sigmoid(1.702 x) (OpenAI CLIP "quick GELU"). The last two: prefill GEMM only
+enum { EPI_STORE = 0, EPI_ADD = 1, EPI_GLU = 2, EPI_GELU = 3, EPI_QKV = 4, EPI_GEGLU = 5, EPI_GELU_ERF = 6, EPI_QGELU = 7 };
 
 struct GemvParams {
   QMat w;

@@ -16,7 +16,9 @@
 // s2 (int8 per 16) / s3 (fp16 per 256). Opt-in (OMX_Q6K_WIDEN=1) for the batch-1 GEMV: it trades the
 // 6-bit unpack chain (~5 us per down-projection launch, profiles/r2_gemv) for +30 % bytes, and in the
 // engine that measured slower (down 13.2 -> 14.6 us). Prefill GEMM and batched GEMV read 6-bit streams.
-enum QType : int { QT_Q4_0 = 2, QT_Q8_0 = 8, QT_Q4_K = 12, QT_Q5_K = 13, QT_Q6_K = 14, QT_Q6_K8 = 114 };
+// QT_F16 (ggml F16): plain fp16 rows [N][SB * 256] (K zero-padded to whole super-blocks) in s0; taken by
+// the prefill GEMM only (gemm_dq.hip), e.g. the CLIP vision tower (models/clip.py)
+enum QType : int { QT_F16 = 1, QT_Q4_0 = 2, QT_Q8_0 = 8, QT_Q4_K = 12, QT_Q5_K = 13, QT_Q6_K = 14, QT_Q6_K8 = 114 };
 
 struct QMat {
   const uint8_t* s0;

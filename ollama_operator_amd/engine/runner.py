@@ -149,7 +149,9 @@ class Runner:
         self.tp_ctrl = tp_ctrl
         self.w = weights or DeviceWeights(model_path, self.device, tp_rank, tp_size)
         # continuous batching on the matrix cores (gemv_mfma.hip): layout M weight copies, built on the
-        # device, whenever this runner can batch sequences (OMX_MFMA_BATCH=0 keeps the int8 GEMV only)
+        # device, whenever this runner can batch sequences (OMX_MFMA_BATCH=0 keeps the int8 GEMV only).
+        # Reading the resident v2 streams directly instead measured 2x slower at B = 4 (16-B row runs per
+        # load instruction: experiments/kernels/gemv_mfma_v2_piece_per_wave.hip, profiles/r4_batch)
         self.mfma_bytes = 0
         if self.is_gpu and max_seqs > 1 and os.environ.get("OMX_MFMA_BATCH", "1") != "0":
             self.mfma_bytes = self.w.build_mfma_layouts()

@@ -27,6 +27,7 @@ from __future__ import annotations
 import hashlib
 import io
 import math
+import os
 from dataclasses import dataclass
 
 import numpy as np
@@ -125,8 +126,128 @@ def preprocess(image: bytes | np.ndarray, cfg: ClipConfig) -> np.ndarray:
     return np.ascontiguousarray(a.transpose(2, 0, 1))
 
 
+class _NativeTower:
+    """The CLIP tower on the engine's own kernels (GPU): every projection is the stream-order MFMA GEMM
+    (csrc/kernels/gemm_dq.hip) on fp16 weight rows (QT_F16, K zero-padded to 256) with the LayerNorm
+    fused into its activation prologue and bias / quick-GELU / erf-GELU / residual add in its epilogue;
+    QKV goes through the same RoPE-less QKV epilogue as the LLM and scatters K/V into a private paged
+    cache that the MFMA flash-attention kernel (attention.hip) reads with every key visible to every
+    query (q_len = n: bidirectional). Only the patch im2col, the class/position add and the stand-alone
+    pre/post LayerNorms stay torch element-wise ops."""
+
+    QT_F16 = 1
+    EPI_STORE, EPI_ADD, EPI_QKV, EPI_GELU_ERF, EPI_QGELU = 0, 1, 4, 6, 7
+    NORM_LAYER = 2
+
+    def __init__(self, enc: "ClipEncoder"):
+        from ..ops import native
+        self.C = native()
+        self.enc = enc
+        c = enc.cfg
+        dev = enc.device
+        h16 = dict(device=dev, dtype=torch.float16)
+        f32 = dict(device=dev, dtype=torch.float32)
+
+        def mat(w: torch.Tensor):  # [N][K] -> fp16 rows padded to whole 256-blocks (QMat tuple, tensor)
+            N, K = w.shape
+            Kp = (K + 255) // 256 * 256
+            t = torch.zeros(N, Kp, **h16)
+            t[:, :K] = w.to(torch.float16)
+            return (t.data_ptr(), 0, 0, 0, N, K, self.QT_F16), t
+
+        self.keep = []
+
+        def M(w):
+            tup, t = mat(w)
+            self.keep.append(t)
+            return tup
+
+        f = lambda v: v.to(**f32).contiguous()  # noqa: E731
+        E, n = c.E, c.n_patches + 1
+        self.patch = M(enc.patch_w.reshape(E, -1))
+        self.patch_b = f(enc.patch_b) if enc.patch_b is not None else None
+        self.layers = []
+        for b in enc.blocks:
+            self.layers.append(dict(
+                qkv=M(torch.cat([b["attn_q.weight"], b["attn_k.weight"], b["attn_v.weight"]], 0)),
+                bqkv=f(torch.cat([b["attn_q.bias"], b["attn_k.bias"], b["attn_v.bias"]], 0)),
+                o=M(b["attn_out.weight"]), bo=f(b["attn_out.bias"]),
+                up=M(b["ffn_up.weight"]), bup=f(b["ffn_up.bias"]),
+                down=M(b["ffn_down.weight"]), bdown=f(b["ffn_down.bias"]),
+                ln1=(f(b["ln1.weight"]), f(b["ln1.bias"])), ln2=(f(b["ln2.weight"]), f(b["ln2.bias"]))))
+        (w0, b0), (w2, b2) = enc.mm
+        self.mm0, self.mb0 = M(w0), f(b0)
+        self.mm2, self.mb2 = M(w2), f(b2)
+        self.F = enc.blocks[0]["ffn_up.weight"].shape[0] if enc.blocks else E
+        self.P = w0.shape[0]
+        # workspaces: fp16 activations (largest K), split-K slabs, the attention cache and step inputs
+        kmax = max((w.shape[1] + 255) // 256 * 256 for w in [enc.patch_w.reshape(E, -1), w0, w2] +
+                   [b["ffn_down.weight"] for b in enc.blocks] + [b["attn_q.weight"] for b in enc.blocks])
+        self.xws = torch.empty(n * kmax, **h16)
+        self.gws = torch.empty(8 << 20, **f32)
+        self.H, self.D = c.n_head, E // c.n_head
+        self.bs = 16
+        nblk = (n + self.bs - 1) // self.bs
+        self.kc = torch.zeros(nblk, self.H, self.bs, self.D, **h16)
+        self.vc = torch.zeros_like(self.kc)
+        i32 = dict(device=dev, dtype=torch.int32)
+        self.pos = torch.arange(n, **i32)
+        self.qlen = torch.full((n,), n, **i32)  # every key visible to every query: bidirectional
+        self.bt = torch.arange(nblk, **i32)[None].contiguous()
+        self.nblk = nblk
+        self.q = torch.empty(n, E, **f32)
+        self.a = torch.empty(n, E, **f32)
+        self.h = torch.empty(n, max(self.F, self.P), **f32)
+        self.dummy = torch.zeros(max(1, self.D), **f32)
+
+    def _gemm(self, w, B, x, ldx, y, ldy, epi, bias=None, norm=None, extra=None):
+        d = dict(extra or {})
+        d.update(xws=self.xws.data_ptr(), xws_elems=self.xws.numel(), gws=self.gws.data_ptr(),
+                 gws_elems=self.gws.numel())
+        nw, nb = norm if norm is not None else (None, None)
+        p = lambda t: t.data_ptr() if t is not None else 0  # noqa: E731
+        self.C.gemv(w, B, x.data_ptr(), ldx, self.NORM_LAYER if norm is not None else 0, p(nw), p(nb),
+                    self.enc.cfg.eps, epi, y.data_ptr(), ldy, p(bias), 0, d, torch.cuda.current_stream().cuda_stream)
+
+    @torch.no_grad()
+    def encode(self, px: torch.Tensor) -> torch.Tensor:
+        enc, c = self.enc, self.enc.cfg
+        E, ps, n, H, D = c.E, c.patch_size, c.n_patches + 1, self.H, self.D
+        # patch embedding as a GEMM: im2col rows in the conv weight's (channel, y, x) order
+        x = torch.as_tensor(px).to(enc.device, torch.float32)
+        cols = x.unfold(1, ps, ps).unfold(2, ps, ps)  # [3, g, g, ps, ps]
+        cols = cols.permute(1, 2, 0, 3, 4).reshape(c.n_patches, -1).contiguous()
+        emb = torch.empty(c.n_patches, E, device=enc.device)
+        self._gemm(self.patch, c.n_patches, cols, cols.shape[1], emb, E, self.EPI_STORE, self.patch_b)
+        xs = torch.cat([enc.cls.float()[None], emb], 0) + enc.pos.float()
+        if enc.pre_ln[0] is not None:
+            xs = F.layer_norm(xs, (E,), enc.pre_ln[0].float(), enc.pre_ln[1].float(), c.eps)
+        xs = xs.contiguous()
+        qkv = dict(pos=self.pos.data_ptr(), slot=self.pos.data_ptr(), kc=self.kc.data_ptr(), vc=self.vc.data_ptr(),
+                   inv_freq=self.dummy.data_ptr(), Eq=E, Ekv=E, D=D, n_rot=0, n_kv=H, bs=self.bs)
+        st = torch.cuda.current_stream().cuda_stream
+        for L in self.layers:
+            self._gemm(L["qkv"], n, xs, E, self.q, E, self.EPI_QKV, L["bqkv"], L["ln1"], qkv)
+            self.C.attention(self.q.data_ptr(), E, self.kc.data_ptr(), self.vc.data_ptr(), self.bt.data_ptr(),
+                             self.nblk, 0, self.qlen.data_ptr(), n, H, H, D, self.bs, 1.0 / math.sqrt(D), 0,
+                             self.a.data_ptr(), E, 0, 1, 0, st, 1, D)
+            self._gemm(L["o"], n, self.a, E, xs, E, self.EPI_ADD, L["bo"])
+            act = self.EPI_GELU_ERF if c.use_gelu else self.EPI_QGELU
+            self._gemm(L["up"], n, xs, E, self.h, self.h.shape[1], act, L["bup"], L["ln2"])
+            self._gemm(L["down"], n, self.h, self.h.shape[1], xs, E, self.EPI_ADD, L["bdown"])
+        if enc.post_ln[0] is not None:
+            xs = F.layer_norm(xs, (E,), enc.post_ln[0].float(), enc.post_ln[1].float(), c.eps)
+        xs = xs[1:].contiguous()  # LLaVA drops the class token
+        m = n - 1
+        self._gemm(self.mm0, m, xs, E, self.h, self.h.shape[1], self.EPI_GELU_ERF, self.mb0)
+        out = torch.empty(m, self.mm2[4], device=enc.device)
+        self._gemm(self.mm2, m, self.h, self.h.shape[1], out, out.shape[1], self.EPI_STORE, self.mb2)
+        return out
+
+
 class ClipEncoder:
-    """CLIP ViT + LLaVA MLP projector on `device` (fp16 on GPU, fp32 on CPU)."""
+    """CLIP ViT + LLaVA MLP projector on `device`: on a GPU the engine's own kernels (`_NativeTower`:
+    MFMA GEMMs + flash attention; OMX_CLIP_NATIVE=0 keeps the fp16 torch path), on a CPU fp32 torch."""
 
     def __init__(self, path: str, device: str | torch.device = "cpu"):
         self.device = torch.device(device)
@@ -154,6 +275,13 @@ class ClipEncoder:
             g.close()
         if self.pos.shape[0] != self.cfg.n_patches + 1:
             raise VisionError(f"position table has {self.pos.shape[0]} rows, expected {self.cfg.n_patches + 1}")
+        # the native tower needs >= 128 patch rows (the MFMA GEMM's row minimum) and a flash-attention
+        # head dim; smaller / odd towers (test fixtures) keep the fp16 torch path
+        self.native = None
+        c = self.cfg
+        if (self.device.type == "cuda" and os.environ.get("OMX_CLIP_NATIVE", "1") != "0" and c.n_patches >= 128
+                and c.E % c.n_head == 0 and c.E // c.n_head in (64, 80, 96, 128)):
+            self.native = _NativeTower(self)
 
     @property
     def out_dim(self) -> int:
@@ -167,6 +295,12 @@ class ClipEncoder:
     @torch.no_grad()
     def encode_pixels(self, px: np.ndarray | torch.Tensor) -> torch.Tensor:
         """[3, S, S] normalised pixels -> [n_patches, out_dim] fp32 LLM embedding rows."""
+        if self.native is not None:
+            return self.native.encode(px)
+        return self.encode_pixels_torch(px)
+
+    @torch.no_grad()
+    def encode_pixels_torch(self, px: np.ndarray | torch.Tensor) -> torch.Tensor:
         c = self.cfg
         x = torch.as_tensor(px).to(self.device, self.dtype)[None]
         x = F.conv2d(x, self.patch_w, self.patch_b, stride=c.patch_size)  # [1, E, g, g]

@@ -39,3 +39,22 @@ def test_ext_rows_native_gpu(tiny_models):
     assert torch.allclose(r.logits[0, :V], want, rtol=1e-4, atol=1e-4)
     toks = list(r.generate(r.new_sequence(), p2[:6], max_tokens=4))
     assert len(toks) == 4 and all(0 <= x < V for x in toks)
+
+
+@pytest.mark.parametrize("gelu", [False, True])
+def test_native_clip_tower_matches_oracle(tmp_path, gelu):
+    """The CLIP tower on the engine's kernels (F16 MFMA GEMMs with fused LayerNorm / bias / GELU epilogues,
+    RoPE-less QKV scatter, bidirectional flash attention) against the fp64 numpy oracle."""
+    from ollama_operator_amd.models.clip import ClipEncoder, preprocess, reference_encode, write_random_clip_gguf
+    p = str(tmp_path / "mmproj.gguf")
+    write_random_clip_gguf(p, out_dim=E_LLM, image_size=168, patch_size=14, E=256, F_=512, n_layer=2, n_head=4,
+                           seed=3, use_gelu=gelu)
+    enc = ClipEncoder(p, "cuda")
+    assert enc.native is not None and enc.cfg.n_patches == 144
+    px = preprocess(_png(seed=5), enc.cfg)
+    got = enc.encode_pixels(px).cpu().numpy()
+    ref = reference_encode(p, px)
+    assert got.shape == ref.shape
+    assert np.linalg.norm(got - ref) / np.linalg.norm(ref) < 2e-2
+    torch_path = enc.encode_pixels_torch(px).cpu().numpy()
+    assert np.linalg.norm(got - torch_path) / np.linalg.norm(torch_path) < 2e-2
