@@ -12,7 +12,13 @@ Design: the encoder runs once per image (576 patches for LLaVA-1.5 at 336 px), s
 PyTorch module on the runner's device -- fp16 GEMMs on hipBLASLt and fused SDPA attention on the
 GPU -- not a hand-written kernel path; the language model's prefill/decode loop is where the time
 goes. Image preprocessing follows LLaVA-1.5 ("pad" aspect): pad to a square with the mean colour,
-resize to image_size, normalise by image_mean / image_std.
+resize to image_size, normalise by image_mean / image_std. A LLaVA-1.6 projector (metadata
+clip.vision.image_grid_pinpoints + mm_patch_merge_type, tensor model.image_newline) takes the
+any-resolution path instead (`preprocess_anyres` / `ClipEncoder.encode`): the grid resolution that
+keeps the most image detail is picked from the pinpoints, the image is fitted into it and cut into
+image_size tiles, every tile and a downsized whole-image view go through the tower, and the tile
+features are stitched back into one patch grid, unpadded to the image's aspect and closed per row
+with the image_newline embedding ("spatial_unpad"; "flat" concatenates the views).
 
 Tensor names / metadata (llama.cpp clip GGUF): v.patch_embd.weight [E,3,p,p], v.class_embd [E],
 v.position_embd.weight [n_pos,E], v.pre_ln.{weight,bias}, v.blk.{i}.{attn_q,attn_k,attn_v,attn_out,
@@ -57,10 +63,21 @@ class ClipConfig:
     use_gelu: bool
     projector: str
     out_dim: int
+    grid_pinpoints: tuple[tuple[int, int], ...] = ()  # LLaVA-1.6 any-resolution grids (w, h); () = 1.5
+    merge: str = "flat"
 
     @property
     def n_patches(self) -> int:
         return (self.image_size // self.patch_size) ** 2
+
+    @property
+    def max_rows(self) -> int:
+        """Most embedding rows one image can produce (ids / external-row capacity)."""
+        if not self.grid_pinpoints:
+            return self.n_patches
+        g, S = self.image_size // self.patch_size, self.image_size
+        nl = 1 if self.merge == "spatial_unpad" else 0
+        return self.n_patches + max((H // S) * g * ((W // S) * g + nl) for W, H in self.grid_pinpoints)
 
 
 def clip_config(md: dict, tensors: dict) -> ClipConfig:
@@ -71,12 +88,28 @@ def clip_config(md: dict, tensors: dict) -> ClipConfig:
     if proj != "mlp":
         raise VisionError(f"unsupported projector type {proj!r} (supported: mlp)")
     out_dim = tensors["mm.2.weight"].torch_shape[0]
-    return ClipConfig(image_size=int(g("image_size", 336)), patch_size=int(g("patch_size", 14)),
+    S = int(g("image_size", 336))
+    pins = [int(v) for v in g("image_grid_pinpoints", ())]
+    if len(pins) % 2:
+        raise VisionError("clip.vision.image_grid_pinpoints must hold (width, height) pairs")
+    grid = tuple((pins[i], pins[i + 1]) for i in range(0, len(pins), 2))
+    if any(W <= 0 or H <= 0 or W % S or H % S for W, H in grid):
+        raise VisionError(f"grid pinpoints {grid} are not positive multiples of image_size {S}")
+    merge = str(g("mm_patch_merge_type", "flat"))
+    if merge not in ("flat", "spatial_unpad"):
+        raise VisionError(f"unsupported mm_patch_merge_type {merge!r} (supported: flat, spatial_unpad)")
+    if grid and merge == "spatial_unpad" and "model.image_newline" not in tensors:
+        raise VisionError("spatial_unpad merge needs the model.image_newline tensor")
+    c = ClipConfig(image_size=int(g("image_size", 336)), patch_size=int(g("patch_size", 14)),
                       E=int(g("embedding_length")), F=int(g("feature_length")), n_layer=int(g("block_count")),
                       n_head=int(g("attention.head_count")), eps=float(g("attention.layer_norm_epsilon", 1e-5)),
                       mean=tuple(float(v) for v in g("image_mean", (0.48145466, 0.4578275, 0.40821073))),
                       std=tuple(float(v) for v in g("image_std", (0.26862954, 0.26130258, 0.27577711))),
-                      use_gelu=bool(md.get("clip.use_gelu", False)), projector=proj, out_dim=int(out_dim))
+                      use_gelu=bool(md.get("clip.use_gelu", False)), projector=proj, out_dim=int(out_dim),
+                      grid_pinpoints=grid, merge=merge)
+    if c.max_rows > MAX_PATCHES_PER_IMAGE:
+        raise VisionError(f"grid pinpoints give up to {c.max_rows} rows per image (> {MAX_PATCHES_PER_IMAGE})")
+    return c
 
 
 # decoded-size limits: a tiny file can declare a huge (or extremely thin) canvas; nothing larger than
@@ -86,10 +119,9 @@ MAX_IMAGE_SIDE = 16384
 MAX_IMAGE_PIXELS = 1 << 26
 
 
-def preprocess(image: bytes | np.ndarray, cfg: ClipConfig) -> np.ndarray:
-    """Encoded image bytes (PNG/JPEG/...) or an HxWx3 uint8 array -> float32 [3, S, S] normalised.
-    LLaVA-1.5 "pad" aspect: pad to a square with the mean colour, resize to image_size. Images larger
-    than a few times image_size are first downscaled (aspect kept), so the padded canvas stays small."""
+def _decode(image: bytes | np.ndarray):
+    """Encoded image bytes (PNG/JPEG/...) or an HxWx3 uint8 array -> RGB PIL image, size-checked
+    from the header before any pixel is decoded."""
     from PIL import Image
     if isinstance(image, (bytes, bytearray)):
         try:
@@ -109,21 +141,84 @@ def preprocess(image: bytes | np.ndarray, cfg: ClipConfig) -> np.ndarray:
         if a.ndim != 3 or max(a.shape[:2]) > MAX_IMAGE_SIDE or a.shape[0] * a.shape[1] > MAX_IMAGE_PIXELS:
             raise VisionError(f"image array of shape {a.shape} exceeds the limits")
         im = Image.fromarray(a)
-    im = im.convert("RGB")
+    return im.convert("RGB")
+
+
+def _cap(im, cap: int):
+    """Downscale (aspect kept) so the longer side is at most `cap`: later resizes go below it anyway."""
+    from PIL import Image
     w, h = im.size
-    cap = 4 * cfg.image_size  # the final resize goes to image_size: nothing above this survives anyway
     if max(w, h) > cap:
         f = cap / max(w, h)
         im = im.resize((max(1, round(w * f)), max(1, round(h * f))), Image.BICUBIC)
-        w, h = im.size
+    return im
+
+
+def _normalise(im, cfg: ClipConfig) -> np.ndarray:
+    a = np.asarray(im, dtype=np.float32) / 255.0
+    a = (a - np.asarray(cfg.mean, np.float32)) / np.asarray(cfg.std, np.float32)
+    return np.ascontiguousarray(a.transpose(2, 0, 1))
+
+
+def preprocess(image: bytes | np.ndarray, cfg: ClipConfig) -> np.ndarray:
+    """Encoded image bytes (PNG/JPEG/...) or an HxWx3 uint8 array -> float32 [3, S, S] normalised.
+    LLaVA-1.5 "pad" aspect: pad to a square with the mean colour, resize to image_size. Images larger
+    than a few times image_size are first downscaled (aspect kept), so the padded canvas stays small."""
+    from PIL import Image
+    im = _cap(_decode(image), 4 * cfg.image_size)
+    w, h = im.size
     side = max(w, h)
     bg = tuple(int(round(255 * m)) for m in cfg.mean)
     sq = Image.new("RGB", (side, side), bg)
     sq.paste(im, ((side - w) // 2, (side - h) // 2))
-    sq = sq.resize((cfg.image_size, cfg.image_size), Image.BICUBIC)
-    a = np.asarray(sq, dtype=np.float32) / 255.0
-    a = (a - np.asarray(cfg.mean, np.float32)) / np.asarray(cfg.std, np.float32)
-    return np.ascontiguousarray(a.transpose(2, 0, 1))
+    return _normalise(sq.resize((cfg.image_size, cfg.image_size), Image.BICUBIC), cfg)
+
+
+def select_best_resolution(size: tuple[int, int], grid: tuple[tuple[int, int], ...]) -> tuple[int, int]:
+    """The grid (w, h) that keeps the most of the image's pixels when it is fitted in (aspect kept),
+    ties broken by the least canvas left empty (LLaVA-NeXT any-resolution selection)."""
+    w, h = size
+    best, key = grid[0], None
+    for W, H in grid:
+        f = min(W / w, H / h)
+        kept = min(int(w * f) * int(h * f), w * h)
+        k = (kept, -(W * H - kept))
+        if key is None or k > key:
+            best, key = (W, H), k
+    return best
+
+
+def preprocess_anyres(image: bytes | np.ndarray, cfg: ClipConfig):
+    """LLaVA-1.6 views of one image -> (float32 [1 + tiles, 3, S, S], original (w, h), grid (W, H)).
+    View 0 is the whole image resized to S x S; then the image fitted (aspect kept, centred on black)
+    into the best grid resolution and cut into S x S tiles, row-major."""
+    from PIL import Image
+    S = cfg.image_size
+    im = _decode(image)
+    w, h = im.size
+    W, H = select_best_resolution((w, h), cfg.grid_pinpoints)
+    im = _cap(im, 2 * max(W, H))
+    fw, fh = W / w, H / h
+    nw, nh = (W, min(math.ceil(h * fw), H)) if fw < fh else (min(math.ceil(w * fh), W), H)
+    canvas = Image.new("RGB", (W, H), (0, 0, 0))
+    canvas.paste(im.resize((nw, nh), Image.BICUBIC), ((W - nw) // 2, (H - nh) // 2))
+    views = [_normalise(im.resize((S, S), Image.BICUBIC), cfg)]
+    for r in range(H // S):
+        for c in range(W // S):
+            views.append(_normalise(canvas.crop((c * S, r * S, (c + 1) * S, (r + 1) * S)), cfg))
+    return np.stack(views), (w, h), (W, H)
+
+
+def unpad_grid(t: torch.Tensor, size: tuple[int, int]) -> torch.Tensor:
+    """[rows, cols, D] patch grid of the fitted canvas -> the rows / columns that cover the image
+    (the black bands added to reach the grid's aspect are dropped)."""
+    w, h = size
+    rows, cols = t.shape[:2]
+    if w / h > cols / rows:  # image wider than the grid: bands above and below
+        pad = (rows - int(round(h * (cols / w), 7))) // 2
+        return t[pad:rows - pad]
+    pad = (cols - int(round(w * (rows / h), 7))) // 2
+    return t[:, pad:cols - pad]
 
 
 class _NativeTower:
@@ -271,6 +366,8 @@ class ClipEncoder:
                     "attn_out.weight", "attn_out.bias", "ln1.weight", "ln1.bias", "ln2.weight", "ln2.bias",
                     "ffn_up.weight", "ffn_up.bias", "ffn_down.weight", "ffn_down.bias")})
             self.mm = [(t("mm.0.weight"), t("mm.0.bias")), (t("mm.2.weight"), t("mm.2.bias"))]
+            nl = opt("model.image_newline")
+            self.newline = nl.float().reshape(-1) if nl is not None else None
         finally:
             g.close()
         if self.pos.shape[0] != self.cfg.n_patches + 1:
@@ -328,7 +425,20 @@ class ClipEncoder:
         return x.float()
 
     def encode(self, image: bytes | np.ndarray) -> torch.Tensor:
-        return self.encode_pixels(preprocess(image, self.cfg))
+        """One image -> [rows, out_dim] fp32 embedding rows (n_patches for LLaVA-1.5; base view + the
+        stitched tile grid for a LLaVA-1.6 any-resolution projector)."""
+        if not self.cfg.grid_pinpoints:
+            return self.encode_pixels(preprocess(image, self.cfg))
+        views, size, (W, H) = preprocess_anyres(image, self.cfg)
+        feats = [self.encode_pixels(v) for v in views]
+        if self.cfg.merge == "flat":
+            return torch.cat(feats)
+        S, g = self.cfg.image_size, self.cfg.image_size // self.cfg.patch_size
+        gh, gw, D = H // S, W // S, feats[0].shape[1]
+        grid = torch.stack(feats[1:]).view(gh, gw, g, g, D).permute(0, 2, 1, 3, 4).reshape(gh * g, gw * g, D)
+        grid = unpad_grid(grid, size)
+        nl = self.newline.to(grid.device).view(1, 1, D).expand(grid.shape[0], 1, D)
+        return torch.cat([feats[0], torch.cat([grid, nl], 1).reshape(-1, D)])
 
 
 ID_BUCKETS = 500_000  # id ranges of MAX_PATCHES_PER_IMAGE: |id| < 2^31
@@ -433,9 +543,10 @@ def reference_encode(path: str, px: np.ndarray) -> np.ndarray:
 
 def write_random_clip_gguf(path: str, out_dim: int, image_size: int = 336, patch_size: int = 14, E: int = 1024,
                            F_: int = 4096, n_layer: int = 23, n_head: int = 16, seed: int = 0,
-                           use_gelu: bool = False) -> None:
+                           use_gelu: bool = False, grid_pinpoints=None, merge: str = "spatial_unpad") -> None:
     """Random-init LLaVA-1.5-shaped projector file (F16 matrices, F32 norms/biases), as llama.cpp's
-    llava surgery writes it. Defaults: CLIP ViT-L/14-336 with 23 of 24 blocks, 4096-wide MLP projector."""
+    llava surgery writes it. Defaults: CLIP ViT-L/14-336 with 23 of 24 blocks, 4096-wide MLP projector.
+    grid_pinpoints [(w, h), ...] makes it LLaVA-1.6-shaped (any-resolution metadata + image_newline)."""
     from ..gguf.constants import GGMLType
     from ..gguf.writer import GGUFWriter
     rng = np.random.default_rng(seed)
@@ -448,6 +559,9 @@ def write_random_clip_gguf(path: str, out_dim: int, image_size: int = 336, patch
           "clip.vision.attention.layer_norm_epsilon": 1e-5,
           "clip.vision.image_mean": [0.48145466, 0.4578275, 0.40821073],
           "clip.vision.image_std": [0.26862954, 0.26130258, 0.27577711]}
+    if grid_pinpoints:
+        md["clip.vision.image_grid_pinpoints"] = [int(v) for wh in grid_pinpoints for v in wh]
+        md["clip.vision.mm_patch_merge_type"] = merge
     for k, v in md.items():
         w.add(k, v)
     n_pos = (image_size // patch_size) ** 2 + 1
@@ -478,4 +592,6 @@ def write_random_clip_gguf(path: str, out_dim: int, image_size: int = 336, patch
     add("mm.0.bias", (out_dim,), 0.02, f16=False)
     add("mm.2.weight", (out_dim, out_dim), 1.0 / math.sqrt(out_dim))
     add("mm.2.bias", (out_dim,), 0.02, f16=False)
+    if grid_pinpoints and merge == "spatial_unpad":
+        add("model.image_newline", (out_dim,), 0.5, f16=False)
     w.write()

@@ -173,7 +173,7 @@ class ModelManager:
             dev = self.tp_world.device if self.tp_world is not None else (self.device or (
                 "cuda" if _cuda_available() else "cpu"))
             vision = ClipEncoder(self.store.blob_path(pl["digest"]), dev)
-            ext_rows = int(os.environ.get("OMX_IMAGE_ROWS", str(8 * vision.cfg.n_patches)))
+            ext_rows = int(os.environ.get("OMX_IMAGE_ROWS", str(8 * vision.cfg.max_rows)))
         scheduler = None
         # continuous batching (Ollama OLLAMA_NUM_PARALLEL): parallel rows + as many idle sequences
         # kept for prefix reuse; KV is sized for all of them at full context (288 GB HBM)

@@ -11,7 +11,8 @@ import numpy as np
 import pytest
 import torch
 
-from ollama_operator_amd.models.clip import (ClipEncoder, VisionError, ImageIds, preprocess,
+from ollama_operator_amd.models.clip import (ClipEncoder, VisionError, ImageIds, preprocess, preprocess_anyres,
+                                             select_best_resolution,
                                              reference_encode, write_random_clip_gguf)
 
 E_LLM = 256  # tiny-llama n_embd
@@ -233,3 +234,91 @@ def test_images_rejected_without_projector(llava_client):
 def test_show_lists_clip_family(llava_client):
     d = llava_client.post("/api/show", json={"model": "tiny-llava"}).json()
     assert "clip" in (d.get("details", {}).get("families") or [])
+
+
+# ------------------------------------------------------------------ LLaVA-1.6 any-resolution
+PINS = [(28, 56), (56, 28), (56, 56)]
+
+
+@pytest.fixture(scope="module")
+def anyres_clip(tmp_path_factory):
+    p = str(tmp_path_factory.mktemp("clip16") / "mmproj.gguf")
+    write_random_clip_gguf(p, out_dim=E_LLM, image_size=28, patch_size=7, E=64, F_=128, n_layer=2, n_head=4, seed=4,
+                           grid_pinpoints=PINS)
+    return p
+
+
+def test_select_best_resolution_llava16_grid():
+    grid = [(336, 672), (672, 336), (672, 672), (1008, 336), (336, 1008)]
+    assert select_best_resolution((400, 200), grid) == (672, 336)  # keeps every pixel with the least waste
+    assert select_best_resolution((200, 400), grid) == (336, 672)
+    assert select_best_resolution((1000, 1000), grid) == (672, 672)  # most pixels kept
+    assert select_best_resolution((2000, 500), grid) == (1008, 336)
+    assert select_best_resolution((20, 30), PINS) == (28, 56)
+
+
+def test_anyres_preprocess_views_and_padding(anyres_clip):
+    enc = ClipEncoder(anyres_clip, "cpu")
+    c = enc.cfg
+    assert c.grid_pinpoints == tuple(PINS) and c.merge == "spatial_unpad"
+    assert c.max_rows == 16 + 8 * 9  # base 4x4 + the 56x56 grid (8 x 8 patches + a newline per row)
+    img = np.full((30, 20, 3), 200, np.uint8)  # 20 wide, 30 tall -> grid 28 x 56 (two tiles stacked)
+    views, size, grid = preprocess_anyres(img, c)
+    assert views.shape == (3, 3, 28, 28) and size == (20, 30) and grid == (28, 56)
+    black = (0.0 - np.asarray(c.mean)) / np.asarray(c.std)
+    # fitted 28 x 42, centred: rows 0..6 of the top tile and 49..55 (tile 2 rows 21..27) are black bands
+    assert np.allclose(views[1][:, :7].transpose(1, 2, 0), black, atol=1e-5)
+    assert np.allclose(views[2][:, 21:].transpose(1, 2, 0), black, atol=1e-5)
+    assert not np.allclose(views[1][:, 8], black[:, None], atol=0.1)
+
+
+def _oracle_anyres(path, img, c):
+    """Stitch per-view fp64 oracle features the LLaVA-NeXT way, written independently of ClipEncoder."""
+    from ollama_operator_amd.gguf import read_gguf
+    views, (w, h), (W, H) = preprocess_anyres(img, c)
+    f = [reference_encode(path, v) for v in views]
+    g, S = c.image_size // c.patch_size, c.image_size
+    gw, gh = W // S, H // S
+    rows, cols = gh * g, gw * g
+    full = np.zeros((rows, cols, f[0].shape[1]))
+    for R in range(rows):
+        for C in range(cols):
+            full[R, C] = f[1 + (R // g) * gw + C // g][(R % g) * g + C % g]
+    if w * rows > h * cols:  # wider than the grid: trim rows
+        keep = int(h * cols / w)
+        p = (rows - keep) // 2
+        full = full[p:rows - p]
+    else:
+        keep = int(w * rows / h)
+        p = (cols - keep) // 2
+        full = full[:, p:cols - p]
+    gg = read_gguf(path)
+    nl = np.asarray(gg.array("model.image_newline"), np.float64).reshape(-1)
+    gg.close()
+    out = [f[0]]
+    for r in full:
+        out += [r, nl[None]]
+    return np.concatenate(out)
+
+
+@pytest.mark.parametrize("shape", [(30, 20), (24, 40), (50, 50)])
+def test_anyres_encode_matches_oracle(anyres_clip, shape):
+    enc = ClipEncoder(anyres_clip, "cpu")
+    img = (np.random.default_rng(sum(shape)).random(shape + (3,)) * 255).astype(np.uint8)
+    got = enc.encode(img).numpy()
+    ref = _oracle_anyres(anyres_clip, img, enc.cfg)
+    assert got.shape == ref.shape and got.shape[0] <= enc.cfg.max_rows
+    assert np.linalg.norm(got - ref) / np.linalg.norm(ref) < 1e-4
+
+
+def test_anyres_flat_merge_and_bad_metadata(tmp_path):
+    p = str(tmp_path / "flat.gguf")
+    write_random_clip_gguf(p, out_dim=32, image_size=28, patch_size=14, E=32, F_=64, n_layer=1, n_head=2,
+                           grid_pinpoints=[(56, 28)], merge="flat")
+    enc = ClipEncoder(p, "cpu")
+    assert enc.encode(np.zeros((10, 30, 3), np.uint8)).shape == (12, 32)  # base + 2 tiles, 4 patches each
+    bad = str(tmp_path / "bad.gguf")
+    write_random_clip_gguf(bad, out_dim=32, image_size=28, patch_size=14, E=32, F_=64, n_layer=1, n_head=2,
+                           grid_pinpoints=[(50, 28)])
+    with pytest.raises(VisionError):
+        ClipEncoder(bad, "cpu")

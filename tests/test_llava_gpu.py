@@ -58,3 +58,18 @@ def test_native_clip_tower_matches_oracle(tmp_path, gelu):
     assert np.linalg.norm(got - ref) / np.linalg.norm(ref) < 2e-2
     torch_path = enc.encode_pixels_torch(px).cpu().numpy()
     assert np.linalg.norm(got - torch_path) / np.linalg.norm(torch_path) < 2e-2
+
+
+@pytest.mark.gpu
+def test_native_anyres_matches_cpu(tmp_path):
+    """LLaVA-1.6 any-resolution views through the native tower on the GPU vs the fp32 CPU encoder."""
+    from ollama_operator_amd.models.clip import ClipEncoder, write_random_clip_gguf
+    p = str(tmp_path / "mmproj16.gguf")
+    write_random_clip_gguf(p, out_dim=E_LLM, image_size=168, patch_size=14, E=256, F_=512, n_layer=2, n_head=4,
+                           seed=6, grid_pinpoints=[(168, 336), (336, 168), (336, 336)])
+    gpu, cpu = ClipEncoder(p, "cuda"), ClipEncoder(p, "cpu")
+    assert gpu.native is not None
+    img = (np.random.default_rng(2).random((90, 160, 3)) * 255).astype(np.uint8)
+    a, b = gpu.encode(img).cpu().numpy(), cpu.encode(img).numpy()
+    assert a.shape == b.shape and a.shape[0] > 144
+    assert np.linalg.norm(a - b) / np.linalg.norm(b) < 2e-2
