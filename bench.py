@@ -128,6 +128,12 @@ def bench_server(a, url: str, model_path: str, vocab_words: int = 32000):
             # decode-phase aggregate (what the batched steps deliver); the wall aggregate above also
             # holds the P prefills and request ramp
             out["concurrent_decode_tok_s"] = round(sum(out["concurrent_per_client_tok_s"]), 2)
+            # where the wall time went, per client (server-side Ollama durations, ms)
+            ms = lambda k: [round(x.get(k, 0) / 1e6, 2) for x in res]  # noqa: E731
+            out["concurrent_wall_ms"] = round(wall * 1e3, 2)
+            out["concurrent_total_ms"] = ms("total_duration")
+            out["concurrent_prompt_eval_ms"] = ms("prompt_eval_duration")
+            out["concurrent_eval_ms"] = ms("eval_duration")
     return out
 
 

@@ -535,7 +535,7 @@ bool gemm_eligible(const GemvParams& P) {
 
 // Large-M library path (blas.cpp): dequantise W once into fp16 (in prep_x16's K order), one hipBLASLt
 // GEMM into the fp32 slab yws, then the fused epilogue as for split-K (finalize, one slab)
-static int g_lib_min_m = -1;  // -1: OMX_GEMM_LIB_MIN_M (default 256), read once
+static int g_lib_min_m = -1;  // -1: OMX_GEMM_LIB_MIN_M (default 0 = never; the hand-written dq GEMM runs), read once
 
 int gemm_lib_min_m() {
   if (g_lib_min_m < 0) {

@@ -583,6 +583,7 @@ constexpr size_t dq_lds() { return (size_t)((P3 ? 3 : 2) * BM + 2 * BN) * DQ_BK 
 
 int g_dq_enable = -1;  // -1: OMX_GEMM_DQ (default on), read once
 int g_dq_cfg = -2;     // OMX_DQ_CFG: force tile config 0..3 (microbenchmarks); -2 = not read yet
+int g_dq_sk = 0;       // > 0: force the split-K factor (microbenchmarks, set_dq_tuning)
 int g_dq_pipe = -1;    // OMX_DQ_PIPE: 3 = three-stage pipeline (counted waits), else two-stage; -1 = not read
 
 }  // namespace
@@ -604,6 +605,12 @@ bool dq_gemm_enabled() {
 }
 
 void set_dq_gemm(int on) { g_dq_enable = on ? 1 : 0; }
+
+void set_dq_tuning(int cfg, int sk) {
+  dq_gemm_enabled();  // env defaults read first, then overridden
+  g_dq_cfg = cfg;
+  g_dq_sk = sk;
+}
 
 template <int QT, int BM, int BN, int WM, int WN>
 static void launch_dq(const GemvParams& P, const f16* xp, int Kp, int sk, hipStream_t s) {
@@ -643,6 +650,7 @@ static void run_dq(const GemvParams& P, f16* xp, int Kp, hipStream_t s) {
   int sk = 1;
   if (P.gws && P.gws_elems > 0)
     while (sk < 8 && tiles * sk < 240 && nks / (2 * sk) >= 8 && (long long)(2 * sk) * M * N <= P.gws_elems) sk *= 2;
+  if (g_dq_sk > 0 && P.gws && (long long)g_dq_sk * M * N <= P.gws_elems && nks / g_dq_sk >= 2) sk = g_dq_sk;
   switch (cfg) {
     case 0: launch_dq<QT, 256, 256, 2, 4>(P, xp, Kp, sk, s); break;
     case 1: launch_dq<QT, 256, 128, 4, 2>(P, xp, Kp, sk, s); break;

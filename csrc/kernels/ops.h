@@ -149,6 +149,7 @@ void gemm(const GemvParams& P, hipStream_t s);
 bool dq_gemm(const GemvParams& P, hipStream_t s);
 bool dq_gemm_enabled();
 void set_dq_gemm(int on);
+void set_dq_tuning(int cfg, int sk);  // microbenchmarks: force tile config (-1 auto) and split-K (0 auto)
 void gemm_finalize(const GemvParams& P, int sk, hipStream_t s);  // sums sk split-K slabs + epilogue
 
 // launch-shape knobs for the decode GEMV (tuned on MI355X; see scripts/bench_gemv.py)
