@@ -121,7 +121,10 @@ def build(jobs: int | None = None, clean: bool = False, verbose: bool = False, d
         os.makedirs(os.path.join(build_dir, "ollama_operator_amd"), exist_ok=True)
         out = os.path.join(build_dir, "ollama_operator_amd", os.path.basename(out))
     if not os.path.exists(out) or jobs_list or any(os.path.getmtime(o) > os.path.getmtime(out) for o in objs):
-        link = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", out, *objs, "-lpthread"]
+        # linked beside the target, then renamed: a reader of the tree (a test, a tree snapshot) never
+        # sees a half-written library
+        tmp = out + ".tmp"
+        link = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", tmp, *objs, "-lpthread"]
         tl = _torch_lib()
         if tl:
             link += [f"-L{tl}", f"-Wl,-rpath,{tl}"]
@@ -131,6 +134,7 @@ def build(jobs: int | None = None, clean: bool = False, verbose: bool = False, d
         r = subprocess.run(link, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError("link failed:\n" + " ".join(link) + "\n" + r.stdout + r.stderr)
+        os.replace(tmp, out)
     return out
 
 

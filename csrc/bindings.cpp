@@ -339,6 +339,7 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("mfma_layout_bytes", &mfma_layout_bytes);
   m.def("x8_bytes", [](int K) { return x8_bytes(K); });
+  m.def("x8_stat_ld", [](int K) { return x8_stat_ld(K); });
   m.def("gemv8_ffn", [](py::object wg, py::object wd, uintptr_t img_in, uintptr_t stat, uintptr_t img_f, uintptr_t h,
                         uintptr_t resid, uintptr_t nw, uintptr_t img_out, uintptr_t stat_out, uintptr_t sync, int epi,
                         float eps, uintptr_t stream) {
@@ -522,8 +523,15 @@ PYBIND11_MODULE(_C, m) {
         w.x8q = Pp<void>(ptr("x8q"));
         w.x8_fuse = d.contains("x8_fuse") ? d["x8_fuse"].cast<int>() : 1;
         w.x8_ok = (d.contains("x8_ok") ? d["x8_ok"].cast<int>() : 0) && e.x8_capable() ? 1 : 0;
+        {  // continuous-batching rows on the chain: as many as asked for and every emitter covers
+          const int want = d.contains("x8_bmax") ? d["x8_bmax"].cast<int>() : 1;
+          w.x8_bmax = 1;
+          if (w.x8_ok)
+            for (int b = 2; b <= want && b <= 4 && e.x8_capable(b); ++b) w.x8_bmax = b;
+        }
       })
       .def_property_readonly("x8_on", [](const Executor& e) { return e.ws.x8_ok; })
+      .def_property_readonly("x8_bmax", [](const Executor& e) { return e.ws.x8_ok ? e.ws.x8_bmax : 0; })
       .def_property_readonly("n_attn8", [](const Executor& e) { return e.n_attn8; })
       .def_property_readonly("n_ffn8", [](const Executor& e) { return e.n_ffn8; })
       .def("set_segments", [](Executor& e, std::vector<std::pair<int, int>> segs) { e.segments = std::move(segs); })

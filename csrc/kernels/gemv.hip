@@ -812,8 +812,8 @@ static bool launch_dual_a(const GemvParams& A, const GemvParams& Bp, int need, h
 }
 
 void gemv2(const GemvParams& A0, const GemvParams& B0, hipStream_t s) {
+  if (A0.x8 && gemv8_2(A0, B0, s)) return;  // int8 activation chain (gemv8.hip)
   if (A0.B > 1 && gemv_mb2(A0, B0, s)) return;  // batched decode chain: q,k + v on the matrix cores
-  if (A0.B == 1 && A0.x8 && gemv8_2(A0, B0, s)) return;  // int8 activation chain (gemv8.hip)
   GemvParams A = A0, Bp = B0;
   A.xfirst = Bp.xfirst = g_tune.xfirst;
   const int need = ((A.w.K + 255) / 256 + 15) / 16;
@@ -842,7 +842,7 @@ bool gemv_merge_supported(int B, int K, int D, int S) {
 }
 
 void gemv(const GemvParams& P0, hipStream_t s) {
-  if (P0.B == 1 && (P0.x8 || P0.emit8) && gemv8(P0, s)) return;  // int8 activation chain (gemv8.hip)
+  if ((P0.x8 || P0.emit8) && gemv8(P0, s)) return;  // int8 activation chain (gemv8.hip)
   if (P0.emit8) throw std::runtime_error("gemv: int8 activation emitter not covered by gemv8");
   if (P0.w.qtype == QT_F16) {  // fp16 weights (vision tower): the stream-order GEMM only
     if (!dq_gemm(P0, s)) throw std::runtime_error("gemv: F16 weights need >= 128 rows and an fp16 workspace");

@@ -29,16 +29,19 @@ namespace omx {
 // One block = KS groups of 4 waves on the same 16-row tiles (group kg owns super-blocks
 // [kg * CH, (kg + 1) * CH)); J consecutive tiles per block, every weight load issued up front.
 // MS: merge slabs of IN_MERGE (1 = plain fp32 input, no merge).
-template <int QT, int NSB, int J, int KS, int IN, int MS, int EMIT, bool WT = false>
+// BT: batch rows (continuous batching): every weight tile is read once and dotted with BT activation
+// images (row b of the LDS image at b * XSP slots); rows >= P.B are computed but never stored.
+template <int QT, int NSB, int J, int KS, int IN, int MS, int EMIT, bool WT = false, int BT = 1>
 __device__ __forceinline__ void gemv8_body(const GemvParams& P, const int bx) {
+  static_assert(BT == 1 || MS <= 1, "batched rows take the plain fp32 input (no deferred merge)");
   constexpr int NT = GEMV_NT * KS;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const QMat& w = P.w;
   const int K = w.K, N = w.N, SB = n_sb(K), XS = SB * XPAD, XSP = x8_slots_dev(K);
-  i32x4* lq = (i32x4*)smem;
-  f32x2* lf = (f32x2*)(smem + (size_t)XSP * 16);
-  float* stage = (float*)(lf + XSP);  // [32]: emitted values, their squares
-  float* part = stage + 32;           // [KS - 1][GEMV_NT] partial sums of the K split
+  i32x4* lq = (i32x4*)smem;                           // [BT][XSP]
+  f32x2* lf = (f32x2*)(smem + (size_t)BT * XSP * 16);  // [BT][XSP]
+  float* stage = (float*)(lf + BT * XSP);             // [BT][32]: emitted values, their squares
+  float* part = stage + 32 * BT;                      // [KS - 1][BT][GEMV_NT] partial sums of the K split
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = lane >> 4, s = lane & 15;
   const int kg = KS > 1 ? wave / GEMV_NW : 0, gtid = tid - kg * GEMV_NT;
   const int CH = KS > 1 ? (SB + KS - 1) / KS : SB;
@@ -48,20 +51,28 @@ __device__ __forceinline__ void gemv8_body(const GemvParams& P, const int bx) {
   const int tile0 = bx * J;
 
   // 1. activation operands FIRST (they return ahead of the weight stream)
-  u32x4 xw[X8_NWI];
-  f32x4 stv[X8_NSTW];
+  u32x4 xw[BT][X8_NWI];
+  f32x4 stv[BT][X8_NSTW];
   constexpr int MG = IN == IN_MERGE ? NSB * KS : 1;  // groups per thread of the merge prologue
   constexpr int MSS = MS > 0 ? MS : 1;
-  f32x4 av[MSS][MG][4];
+  constexpr int AR = BT > 1 ? BT : MSS;  // merge slabs (batch 1) or batch rows of plain fp32 input
+  f32x4 av[AR][MG][4];
   f32x2 ml[MSS][MG];
   const int nwords = XSP * 3 / 2;
+  const size_t img_b = (size_t)XSP * 24;
+  const int st_ld = x8_stat_ld_dev(K);
   if constexpr (IN != IN_MERGE) {
 #pragma unroll
-    for (int i = 0; i < X8_NWI; ++i) xw[i] = ((const u32x4*)P.x8)[min(tid + NT * i, nwords - 1)];
+    for (int b = 0; b < BT; ++b)
+#pragma unroll
+      for (int i = 0; i < X8_NWI; ++i)
+        xw[b][i] = ((const u32x4*)((const char*)P.x8 + b * img_b))[min(tid + NT * i, nwords - 1)];
     if constexpr (IN == IN_X8_RMS) {
       const int n4 = K / 64;  // f32x4 of partials (K / 16 floats)
 #pragma unroll
-      for (int i = 0; i < X8_NSTW; ++i) stv[i] = ((const f32x4*)P.x8_stat)[min(lane + 64 * i, n4 - 1)];
+      for (int b = 0; b < BT; ++b)
+#pragma unroll
+        for (int i = 0; i < X8_NSTW; ++i) stv[b][i] = ((const f32x4*)(P.x8_stat + b * st_ld))[min(lane + 64 * i, n4 - 1)];
     }
   } else {
 #pragma unroll
@@ -77,7 +88,9 @@ __device__ __forceinline__ void gemv8_body(const GemvParams& P, const int bx) {
         }
       } else {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) av[0][i][j] = *(const f32x4*)(P.x + 16 * gi + 4 * j);
+        for (int b = 0; b < BT; ++b)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) av[b][i][j] = *(const f32x4*)(P.x + (long long)b * P.ldx + 16 * gi + 4 * j);
       }
     }
   }
@@ -92,74 +105,90 @@ __device__ __forceinline__ void gemv8_body(const GemvParams& P, const int bx) {
   }
   __builtin_amdgcn_sched_barrier(0);
 
-  // 3. the activation image into LDS (the copy waits for the activation loads only)
-  float rstd = 1.f;
+  // 3. the activation images into LDS (the copy waits for the activation loads only); a row's image
+  //    is [XSP] int8 words then [XSP] (d, d * sum q) pairs, split here into the lq / lf planes
+  float rstd[BT];
+#pragma unroll
+  for (int b = 0; b < BT; ++b) rstd[b] = 1.f;
   if constexpr (IN != IN_MERGE) {
 #pragma unroll
-    for (int i = 0; i < X8_NWI; ++i)
-      if (tid + NT * i < nwords) ((u32x4*)smem)[tid + NT * i] = xw[i];
+    for (int b = 0; b < BT; ++b)
+#pragma unroll
+      for (int i = 0; i < X8_NWI; ++i) {
+        const int wd = tid + NT * i;
+        if (wd < nwords) {
+          u32x4* dst = wd < XSP ? (u32x4*)lq + b * XSP + wd : (u32x4*)(lf + b * XSP) + (wd - XSP);
+          *dst = xw[b][i];
+        }
+      }
     if constexpr (IN == IN_X8_RMS) {
       const int n4 = K / 64;
-      float ss = 0.f;
 #pragma unroll
-      for (int i = 0; i < X8_NSTW; ++i)
-        if (lane + 64 * i < n4) ss += stv[i].x + stv[i].y + stv[i].z + stv[i].w;
-      rstd = rsqrtf(wave_sum(ss) / K + P.eps);
+      for (int b = 0; b < BT; ++b) {
+        float ss = 0.f;
+#pragma unroll
+        for (int i = 0; i < X8_NSTW; ++i)
+          if (lane + 64 * i < n4) ss += stv[b][i].x + stv[b][i].y + stv[b][i].z + stv[b][i].w;
+        rstd[b] = rsqrtf(wave_sum(ss) / K + P.eps);
+      }
     }
   } else {
 #pragma unroll
     for (int i = 0; i < MG; ++i) {
       const int gi = tid + NT * i;
-      f32x4 xv[4];
-      if constexpr (MS > 1) {  // flash-decode merge: splits without keys carry m = -inf, l = 0
-        float M = -INFINITY;
 #pragma unroll
-        for (int sp = 0; sp < MS; ++sp) M = fmaxf(M, ml[sp][i].x);
-        float L = 0.f;
-        f32x4 a[4] = {};
+      for (int b = 0; b < BT; ++b) {
+        f32x4 xv[4];
+        if constexpr (MS > 1) {  // flash-decode merge: splits without keys carry m = -inf, l = 0
+          float M = -INFINITY;
 #pragma unroll
-        for (int sp = 0; sp < MS; ++sp) {
-          const float c = ml[sp][i].x == -INFINITY ? 0.f : __expf(ml[sp][i].x - M);
-          L += c * ml[sp][i].y;
+          for (int sp = 0; sp < MS; ++sp) M = fmaxf(M, ml[sp][i].x);
+          float L = 0.f;
+          f32x4 a[4] = {};
 #pragma unroll
-          for (int j = 0; j < 4; ++j) a[j] += c * av[sp][i][j];
+          for (int sp = 0; sp < MS; ++sp) {
+            const float c = ml[sp][i].x == -INFINITY ? 0.f : __expf(ml[sp][i].x - M);
+            L += c * ml[sp][i].y;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) a[j] += c * av[sp][i][j];
+          }
+          const float inv = L > 0.f ? 1.f / L : 0.f;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) xv[j] = a[j] * inv;
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) xv[j] = av[b][i][j];
         }
-        const float inv = L > 0.f ? 1.f / L : 0.f;
+        const int slot = b * XSP + (gi < SB * 16 ? (gi >> 4) * XPAD + (gi & 15) : XS);
+        float v[16];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) xv[j] = a[j] * inv;
-      } else {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) xv[j] = av[0][i][j];
-      }
-      const int slot = gi < SB * 16 ? (gi >> 4) * XPAD + (gi & 15) : XS;
-      float v[16];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        v[4 * j] = xv[j].x; v[4 * j + 1] = xv[j].y; v[4 * j + 2] = xv[j].z; v[4 * j + 3] = xv[j].w;
-      }
-      if (16 * gi >= K) {
-#pragma unroll
-        for (int j = 0; j < 16; ++j) v[j] = 0.f;
-      }
-      float amax = 0.f;
-#pragma unroll
-      for (int j = 0; j < 16; ++j) amax = fmaxf(amax, fabsf(v[j]));
-      const float d = amax / 127.f, id = amax > 0.f ? 127.f / amax : 0.f;
-      int qsum = 0;
-      i32x4 pk;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        int word = 0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int q = (int)rintf(v[4 * j + k] * id);
-          qsum += q;
-          word |= (q & 0xFF) << (8 * k);
+        for (int j = 0; j < 4; ++j) {
+          v[4 * j] = xv[j].x; v[4 * j + 1] = xv[j].y; v[4 * j + 2] = xv[j].z; v[4 * j + 3] = xv[j].w;
         }
-        pk[j] = word;
+        if (16 * gi >= K) {
+#pragma unroll
+          for (int j = 0; j < 16; ++j) v[j] = 0.f;
+        }
+        float amax = 0.f;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) amax = fmaxf(amax, fabsf(v[j]));
+        const float d = amax / 127.f, id = amax > 0.f ? 127.f / amax : 0.f;
+        int qsum = 0;
+        i32x4 pk;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          int word = 0;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int q = (int)rintf(v[4 * j + k] * id);
+            qsum += q;
+            word |= (q & 0xFF) << (8 * k);
+          }
+          pk[j] = word;
+        }
+        lq[slot] = pk;
+        lf[slot] = (f32x2){d, d * (float)qsum};
       }
-      lq[slot] = pk;
-      lf[slot] = (f32x2){d, d * (float)qsum};
     }
     // K padding groups beyond the threads' reach stay whatever they were: every group < SB * 16 is
     // written above (NT * MG >= SB * 16 by the launch rule), the pad / dummy slots are never read
@@ -167,52 +196,75 @@ __device__ __forceinline__ void gemv8_body(const GemvParams& P, const int bx) {
   __syncthreads();
 
   // 4. consume the tiles in issue order; epilogue (+ emission) per tile
+  const int nb = BT > 1 ? min(P.B, BT) : 1;  // rows stored / emitted
 #pragma unroll
   for (int j = 0; j < J; ++j) {
     const int t = tile0 + j;
     if (t >= n_tiles) break;  // block-uniform
-    float acc[1][1] = {{0.f}};
-    compute_wtile<QT, NSB, 1, 1>(T[j], SB, sb0, s, lq, lf, XS, acc, se);
+    float acc[1][BT];
+#pragma unroll
+    for (int b = 0; b < BT; ++b) acc[0][b] = 0.f;
+    compute_wtile<QT, NSB, 1, BT>(T[j], SB, sb0, s, lq, lf, XSP, acc, se);
     if constexpr (KS > 1) {  // partial sums of groups 1.. meet group 0's in LDS
-      if (kg > 0) part[(kg - 1) * GEMV_NT + gtid] = acc[0][0];
+      if (kg > 0) {
+#pragma unroll
+        for (int b = 0; b < BT; ++b) part[((kg - 1) * BT + b) * GEMV_NT + gtid] = acc[0][b];
+      }
       __syncthreads();
       if (kg == 0) {
 #pragma unroll
-        for (int k = 1; k < KS; ++k) acc[0][0] += part[(k - 1) * GEMV_NT + gtid];
+        for (int k = 1; k < KS; ++k)
+#pragma unroll
+          for (int b = 0; b < BT; ++b) acc[0][b] += part[((k - 1) * BT + b) * GEMV_NT + gtid];
       }
     }
-    acc[0][0] *= rstd;
+#pragma unroll
+    for (int b = 0; b < BT; ++b) acc[0][b] *= rstd[b];
     if constexpr (EMIT == EM_NONE) {
-      if (kg == 0) finish_rows<1, 1>(P, acc, t * 16 + rbase, N, 0, s);
+      if (kg == 0) finish_rows<1, BT>(P, acc, t * 16 + rbase, N, 0, s);
     } else {
-      const float v = row16_sum(acc[0][0]);
-      const float pv = __shfl_xor(v, 16, OMX_WAVE);  // row rbase ^ 1 (GLU partner)
       const int n = t * 16 + rbase;
+      float v[BT], pv[BT];
+#pragma unroll
+      for (int b = 0; b < BT; ++b) {
+        v[b] = row16_sum(acc[0][b]);
+        pv[b] = __shfl_xor(v[b], 16, OMX_WAVE);  // row rbase ^ 1 (GLU partner)
+      }
       if constexpr (EMIT == EM_ADD) {
         if (kg == 0 && s == 0) {
-          float nv = 0.f;
-          if (n < N) {
-            float* dst = P.y + n;
-            nv = *dst + v + (P.bias ? P.bias[n] : 0.f);
-            *dst = nv;
+#pragma unroll
+          for (int b = 0; b < BT; ++b) {
+            float nv = 0.f;
+            if (n < N && b < nb) {
+              float* dst = P.y + (long long)b * P.ldy + n;
+              nv = *dst + v[b] + (P.bias ? P.bias[n] : 0.f);
+              *dst = nv;
+            }
+            stage[32 * b + rbase] = n < N ? nv * P.emit8_nw[n] : 0.f;
+            stage[32 * b + 16 + rbase] = nv * nv;
           }
-          stage[rbase] = n < N ? nv * P.emit8_nw[n] : 0.f;
-          stage[16 + rbase] = nv * nv;
         }
         __syncthreads();
-        if (tid == 0) emit_group(P.emit8, N, t, stage, stage + 16, P.emit8_stat);
+        if (tid < nb)
+          emit_group((char*)P.emit8 + (size_t)tid * x8_slots_dev(N) * 24, N, t, stage + 32 * tid, stage + 32 * tid + 16,
+                     P.emit8_stat + tid * x8_stat_ld_dev(N));
         __syncthreads();  // the stage is reused by the next tile
       } else {  // EM_GLU: even row = gate, odd = up; 8 outputs per tile, a group per tile pair
         const int half = (t & 1) * 8;
         if (kg == 0 && s == 0 && (rbase & 1) == 0) {
-          const float h = n < N ? (P.epi == EPI_GEGLU ? gelu_tanh(v) : silu(v)) * pv : 0.f;
-          if (n < N) P.y[n >> 1] = h;
-          stage[half + (rbase >> 1)] = h;
-          if (half == 0 && t + 1 >= n_tiles) stage[8 + (rbase >> 1)] = 0.f;  // trailing half group
+#pragma unroll
+          for (int b = 0; b < BT; ++b) {
+            const float h = n < N ? (P.epi == EPI_GEGLU ? gelu_tanh(v[b]) : silu(v[b])) * pv[b] : 0.f;
+            if (n < N && b < nb) P.y[(long long)b * P.ldy + (n >> 1)] = h;
+            stage[32 * b + half + (rbase >> 1)] = h;
+            if (half == 0 && t + 1 >= n_tiles) stage[32 * b + 8 + (rbase >> 1)] = 0.f;  // trailing half group
+          }
         }
         if ((t & 1) || t + 1 >= n_tiles) {
           __syncthreads();
-          if (tid == 0) emit_group<WT>(P.emit8, N / 2, t >> 1, stage, nullptr, nullptr);
+          if (tid < nb)
+            emit_group<WT>((char*)P.emit8 + (size_t)tid * x8_slots_dev(N / 2) * 24, N / 2, t >> 1, stage + 32 * tid,
+                           nullptr, nullptr);
           __syncthreads();
         }
       }
@@ -221,16 +273,16 @@ __device__ __forceinline__ void gemv8_body(const GemvParams& P, const int bx) {
   }
 }
 
-template <int QT, int NSB, int J, int KS, int IN, int MS, int EMIT>
+template <int QT, int NSB, int J, int KS, int IN, int MS, int EMIT, int BT>
 __global__ __launch_bounds__(GEMV_NT * KS) void qgemv8_kernel(GemvParams P) {
-  gemv8_body<QT, NSB, J, KS, IN, MS, EMIT>(P, blockIdx.x);
+  gemv8_body<QT, NSB, J, KS, IN, MS, EMIT, false, BT>(P, blockIdx.x);
 }
 
 // q,k rows + v rows of different quant types (Q4_K_M QKV) over the same image: one launch
-template <int QA, int QB, int IN>
+template <int QA, int QB, int IN, int BT>
 __global__ __launch_bounds__(GEMV_NT) void qgemv8_dual_kernel(GemvParams PA, GemvParams PB, int gxa) {
-  if ((int)blockIdx.x < gxa) gemv8_body<QA, 1, 1, 1, IN, 0, EM_NONE>(PA, blockIdx.x);
-  else gemv8_body<QB, 1, 1, 1, IN, 0, EM_NONE>(PB, (int)blockIdx.x - gxa);
+  if ((int)blockIdx.x < gxa) gemv8_body<QA, 1, 1, 1, IN, 0, EM_NONE, false, BT>(PA, blockIdx.x);
+  else gemv8_body<QB, 1, 1, 1, IN, 0, EM_NONE, false, BT>(PB, (int)blockIdx.x - gxa);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -304,7 +356,24 @@ __global__ __launch_bounds__(GEMV_NT, 2) void ffn8_kernel(GemvParams PA, GemvPar
 // host side
 namespace {
 
-size_t lds8(int K, int KS) { return x8_bytes(K) + (size_t)(32 + (KS - 1) * GEMV_NT) * 4; }
+size_t lds8(int K, int KS, int BT = 1) { return BT * x8_bytes(K) + (size_t)BT * (32 + (KS - 1) * GEMV_NT) * 4; }
+
+// batch rows per launch: B = 1, 2, or 3-4 (row 3 of a B = 3 launch is computed, never stored)
+int bt_of(int B) { return B <= 2 ? B : 4; }
+
+// 4 rows fit the register budget of 768 / 1024-thread blocks only without the RMS partials and the
+// Q5_K high-bit planes (kernel-resource-usage: these would spill); such launches are not covered
+constexpr bool bt4_ok(int qt, int ks, int in) { return ks <= 2 || (ks == 3 && in != IN_X8_RMS && qt != QT_Q5_K); }
+
+// > 64 KB of LDS (batched rows of a long-K image): raised once per kernel instantiation
+template <typename Kern>
+void lds_attr(Kern k, size_t lds) {
+  static bool done = false;
+  if (lds > 64 * 1024 && !done) {
+    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    done = true;
+  }
+}
 
 int emit_mode(const GemvParams& P) {
   if (!P.emit8) return EM_NONE;
@@ -345,9 +414,10 @@ bool geometry(const GemvParams& P, Geo& G) {
 }
 
 bool covered(const GemvParams& P, Geo& G) {
-  if (P.B != 1 || P.expert_ids || P.w.s0 == nullptr || P.dbg_ts) return false;
+  if (P.B < 1 || P.B > X8_MAX_B || P.expert_ids || P.w.s0 == nullptr || P.dbg_ts) return false;
   const int em = emit_mode(P), in = in_mode(P);
   if (em < 0 || in < 0) return false;
+  if (P.B > 1 && in == IN_MERGE && P.merge_S > 0) return false;  // batched rows: plain fp32 attention rows
   if (!P.x8 && !P.emit8) return false;  // nothing for this path to do
   if (in == IN_MERGE && P.merge_S > 0 && !(P.merge_S == 2 || P.merge_S == 4 || P.merge_S == 8)) return false;
   if (in == IN_MERGE && (P.w.K > 4096 * 1 || P.w.K % 16)) return false;  // merge prologue: one group per thread
@@ -359,17 +429,39 @@ bool covered(const GemvParams& P, Geo& G) {
   if (!geometry(P, G)) return false;
   if (em == EM_GLU && G.J != 2) return false;  // a block owns whole groups: two tiles, unsplit K
   if (in != IN_MERGE && (size_t)G.ks * GEMV_NT * X8_NWI * 16 < x8_bytes(P.w.K)) return false;
-  return lds8(P.w.K, G.ks) <= 64 * 1024;
+  if (bt_of(P.B) == 4 && !bt4_ok(q, G.ks, in)) return false;
+  return lds8(P.w.K, G.ks, bt_of(P.B)) <= (P.B > 1 ? 160 : 64) * 1024;
+}
+
+template <int QT, int NSB, int J, int KS, int IN, int MS, int EMIT, int BT>
+void launch_k(const GemvParams& P, int grid, hipStream_t s) {
+  const size_t lds = lds8(P.w.K, KS, BT);
+  auto k = qgemv8_kernel<QT, NSB, J, KS, IN, MS, EMIT, BT>;
+  lds_attr(k, lds);
+  hipLaunchKernelGGL(k, dim3(grid), dim3(GEMV_NT * KS), lds, s, P);
+}
+
+template <int QT, int NSB, int J, int KS, int IN, int MS, int BT>
+void launch_em_bt(const GemvParams& P, int em, int grid, hipStream_t s) {
+  if (em == EM_ADD) launch_k<QT, NSB, J, KS, IN, MS, EM_ADD, BT>(P, grid, s);
+  else if (em == EM_GLU) {
+    if constexpr (J == 2) launch_k<QT, NSB, J, KS, IN, MS, EM_GLU, BT>(P, grid, s);
+  } else launch_k<QT, NSB, J, KS, IN, MS, EM_NONE, BT>(P, grid, s);
 }
 
 template <int QT, int NSB, int J, int KS, int IN, int MS>
 void launch_em(const GemvParams& P, int em, int grid, hipStream_t s) {
-  const size_t lds = lds8(P.w.K, KS);
-  const dim3 g(grid), b(GEMV_NT * KS);
-  if (em == EM_ADD) hipLaunchKernelGGL((qgemv8_kernel<QT, NSB, J, KS, IN, MS, EM_ADD>), g, b, lds, s, P);
-  else if (em == EM_GLU) {
-    if constexpr (J == 2) hipLaunchKernelGGL((qgemv8_kernel<QT, NSB, J, KS, IN, MS, EM_GLU>), g, b, lds, s, P);
-  } else hipLaunchKernelGGL((qgemv8_kernel<QT, NSB, J, KS, IN, MS, EM_NONE>), g, b, lds, s, P);
+  if constexpr (MS > 1) {
+    launch_em_bt<QT, NSB, J, KS, IN, MS, 1>(P, em, grid, s);
+  } else {
+    switch (bt_of(P.B)) {
+      case 1: launch_em_bt<QT, NSB, J, KS, IN, MS, 1>(P, em, grid, s); break;
+      case 2: launch_em_bt<QT, NSB, J, KS, IN, MS, 2>(P, em, grid, s); break;
+      default:
+        if constexpr (bt4_ok(QT, KS, IN)) launch_em_bt<QT, NSB, J, KS, IN, MS, 4>(P, em, grid, s);
+        break;
+    }
+  }
 }
 
 template <int QT, int NSB, int J, int KS>
@@ -402,11 +494,27 @@ bool launchable(const GemvParams& P, const Geo& G) {
   return in_mode(P) != IN_MERGE || (G.ks == 1 && G.nsb == 1 && G.J == 1);
 }
 
+template <int QA, int QB, int IN, int BT>
+void launch_dual_k(const GemvParams& A, const GemvParams& B, int gxa, int gxb, hipStream_t s) {
+  const size_t lds = lds8(A.w.K, 1, BT);
+  auto k = qgemv8_dual_kernel<QA, QB, IN, BT>;
+  lds_attr(k, lds);
+  hipLaunchKernelGGL(k, dim3(gxa + gxb), dim3(GEMV_NT), lds, s, A, B, gxa);
+}
+
+template <int QA, int QB, int IN>
+void launch_dual_in(const GemvParams& A, const GemvParams& B, int gxa, int gxb, hipStream_t s) {
+  switch (bt_of(A.B)) {
+    case 1: launch_dual_k<QA, QB, IN, 1>(A, B, gxa, gxb, s); break;
+    case 2: launch_dual_k<QA, QB, IN, 2>(A, B, gxa, gxb, s); break;
+    default: launch_dual_k<QA, QB, IN, 4>(A, B, gxa, gxb, s); break;
+  }
+}
+
 template <int QA, int QB>
 void launch_dual(const GemvParams& A, const GemvParams& B, int gxa, int gxb, hipStream_t s) {
-  const size_t lds = lds8(A.w.K, 1);
-  if (A.x8_stat) hipLaunchKernelGGL((qgemv8_dual_kernel<QA, QB, IN_X8_RMS>), dim3(gxa + gxb), dim3(GEMV_NT), lds, s, A, B, gxa);
-  else hipLaunchKernelGGL((qgemv8_dual_kernel<QA, QB, IN_X8>), dim3(gxa + gxb), dim3(GEMV_NT), lds, s, A, B, gxa);
+  if (A.x8_stat) launch_dual_in<QA, QB, IN_X8_RMS>(A, B, gxa, gxb, s);
+  else launch_dual_in<QA, QB, IN_X8>(A, B, gxa, gxb, s);
 }
 
 template <int QA>
@@ -469,7 +577,7 @@ bool ffn_b(const GemvParams& G, const GemvParams& D, const Handoff& H, hipStream
 
 bool gemv8_ffn(const GemvParams& G, const GemvParams& D, void* sync, hipStream_t s) {
   Geo GG, GD;
-  if (!sync || !covered(G, GG) || !covered(D, GD)) return false;
+  if (!sync || G.B != 1 || !covered(G, GG) || !covered(D, GD)) return false;
   if (emit_mode(G) != EM_GLU || in_mode(G) != IN_X8_RMS || GG.nsb != 1 || GG.ks != 1 || GG.J != 2) return false;
   if (emit_mode(D) != EM_ADD || in_mode(D) != IN_X8 || D.x8 != G.emit8 || D.w.K != G.w.N / 2) return false;
   if ((size_t)FFN_IMG_DW * GEMV_NT * 4 < x8_bytes(D.w.K)) return false;
@@ -505,7 +613,7 @@ bool gemv8(const GemvParams& P, hipStream_t s) {
 
 bool gemv8_2(const GemvParams& A, const GemvParams& B, hipStream_t s) {
   Geo GA, GB;
-  if (!A.x8 || !B.x8 || A.x8 != B.x8 || A.emit8 || B.emit8 || A.w.K != B.w.K) return false;
+  if (!A.x8 || !B.x8 || A.x8 != B.x8 || A.emit8 || B.emit8 || A.w.K != B.w.K || A.B != B.B) return false;
   if (!covered(A, GA) || !covered(B, GB) || GA.nsb != 1 || GA.ks != 1 || GB.nsb != 1 || GB.ks != 1) return false;
   const int gxa = (A.w.N + 15) / 16, gxb = (B.w.N + 15) / 16;  // one tile per block on both sides
   switch (A.w.qtype) {

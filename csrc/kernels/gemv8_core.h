@@ -10,6 +10,11 @@ enum { EM_NONE = 0, EM_ADD = 1, EM_GLU = 2 };
 
 __device__ __forceinline__ int x8_slots_dev(int K) { return ((n_sb(K) * XPAD + 1) + 1) & ~1; }
 
+// batched rows (continuous batching, B = 2..X8_MAX_B): row b's image at b * x8_bytes(K), its RMS
+// partials at b * x8_stat_ld(K) floats (ops.h; 16-B aligned rows)
+constexpr int X8_MAX_B = 4;
+__device__ __forceinline__ int x8_stat_ld_dev(int K) { return ((K >> 4) + 3) & ~3; }
+
 constexpr int X8_NWI = 3;   // 16-byte image words per thread (K <= 16384 at 256 threads x KS)
 constexpr int X8_NSTW = 2;  // f32x4 RMS partials per lane (K <= 8192)
 

@@ -100,6 +100,7 @@ struct GemvParams {
 // with one pad slot per 256-element super-block and a trailing dummy slot (the GEMV's LDS layout)
 inline int x8_slots(int K) { return ((((K + 255) / 256) * 17 + 1) + 1) & ~1; }
 inline size_t x8_bytes(int K) { return (size_t)x8_slots(K) * 24; }
+inline int x8_stat_ld(int K) { return ((K >> 4) + 3) & ~3; }  // RMS-partial floats per batch row
 // batch-1 decode GEMV on the int8 activation chain; false = not covered (caller takes gemv.hip)
 bool gemv8(const GemvParams& P, hipStream_t s);
 bool gemv8_2(const GemvParams& A, const GemvParams& B, hipStream_t s);  // q,k + v rows, one launch

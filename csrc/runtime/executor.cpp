@@ -30,7 +30,7 @@ static GemvParams base_params(const QMat& w, int B, const float* x, int ldx, con
 // the consumer (gate_up, next QKV, LM head) reads them straight from global memory and applies
 // rsqrt(mean + eps) to its outputs -- no per-block activation staging, no separate norm launch.
 bool Executor::chain(const StepInputs& in) const {
-  return ws.mb_ok && mb_enabled() && in.B >= 3 && in.B <= MB_CHAIN_MAX && !in.prefill && cfg.tp == 1 && cfg.arch == 0 &&
+  return !x8(in) && ws.mb_ok && mb_enabled() && in.B >= 3 && in.B <= MB_CHAIN_MAX && !in.prefill && cfg.tp == 1 && cfg.arch == 0 &&
          cfg.n_expert == 0 && ws.xa16 && ws.h16 && ws.a16 && ws.st[0] && ws.st[1];
 }
 
@@ -75,11 +75,13 @@ bool Executor::chain_capable() const {
   return ok(lm_head, EPI_STORE, NORM_RMS, true, false);
 }
 
-// Batch-1 int8 activation chain (gemv8.hip): O and down emit the next RMSNorm'd GEMV's input as an int8
-// image (+ sum-of-squares partials), gate_up emits down's; consumers skip the fp32 activation prologue.
-// Layer 0's QKV reads the embedding rows through gemv.hip's prologue.
+// Int8 activation chain (gemv8.hip): O and down emit the next RMSNorm'd GEMV's input as an int8 image
+// (+ sum-of-squares partials), gate_up emits down's; consumers skip the fp32 activation prologue.
+// Layer 0's QKV reads the embedding rows through gemv.hip's prologue. Batch 1, and up to ws.x8_bmax
+// (<= X8_MAX_B) continuous-batching rows, which then read each weight tile once for every row.
 bool Executor::x8(const StepInputs& in) const {
-  return ws.x8_ok && in.B == 1 && !in.prefill && cfg.tp == 1 && cfg.arch == 0 && cfg.n_expert == 0;
+  return ws.x8_ok && (in.B == 1 || in.B <= ws.x8_bmax) && !in.prefill && cfg.tp == 1 && cfg.arch == 0 &&
+         cfg.n_expert == 0;
 }
 
 static void x8_in(GemvParams& P, const void* img, const float* stat) {
@@ -96,27 +98,27 @@ static void x8_emit(GemvParams& P, void* img, const float* nw, float* stat) {
 // consumers fall back to gemv.hip's fp32 prologue on their own (the producers keep writing the fp32
 // residual / GLU rows too); an emitter the int8 kernel does not cover would leave its consumer a stale
 // image, so the chain is on only when every emitter is covered
-bool Executor::x8_capable() const {
+bool Executor::x8_capable(int B) const {
   if (cfg.tp != 1 || cfg.arch != 0 || cfg.n_expert != 0 || layers.empty() || !ws.x8e || !ws.x8f || !ws.x8st)
     return false;
   static const float dummy[4] = {0.f, 0.f, 0.f, 0.f};
   for (const LayerW& L : layers) {
     GemvParams O{};
     O.w = L.wo;
-    O.B = 1;
+    O.B = B;
     O.epi = EPI_ADD;
     O.n_sel = 1;
     x8_emit(O, (void*)dummy, dummy, (float*)dummy);
     GemvParams G{};
     G.w = L.wgu;
-    G.B = 1;
+    G.B = B;
     G.epi = cfg.glu_act ? EPI_GEGLU : EPI_GLU;
     G.n_sel = 1;
     x8_in(G, dummy, dummy);
     G.emit8 = (void*)dummy;
     GemvParams D{};
     D.w = L.wdown;
-    D.B = 1;
+    D.B = B;
     D.epi = EPI_ADD;
     D.n_sel = 1;
     x8_in(D, dummy, nullptr);
@@ -160,7 +162,7 @@ void Executor::attn_block(int i, const StepInputs& in, hipStream_t s) {
   const bool q8 = x8(in);
   if (ch && i > 0) chain_in(P, ws.xa16, ws.ld_e, ws.st[1], (E + 15) / 16);  // emitted by layer i-1's down
   if (q8 && i > 0) x8_in(P, ws.x8e, ws.x8st);                                 // emitted by layer i-1's down
-  if (q8 && i > 0 && ws.attn_fuse && ws.x8q && !phi) {  // QKV + attention + O in one launch (attn8.hip)
+  if (q8 && i > 0 && B == 1 && ws.attn_fuse && ws.x8q && !phi) {  // QKV + attention + O in one launch (attn8.hip)
     GemvParams V{};
     if (!L.qkv_fused) {
       V = P;
@@ -413,7 +415,7 @@ void Executor::ffn_block(int i, const StepInputs& in, hipStream_t s) {
   if (q8) {
     x8_in(Dn, ws.x8f, nullptr);
     x8_emit(Dn, ws.x8e, i + 1 < (int)layers.size() ? layers[i + 1].attn_norm : out_norm, ws.x8st);
-    if (ws.x8_fuse && gemv8_ffn(G, Dn, ws.x8sync, s)) {  // one launch, in-kernel hand-off
+    if (ws.x8_fuse && B == 1 && gemv8_ffn(G, Dn, ws.x8sync, s)) {  // one launch, in-kernel hand-off
       ++n_ffn8;
       return;
     }
@@ -441,7 +443,7 @@ void Executor::head(const StepInputs& in, hipStream_t s) {
   P.ldy = lm_head.N;
   if (chain(in) && x == ws.resid && in.n_logits == in.B && cfg.n_layer > 0)
     chain_in(P, ws.xa16, ws.ld_e, ws.st[1], (E + 15) / 16);
-  if (x8(in) && x == ws.resid && in.n_logits == 1 && cfg.n_layer > 0) x8_in(P, ws.x8e, ws.x8st);
+  if (x8(in) && x == ws.resid && in.n_logits == in.B && cfg.n_layer > 0) x8_in(P, ws.x8e, ws.x8st);
   gemv(P, s);
 }
 

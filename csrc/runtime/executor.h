@@ -93,6 +93,7 @@ struct Workspace {
   void* x8q = nullptr;       // int8 image of the attention output (the O projection's input, attn8)
   int attn_fuse = 0;         // this step: QKV + attention + O in one launch (attn8; B == 1, short context)
   int x8_ok = 0;
+  int x8_bmax = 1;           // batch rows the chain takes (continuous batching: up to X8_MAX_B)
   int x8_fuse = 1;           // gate_up -> down in one launch (gemv8_ffn) when covered
 };
 constexpr int MB_CHAIN_MAX = 16;
@@ -135,7 +136,7 @@ class Executor {
   void forward_tp(const StepInputs& in, hipStream_t s);  // tp > 1, custom all-reduce (graph-capturable)
   bool ar_fits(int B) const;                             // decode batch B fits the AR slabs
   bool chain_capable() const;                            // every projection takes the fp16 matrix-core chain
-  bool x8_capable() const;                               // every emitter of the int8 chain takes gemv8
+  bool x8_capable(int B = 1) const;                               // every emitter of the int8 chain takes gemv8
   StepInputs bound{};                                    // pre-bound step inputs (set_inputs)
   long long n_attn8 = 0, n_ffn8 = 0;                     // fused launches enqueued (tests: the path ran)
   // batched admission (Runner.admit_many): the rows of a prefill step are several sequences' contiguous

@@ -99,7 +99,8 @@ class NativeExec:
         if not b:
             return {}
         return dict(x8e=b["x8e"].data_ptr(), x8f=b["x8f"].data_ptr(), x8st=b["x8st"].data_ptr(), x8q=b["x8q"].data_ptr(),
-                    x8sync=b["x8sync"].data_ptr(), x8_ok=1, x8_fuse=int(os.environ.get("OMX_X8_FUSE", "0") != "0"))
+                    x8sync=b["x8sync"].data_ptr(), x8_ok=1, x8_fuse=int(os.environ.get("OMX_X8_FUSE", "0") != "0"),
+                    x8_bmax=int(os.environ.get("OMX_X8_BATCH", "4")))
 
     def ar_fits(self, B: int) -> bool:
         return self.exe.ar_fits(B)
@@ -204,8 +205,9 @@ class Runner:
         if self.is_gpu and os.environ.get("OMX_X8", "1") != "0":
             C = native()
             u8 = dict(device=dev, dtype=torch.uint8)
-            self.x8_bufs = dict(x8e=torch.zeros(C.x8_bytes(E), **u8), x8f=torch.zeros(C.x8_bytes(Fl), **u8),
-                                x8st=torch.zeros((E + 15) // 16 + 4, **f32),
+            nb = 4  # batch rows of the chain (gemv8.hip X8_MAX_B): row b's image at b * x8_bytes
+            self.x8_bufs = dict(x8e=torch.zeros(nb * C.x8_bytes(E), **u8), x8f=torch.zeros(nb * C.x8_bytes(Fl), **u8),
+                                x8st=torch.zeros(nb * C.x8_stat_ld(E) + 4, **f32),
                                 x8q=torch.zeros(C.x8_bytes(Eq), **u8),
                                 x8sync=torch.zeros(128, device=dev, dtype=torch.int32))
         self.attn_fuse = os.environ.get("OMX_ATTN_FUSE", "0") != "0"

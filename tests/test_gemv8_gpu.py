@@ -219,3 +219,98 @@ def test_fused_ffn_matches_two_launches(qd):
     hr = torch.nn.functional.silu(gu[0::2]) * gu[1::2]
     ref = r0[0] + hr @ md.w.T
     assert rel(r2[0] - r0[0], ref - r0[0]) < 2e-2
+
+
+# ------------------------------------------------------------------ continuous-batching rows (B = 2..4)
+def images(xs, nw=None):
+    """B rows -> the batched image buffer (row b at b * x8_bytes(K)) and RMS partials (stride x8_stat_ld)."""
+    K = xs.shape[1]
+    ld = C().x8_stat_ld(K)
+    imgs, sts = [], torch.zeros(xs.shape[0] * ld + 4, device="cuda")
+    for b in range(xs.shape[0]):
+        img, st = make_image(xs[b], nw)
+        imgs.append(img)
+        sts[b * ld:b * ld + K // 16] = st[:K // 16]
+    return torch.cat(imgs), sts
+
+
+@pytest.mark.parametrize("B", [2, 3, 4])
+def test_batched_rows_consumer_and_producers(B):
+    """Every chain kernel with B rows: RMS consumer (QKV / gate_up / head shape), GLU producer, residual
+    producer (down, K split over 3 wave groups) and the O projection on plain fp32 attention rows -- each
+    row equal to its own fp32 reference, emitted images per row."""
+    E, F = 4096, 11008
+    x = torch.randn(B, E, device="cuda") * 2
+    nw = torch.rand(E, device="cuda") + 0.5
+    img, st = images(x, nw)
+    xn = x * torch.rsqrt(x.pow(2).mean(1, keepdim=True) + 1e-5) * nw
+    # consumer (store)
+    m = QM(GGMLType.Q4_K, 1024, E, seed=31)
+    y = torch.zeros(B, 1024, device="cuda")
+    call(m, B, None, y, EPI_STORE, {"x8": img.data_ptr(), "x8_stat": st.data_ptr()})
+    assert rel(y, xn @ m.w.T) < 1.5e-2
+    # GLU producer: h rows + down's images
+    mg = QM(GGMLType.Q4_K, 2 * F, E, seed=32)
+    h = torch.zeros(B, F, device="cuda")
+    himg = torch.zeros(B * C().x8_bytes(F), dtype=torch.uint8, device="cuda")
+    call(mg, B, None, h, EPI_GLU, {"x8": img.data_ptr(), "x8_stat": st.data_ptr(), "emit8": himg.data_ptr()})
+    gu = xn @ mg.w.T
+    assert rel(h, torch.nn.functional.silu(gu[:, 0::2]) * gu[:, 1::2]) < 2e-2
+    nbF = C().x8_bytes(F)
+    for b in range(B):
+        assert rel(decode_image(himg[b * nbF:(b + 1) * nbF], F), h[b].cpu()) < 1e-2, b
+    # residual producer (down): K = 11008 split over 3 wave groups
+    for qd in (GGMLType.Q4_K, GGMLType.Q6_K):
+        md = QM(qd, E, F, seed=33)
+        resid0 = torch.randn(B, E, device="cuda") * 4
+        resid = resid0.clone()
+        nw2 = torch.rand(E, device="cuda") + 0.5
+        out = torch.zeros(B * C().x8_bytes(E), dtype=torch.uint8, device="cuda")
+        ld = C().x8_stat_ld(E)
+        sto = torch.zeros(B * ld + 4, device="cuda")
+        call(md, B, None, resid, EPI_ADD, {"x8": himg.data_ptr(), "emit8": out.data_ptr(), "emit8_nw": nw2.data_ptr(),
+                                           "emit8_stat": sto.data_ptr()})
+        hq = torch.stack([decode_image(himg[b * nbF:(b + 1) * nbF], F) for b in range(B)]).cuda()
+        assert rel(resid - resid0, hq @ md.w.T) < 1.5e-2, qd
+        nbE = C().x8_bytes(E)
+        for b in range(B):
+            assert rel(decode_image(out[b * nbE:(b + 1) * nbE], E), (resid[b] * nw2).cpu()) < 1e-2, (qd, b)
+            assert torch.allclose(sto[b * ld:b * ld + E // 16].cpu(), (resid[b].cpu().reshape(-1, 16) ** 2).sum(1),
+                                  rtol=1e-4, atol=1e-3), (qd, b)
+    # O projection: plain fp32 attention rows in (int8-quantised in the prologue), residual + image out
+    mo = QM(GGMLType.Q4_K, E, E, seed=34)
+    a = torch.randn(B, E, device="cuda")
+    resid0 = torch.randn(B, E, device="cuda")
+    resid = resid0.clone()
+    out = torch.zeros(B * C().x8_bytes(E), dtype=torch.uint8, device="cuda")
+    sto = torch.zeros(B * C().x8_stat_ld(E) + 4, device="cuda")
+    call(mo, B, a, resid, EPI_ADD, {"emit8": out.data_ptr(), "emit8_nw": nw.data_ptr(), "emit8_stat": sto.data_ptr()})
+    assert rel(resid - resid0, a @ mo.w.T) < 1.5e-2
+
+
+@pytest.mark.parametrize("B", [2, 3, 4])
+def test_engine_batched_x8_chain_matches_single(tiny_models, B):
+    """Continuous-batching decode steps of B = 2..4 rows on the int8 chain (one weight read for all rows)
+    against each sequence's own batch-1 step."""
+    from ollama_operator_amd.engine.runner import Runner
+    g = Runner(tiny_models["tiny-llama"], device="cuda", max_batch=32, max_seqs=8, ctx=256)
+    assert g.exe.exe.x8_bmax == 4
+    rng = np.random.default_rng(B)
+    prompts = [[1] + [int(x) for x in rng.integers(3, 500, n)] for n in (5, 40, 17, 90)[:B]]
+    sids = []
+    for p in prompts:
+        sid = g.new_sequence()
+        g.prefill(sid, p)
+        sids.append(sid)
+    V = g.cfg.n_vocab
+    nxt = [7, 8, 9, 10][:B]
+    g.set_tokens(nxt)
+    g.decode_batch(sids, [len(p) for p in prompts])
+    torch.cuda.synchronize()
+    batched = g.logits[:B, :V].float().cpu().clone()
+    assert torch.isfinite(batched).all()
+    for b, (sid, p) in enumerate(zip(sids, prompts)):
+        g.set_tokens([nxt[b]])
+        g.decode_batch([sid], [len(p)])
+        torch.cuda.synchronize()
+        assert rel(batched[b], g.logits[0, :V].float().cpu()) < 3e-2, b
