@@ -379,13 +379,21 @@ class TPRunnerProxy:
         return self.r.generate(sid, prompt, o, max_tokens=max_tokens, stop=stop, times=times)
 
     # continuous batching (engine/scheduler.py drives the leader's runner through these)
+    def _prefixes(self, sids) -> dict:
+        """The leader's token record of each reused sequence: the scheduler appends generated tokens on
+        the leader only, so a follower's record stops at its prompt; admit truncates to `keep`, which may
+        reach into generated tokens -- followers adopt the leader's record first (same KV positions)."""
+        seqs = self.r.kv.seqs
+        return {str(sid): list(seqs[sid].tokens) for sid in sids if sid in seqs and seqs[sid].tokens}
+
     def admit(self, sid: int, keep: int, tokens: list[int], opts, history: list[int], seed: int) -> None:
-        self._mirror("admit", sid=sid, keep=keep, tokens=list(tokens), opts=opts, history=list(history), seed=seed)
+        self._mirror("admit", sid=sid, keep=keep, tokens=list(tokens), opts=opts, history=list(history), seed=seed,
+                     prefixes=self._prefixes([sid]))
         self.r.admit(sid, keep, tokens, opts, history, seed)
 
     def admit_many(self, items: list[tuple]) -> list[int]:
         items = [(sid, keep, list(t), o, list(h), sd) for sid, keep, t, o, h, sd in items]
-        self._mirror("admit_many", items=items)
+        self._mirror("admit_many", items=items, prefixes=self._prefixes([it[0] for it in items]))
         return self.r.admit_many(items)
 
     def recompose(self, rows: list[tuple], tokens: list[int]) -> None:
@@ -420,6 +428,14 @@ def load_tp_runner(world: TPWorld, path: str, max_batch: int, max_seqs: int, ctx
     if r.ar is not None:
         world.ar_probe = r.ar.error
     return TPRunnerProxy(world, r, cmd)
+
+
+def adopt_prefixes(runner, prefixes: dict | None) -> None:
+    """Follower side of TPRunnerProxy._prefixes: take the leader's token record of reused sequences."""
+    for sid, toks in (prefixes or {}).items():
+        seq = runner.kv.seqs.get(int(sid))
+        if seq is not None:
+            seq.tokens = list(toks)
 
 
 def worker_main() -> None:
@@ -462,8 +478,10 @@ def worker_main() -> None:
             for _ in runner.generate(cmd["sid"], cmd["prompt"], cmd["options"], max_tokens=cmd["max_tokens"]):
                 pass
         elif op == "admit":
+            adopt_prefixes(runner, cmd.get("prefixes"))
             runner.admit(cmd["sid"], cmd["keep"], cmd["tokens"], cmd["opts"], cmd["history"], cmd["seed"])
         elif op == "admit_many":
+            adopt_prefixes(runner, cmd.get("prefixes"))
             runner.admit_many(cmd["items"])
         elif op == "recompose":
             runner.recompose(cmd["rows"], cmd["tokens"])

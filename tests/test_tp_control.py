@@ -99,3 +99,20 @@ def test_control_channel_two_processes(tmp_path):
         assert open(out).read() == "ok"
     finally:
         bell.close(unlink=True)
+
+
+def test_followers_adopt_leader_token_record():
+    """generated tokens are recorded on the leader only; a prefix reuse that reaches
+    into them must not truncate followers differently -- admit carries the leader's record."""
+    from types import SimpleNamespace
+
+    from ollama_operator_amd.engine.kv_cache import SeqState
+    from ollama_operator_amd.parallel.tp import TPRunnerProxy, adopt_prefixes, decode_cmd, encode_cmd
+    lead = SimpleNamespace(kv=SimpleNamespace(seqs={3: SeqState(row=0, tokens=[1, 5, 6, 7, 40, 41])}))
+    fol = SimpleNamespace(kv=SimpleNamespace(seqs={3: SeqState(row=0, tokens=[1, 5, 6, 7])}))
+    proxy = TPRunnerProxy.__new__(TPRunnerProxy)
+    proxy.r = lead
+    pre = proxy._prefixes([3, 9])
+    cmd = decode_cmd(encode_cmd({"op": "admit", "prefixes": pre}))
+    adopt_prefixes(fol, cmd["prefixes"])
+    assert fol.kv.seqs[3].tokens == [1, 5, 6, 7, 40, 41] and fol.kv.seqs[3].length == 6
