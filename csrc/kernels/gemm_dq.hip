@@ -584,6 +584,8 @@ constexpr size_t dq_lds() { return (size_t)((P3 ? 3 : 2) * BM + 2 * BN) * DQ_BK 
 int g_dq_enable = -1;  // -1: OMX_GEMM_DQ (default on), read once
 int g_dq_cfg = -2;     // OMX_DQ_CFG: force tile config 0..3 (microbenchmarks); -2 = not read yet
 int g_dq_sk = 0;       // > 0: force the split-K factor (microbenchmarks, set_dq_tuning)
+int g_dq_split = -1;   // OMX_DQ_SPLIT: 1 = 256 x 256 tiles + split-K for grids short of the chip (narrow N),
+                       // 2 = also split when it evens out the last wave; 0 = narrower tiles instead
 int g_dq_pipe = -1;    // OMX_DQ_PIPE: 3 = three-stage pipeline (counted waits), else two-stage; -1 = not read
 
 }  // namespace
@@ -600,6 +602,10 @@ bool dq_gemm_enabled() {
   if (g_dq_pipe < 0) {
     const char* c = getenv("OMX_DQ_PIPE");
     g_dq_pipe = c ? atoi(c) : 2;
+  }
+  if (g_dq_split < 0) {
+    const char* c = getenv("OMX_DQ_SPLIT");
+    g_dq_split = c ? atoi(c) : 0;
   }
   return g_dq_enable != 0;
 }
@@ -650,6 +656,21 @@ static void run_dq(const GemvParams& P, f16* xp, int Kp, hipStream_t s) {
   int sk = 1;
   if (P.gws && P.gws_elems > 0)
     while (sk < 8 && tiles * sk < 240 && nks / (2 * sk) >= 8 && (long long)(2 * sk) * M * N <= P.gws_elems) sk *= 2;
+  if (g_dq_split > 0 && g_dq_cfg < 0 && M >= 256 && P.gws && P.gws_elems > 0) {
+    // keep the 256 x 256 tile (the most MFMA work per LDS byte) and split K instead of narrowing it:
+    // the fewest waves per unit of work, ties to the smaller split (each split adds a slab write + read)
+    const long long t0 = ntl(256, 256);
+    int best = 0;
+    double bw = 0.0;
+    for (int k = 1; k <= 4; ++k) {
+      if (k > 1 && ((long long)k * M * N > P.gws_elems || nks / k < 8)) break;
+      if (k == 1 && g_dq_split == 1 && t0 < 240) continue;  // narrow grids always split (mode 1)
+      if (k > 1 && g_dq_split == 1 && t0 >= 240) break;
+      const double waves = (double)((t0 * k + 255) / 256) / k;
+      if (best == 0 || waves < bw - 1e-9) best = k, bw = waves;
+    }
+    if (best > 0) cfg = 0, tiles = t0, sk = best;
+  }
   if (g_dq_sk > 0 && P.gws && (long long)g_dq_sk * M * N <= P.gws_elems && nks / g_dq_sk >= 2) sk = g_dq_sk;
   switch (cfg) {
     case 0: launch_dq<QT, 256, 256, 2, 4>(P, xp, Kp, sk, s); break;

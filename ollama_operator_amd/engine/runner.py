@@ -31,7 +31,7 @@ from .sampling import SamplingOptions, sample_host
 from .weights import DeviceWeights, DevQMat
 
 HIST_CAP = 256
-GEMM_SPLIT_WS_FLOATS = 8 << 20  # 32 MiB of fp32 split-K slabs (prefill GEMMs at small M)
+GEMM_SPLIT_WS_FLOATS = 32 << 20  # 128 MiB of fp32 split-K slabs (2-way split of a 2048 x 8192 output)
 
 
 class NativeExec:

@@ -35,7 +35,7 @@ def main():
             x = torch.randn(M, K, device="cuda")
             y = torch.zeros(M, N, device="cuda")
             xws = torch.empty(M * ((K + 255) // 256 * 256), device="cuda", dtype=torch.float16)
-            gws = torch.empty(8 << 20, device="cuda")  # the runner's split-K workspace
+            gws = torch.empty(32 << 20, device="cuda")  # the runner's split-K workspace (GEMM_SPLIT_WS_FLOATS)
             w16 = torch.empty(N * K, device="cuda", dtype=torch.float16)
             yws = torch.empty(M * N, device="cuda")
             ws = {"xws": xws.data_ptr(), "xws_elems": xws.numel(), "gws": gws.data_ptr(), "gws_elems": gws.numel(), "w16ws": w16.data_ptr(),
