@@ -61,18 +61,20 @@ __device__ __forceinline__ void gemv8_body(const GemvParams& P, const int bx) {
   const int nwords = XSP * 3 / 2;
   const size_t img_b = (size_t)XSP * 24;
   const int st_ld = x8_stat_ld_dev(K);
+  const int blast = BT > 1 ? min(P.B, BT) - 1 : 0;  // rows >= P.B re-read the last real row (never stored)
   if constexpr (IN != IN_MERGE) {
 #pragma unroll
     for (int b = 0; b < BT; ++b)
 #pragma unroll
       for (int i = 0; i < X8_NWI; ++i)
-        xw[b][i] = ((const u32x4*)((const char*)P.x8 + b * img_b))[min(tid + NT * i, nwords - 1)];
+        xw[b][i] = ((const u32x4*)((const char*)P.x8 + min(b, blast) * img_b))[min(tid + NT * i, nwords - 1)];
     if constexpr (IN == IN_X8_RMS) {
       const int n4 = K / 64;  // f32x4 of partials (K / 16 floats)
 #pragma unroll
       for (int b = 0; b < BT; ++b)
 #pragma unroll
-        for (int i = 0; i < X8_NSTW; ++i) stv[b][i] = ((const f32x4*)(P.x8_stat + b * st_ld))[min(lane + 64 * i, n4 - 1)];
+        for (int i = 0; i < X8_NSTW; ++i)
+          stv[b][i] = ((const f32x4*)(P.x8_stat + min(b, blast) * st_ld))[min(lane + 64 * i, n4 - 1)];
     }
   } else {
 #pragma unroll
@@ -90,7 +92,7 @@ __device__ __forceinline__ void gemv8_body(const GemvParams& P, const int bx) {
 #pragma unroll
         for (int b = 0; b < BT; ++b)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) av[b][i][j] = *(const f32x4*)(P.x + (long long)b * P.ldx + 16 * gi + 4 * j);
+          for (int j = 0; j < 4; ++j) av[b][i][j] = *(const f32x4*)(P.x + (long long)min(b, blast) * P.ldx + 16 * gi + 4 * j);
       }
     }
   }
@@ -196,7 +198,7 @@ __device__ __forceinline__ void gemv8_body(const GemvParams& P, const int bx) {
   __syncthreads();
 
   // 4. consume the tiles in issue order; epilogue (+ emission) per tile
-  const int nb = BT > 1 ? min(P.B, BT) : 1;  // rows stored / emitted
+  const int nb = blast + 1;  // rows stored / emitted
 #pragma unroll
   for (int j = 0; j < J; ++j) {
     const int t = tile0 + j;

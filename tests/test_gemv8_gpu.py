@@ -289,10 +289,11 @@ def test_batched_rows_consumer_and_producers(B):
 
 
 @pytest.mark.parametrize("B", [2, 3, 4])
-def test_engine_batched_x8_chain_matches_single(tiny_models, B):
+def test_engine_batched_x8_chain_matches_single(tiny_models, B, monkeypatch):
     """Continuous-batching decode steps of B = 2..4 rows on the int8 chain (one weight read for all rows)
     against each sequence's own batch-1 step."""
     from ollama_operator_amd.engine.runner import Runner
+    monkeypatch.setenv("OMX_X8_BATCH", "4")
     g = Runner(tiny_models["tiny-llama"], device="cuda", max_batch=32, max_seqs=8, ctx=256)
     assert g.exe.exe.x8_bmax == 4
     rng = np.random.default_rng(B)
