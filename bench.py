@@ -103,11 +103,12 @@ def bench_server(a, url: str, model_path: str, vocab_words: int = 32000):
         def prompt():  # synthetic prompt of a.prompt tokens, passed as Ollama `context` token ids
             return [1] + [rng.randrange(3, vocab_words) for _ in range(a.prompt - 2)]
 
-        def gen(n, p):
-            with httpx.Client(base_url=url, timeout=600) as cc:
-                d = cc.post("/api/generate", json={"model": "bench", "prompt": " a", "context": p, "raw": True, "stream": False,
-                                                   "options": {"num_predict": n, "seed": 42}}).json()
-            return d
+        def gen(n, p, cc=None):
+            if cc is None:
+                with httpx.Client(base_url=url, timeout=600) as c1:
+                    return gen(n, p, c1)
+            return cc.post("/api/generate", json={"model": "bench", "prompt": " a", "context": p, "raw": True, "stream": False,
+                                                  "options": {"num_predict": n, "seed": 42}}).json()
 
         gen(32, prompt())  # load + warm
         d = gen(a.steps, prompt())
@@ -118,10 +119,19 @@ def bench_server(a, url: str, model_path: str, vocab_words: int = 32000):
         P = a.server_parallel
         if P > 1:
             prompts = [prompt() for _ in range(P)]
-            t0 = time.perf_counter()
+            # one connected client per simulated user, built before the clock starts: an httpx.Client
+            # builds an SSL context (CA bundle load), which 4 threads contending for the GIL took
+            # ~0.3 s to do -- client setup, not serving time
+            clients = [httpx.Client(base_url=url, timeout=600) for _ in range(P)]
+            for cc in clients:
+                cc.get("/api/version")
             with cf.ThreadPoolExecutor(P) as ex:
-                res = list(ex.map(lambda p: gen(a.steps, p), prompts))
-            wall = time.perf_counter() - t0
+                list(ex.map(lambda i: None, range(P)))  # worker threads started before the clock too
+                t0 = time.perf_counter()
+                res = list(ex.map(lambda pc: gen(a.steps, pc[0], pc[1]), zip(prompts, clients)))
+                wall = time.perf_counter() - t0
+            for cc in clients:
+                cc.close()
             out["concurrent_clients"] = P
             out["concurrent_aggregate_tok_s"] = round(sum(x["eval_count"] for x in res) / wall, 2)
             out["concurrent_per_client_tok_s"] = [round(x["eval_count"] / x["eval_duration"] * 1e9, 2) for x in res]

@@ -183,6 +183,74 @@ __device__ __forceinline__ void load_piece(const QMat& w, long long row, int SB,
   }
 }
 
+// The same loads as inline asm (the 3-stage pipeline): hipcc neither counts nor waits for them -- with an
+// LDS DMA in flight it would wait vmcnt(0) at the first use of an ordinary load and drain the ring
+// (cdna_hip_programming.md §5 "three .s-level traps" (b), §5.7 item 1 form (ii)); the kernel counts
+// both queues itself and pins the destinations ("+v") after each counted wait.
+__device__ __forceinline__ u32x4 ald16(const void* p) {
+  u32x4 r;
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r) : "v"(p) : "memory");
+  return r;
+}
+__device__ __forceinline__ u32x2 ald8(const void* p) {
+  u32x2 r;
+  asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(r) : "v"(p) : "memory");
+  return r;
+}
+__device__ __forceinline__ unsigned ald4(const void* p) {
+  unsigned r;
+  asm volatile("global_load_dword %0, %1, off" : "=v"(r) : "v"(p) : "memory");
+  return r;
+}
+__device__ __forceinline__ unsigned ald2(const void* p) {
+  unsigned r;
+  asm volatile("global_load_ushort %0, %1, off" : "=v"(r) : "v"(p) : "memory");
+  return r;
+}
+// VMEM instructions per piece load (the counted-wait arithmetic)
+template <int QT>
+constexpr int piece_loads() {
+  return QT == QT_Q4_K ? 2 : QT == QT_Q5_K ? 3 : QT == QT_Q6_K ? 4 : QT == QT_Q4_0 ? 2 : QT == QT_Q8_0 ? 3 : 4;
+}
+template <int QT>
+__device__ __forceinline__ void load_piece_asm(const QMat& w, long long row, int SB, int pc, Piece<QT>& R) {
+  if constexpr (QT == QT_F16) {
+    const uint8_t* q = w.s0 + row * SB * 512 + 64LL * pc;
+    R.a = ald16(q);
+    R.b = ald16(q + 16);
+    R.f[0] = ald16(q + 32);
+    R.f[1] = ald16(q + 48);
+    return;
+  }
+  const int t = pc / SB, sb = pc - t * SB;
+  if constexpr (QT == QT_Q8_0) {
+    const uint8_t* q = w.s0 + row * SB * 256 + 32LL * pc;
+    R.a = ald16(q);
+    R.b = ald16(q + 16);
+    R.e = ald2(w.s1 + row * SB * 16 + 16LL * sb + 2 * t);
+  } else {
+    R.a = ald16(w.s0 + row * SB * 128 + 16LL * pc);
+    if constexpr (QT == QT_Q4_K || QT == QT_Q5_K) R.m = ald16(w.s1 + row * SB * 16 + 16LL * sb);
+    if constexpr (QT == QT_Q5_K) R.e = ald4(w.s2 + row * SB * 32 + 4LL * pc);
+    if constexpr (QT == QT_Q6_K) {
+      R.h = ald8(w.s1 + row * SB * 64 + 8LL * pc);
+      R.m = ald16(w.s2 + row * SB * 16 + 16LL * sb);
+      R.e = ald2(w.s3 + row * SB * 2 + 2LL * sb);
+    }
+    if constexpr (QT == QT_Q4_0) R.e = ald2(w.s1 + row * SB * 16 + 16LL * sb + 2 * t);
+  }
+}
+// make a piece's registers opaque at this point (after the counted wait that retires its loads)
+template <int QT>
+__device__ __forceinline__ void pin_piece(Piece<QT>& R) {
+  if constexpr (QT == QT_F16) asm volatile("" : "+v"(R.a), "+v"(R.b), "+v"(R.f[0]), "+v"(R.f[1]));
+  else if constexpr (QT == QT_Q8_0) asm volatile("" : "+v"(R.a), "+v"(R.b), "+v"(R.e));
+  else if constexpr (QT == QT_Q4_K) asm volatile("" : "+v"(R.a), "+v"(R.m));
+  else if constexpr (QT == QT_Q5_K) asm volatile("" : "+v"(R.a), "+v"(R.m), "+v"(R.e));
+  else if constexpr (QT == QT_Q6_K) asm volatile("" : "+v"(R.a), "+v"(R.h), "+v"(R.m), "+v"(R.e));
+  else asm volatile("" : "+v"(R.a), "+v"(R.e));
+}
+
 // Q4_K / Q5_K 6-bit scale and min of sub-block j
 __device__ __forceinline__ void k_scale(const u32x4& m, int j, float& sc, float& mn) {
   const float d = h2f(m.x & 0xFFFF), dmin = h2f(m.x >> 16);
@@ -290,14 +358,14 @@ __device__ __forceinline__ void dq_out(const GemvParams& P, const f32x16 (&acc)[
 }
 
 // ------------------------------------------------------------------------------------------------
-template <int QT, int BM, int BN, int WM, int WN>
+template <int QT, int BM, int BN, int WM, int WN, bool P3>
 __global__ __launch_bounds__(DQ_NT, 1) void dq_gemm_kernel(GemvParams P, const f16* __restrict__ X, int Kp, int sk) {
   static_assert(WM * WN == 8, "8 waves");
   constexpr int TM = BM / WM / 32, TN = BN / WN / 32;  // 32 x 32 accumulator tiles per wave
   constexpr int XS = BM * DQ_BK, WS = BN * DQ_BK;      // halves per LDS buffer (128-B rows, swizzled)
   constexpr int XL = BM / 64;                          // 16-B X chunks per thread per K step
   static_assert(TM >= 1 && TN >= 1 && BN * 2 <= DQ_NT && XL >= 1, "tile shape");
-  constexpr int NXB = 2;  // X buffers
+  constexpr int NXB = P3 ? 3 : 2;  // X buffers (the 3-stage pipeline keeps two steps in flight)
   extern __shared__ __attribute__((aligned(16))) char smem[];
   f16* Xs = (f16*)smem;     // [NXB][BM][64] swizzled
   f16* Ws = Xs + NXB * XS;  // [2][BN][64] swizzled
@@ -385,6 +453,72 @@ __global__ __launch_bounds__(DQ_NT, 1) void dq_gemm_kernel(GemvParams P, const f
   };
   auto compute = [&](int buf) { compute_b(buf, buf); };
 
+  if constexpr (P3) {
+    // 3-stage pipeline: X by LDS DMA two steps ahead (3 buffers), W pieces by inline-asm loads two
+    // steps ahead (2 register sets), counted waits only (raw s_barrier: hipcc's __syncthreads would
+    // drain every DMA in flight). Issue order per step j: W(j + 3), X(j + 2); so at the stage point of
+    // step j at most W(j + 2) and X(j + 1) may still be outstanding behind W(j + 1), and at its end at
+    // most W(j + 3) and X(j + 2) behind X(j + 1): both waits are vmcnt(NW + XL). Every thread issues the
+    // same loads (rows past the tile re-load a valid row) so the counts hold per thread.
+    constexpr int NW = piece_loads<QT>(), NWAIT = NW + XL;
+    const long long prow = min(n0 + (wr & (BN - 1)), N - 1);
+    Piece<QT> R0, R1;
+    auto ld_w = [&](int k, Piece<QT>& R) { load_piece_asm<QT>(w, prow, SB, 2 * min(k, ks1 - 1) + wh, R); };
+    auto ld_x = [&](int k, int buf) { issue_x(min(k, ks1 - 1), buf); };
+    auto wait_vm = [&]() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NWAIT) : "memory"); };
+    auto bar = [&]() {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    };
+    auto stage_r = [&](int k, int buf, Piece<QT>& R) {
+      pin_piece<QT>(R);
+      if (wr < BN) {
+        const int pc = 2 * k + wh;
+        unsigned o[16];
+        dq_piece<QT>(R, SB == 1 ? pc : (int)__umulhi((unsigned)pc, sbinv), o);
+        f16* wd = Ws + buf * WS;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          *(u32x4*)(wd + swz(wr, 4 * wh + i)) = (u32x4){o[4 * i], o[4 * i + 1], o[4 * i + 2], o[4 * i + 3]};
+      }
+    };
+    // prologue: W0, X0, W1, X1 in flight; stage W0; W2 into the freed set; X0 + staged W0 visible
+    ld_w(ks0, R0);
+    ld_x(ks0, 0);
+    ld_w(ks0 + 1, R1);
+    ld_x(ks0 + 1, 1);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * XL + NW) : "memory");
+    stage_r(ks0, 0, R0);
+    ld_w(ks0 + 2, R0);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NW + XL) : "memory");
+    bar();
+    // step j (relative index r = j - ks0): X in buffer r % 3, W in r % 2, stages W(j + 1) from set
+    // (r + 1) % 2 and reloads it with W(j + 3)
+    auto step = [&](int j, int xb, int wb, Piece<QT>& Rn) {
+      wait_vm();
+      stage_r(min(j + 1, ks1 - 1), wb ^ 1, Rn);
+      ld_w(j + 3, Rn);
+      ld_x(j + 2, (xb + 2) % 3);
+      compute_b(xb, wb);
+      wait_vm();
+      bar();
+    };
+    int j = ks0;
+    for (; j + 5 < ks1; j += 6) {
+      step(j, 0, 0, R1);
+      step(j + 1, 1, 1, R0);
+      step(j + 2, 2, 0, R1);
+      step(j + 3, 0, 1, R0);
+      step(j + 4, 1, 0, R1);
+      step(j + 5, 2, 1, R0);
+    }
+    for (; j < ks1; ++j) {  // tail: runtime buffer indices
+      const int r = j - ks0;
+      if (r & 1) step(j, r % 3, 1, R0);
+      else step(j, r % 3, 0, R1);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // redundant tail DMAs land before the block ends
+  } else {
   // Two K steps per trip with literal buffer indices and no branches in between: the compiler sees the
   // staging writes (other buffer) and the fragment reads (this buffer) as disjoint, so it can interleave
   // the dequant VALU / LDS writes of step ks + 1 with the MFMAs of step ks. Order inside a step: the
@@ -413,6 +547,7 @@ __global__ __launch_bounds__(DQ_NT, 1) void dq_gemm_kernel(GemvParams P, const f
   if (ks < ks1) {  // odd step count: the last step sits in buffer 0
     __syncthreads();
     compute(0);
+  }
   }
 
   // C fragment (32 x 32): weight row n = lane & 31 (+ 32 j), token row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
@@ -443,12 +578,15 @@ __global__ __launch_bounds__(DQ_NT, 1) void dq_gemm_kernel(GemvParams P, const f
   }
 }
 
-template <int BM, int BN>
-constexpr size_t dq_lds() { return (size_t)(2 * BM + 2 * BN) * DQ_BK * sizeof(f16); }
+template <int BM, int BN, bool P3>
+constexpr size_t dq_lds() { return (size_t)((P3 ? 3 : 2) * BM + 2 * BN) * DQ_BK * sizeof(f16); }
 
 int g_dq_enable = -1;  // -1: OMX_GEMM_DQ (default on), read once
 int g_dq_cfg = -2;     // OMX_DQ_CFG: force tile config 0..3 (microbenchmarks); -2 = not read yet
 int g_dq_sk = 0;       // > 0: force the split-K factor (microbenchmarks, set_dq_tuning)
+int g_dq_split = -1;   // OMX_DQ_SPLIT: 1 = 256 x 256 tiles + split-K for grids short of the chip (narrow N),
+                       // 2 = also split when it evens out the last wave; 0 = narrower tiles instead
+int g_dq_pipe = -1;    // OMX_DQ_PIPE: 3 = three-stage pipeline (counted waits), else two-stage; -1 = not read
 
 }  // namespace
 
@@ -460,6 +598,14 @@ bool dq_gemm_enabled() {
   if (g_dq_cfg == -2) {
     const char* c = getenv("OMX_DQ_CFG");
     g_dq_cfg = c ? atoi(c) : -1;
+  }
+  if (g_dq_pipe < 0) {
+    const char* c = getenv("OMX_DQ_PIPE");
+    g_dq_pipe = c ? atoi(c) : 2;
+  }
+  if (g_dq_split < 0) {
+    const char* c = getenv("OMX_DQ_SPLIT");
+    g_dq_split = c ? atoi(c) : 0;
   }
   return g_dq_enable != 0;
 }
@@ -475,35 +621,57 @@ void set_dq_tuning(int cfg, int sk) {
 template <int QT, int BM, int BN, int WM, int WN>
 static void launch_dq(const GemvParams& P, const f16* xp, int Kp, int sk, hipStream_t s) {
   const int mt = (P.B + BM - 1) / BM, nt = (P.w.N + BN - 1) / BN;
-  const size_t lds = dq_lds<BM, BN>();
-  hipLaunchKernelGGL((dq_gemm_kernel<QT, BM, BN, WM, WN>), dim3(mt * nt * sk), dim3(DQ_NT), lds, s, P, xp, Kp, sk);
+  if (g_dq_pipe == 3 && !(BM == 256 && BN == 256)) {  // 256 x 256: 3 X buffers + 2 register sets spill
+    const size_t lds = dq_lds<BM, BN, true>();
+    auto k = dq_gemm_kernel<QT, BM, BN, WM, WN, !(BM == 256 && BN == 256)>;
+    static bool attr = false;  // > 64 KB dynamic LDS: one attribute call per instantiation, before capture
+    if (!attr) {
+      (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      attr = true;
+    }
+    hipLaunchKernelGGL(k, dim3(mt * nt * sk), dim3(DQ_NT), lds, s, P, xp, Kp, sk);
+    return;
+  }
+  const size_t lds = dq_lds<BM, BN, false>();
+  hipLaunchKernelGGL((dq_gemm_kernel<QT, BM, BN, WM, WN, false>), dim3(mt * nt * sk), dim3(DQ_NT), lds, s, P, xp, Kp, sk);
 }
 
 template <int QT>
 static void run_dq(const GemvParams& P, f16* xp, int Kp, hipStream_t s) {
   hipLaunchKernelGGL(prep_xp_kernel<QT>, dim3(P.B), dim3(256), 0, s, P, xp, Kp);
   const int M = P.B, N = P.w.N, nks = Kp / DQ_BK;
-  // tile x split-K from a wave model calibrated on MI355X (scripts/bench_dq_sweep.py, profiles/r4_gemm):
-  // time = waves * (K steps per split) * c[cfg] + split-K slab traffic, waves = ceil(units / slots);
-  // c = measured cost of one K step of a full wave of tiles (256x256 2.19 us, 256x128 1.32, 128x256 1.44,
-  // 128x128 1.34 with two blocks per CU, i.e. 512 slots); slabs: sk * M * N fp32 written + read at ~5 TB/s
-  const int bm[4] = {256, 256, 128, 128}, bn[4] = {256, 128, 256, 128};
-  const double cst[4] = {2.19, 1.32, 1.44, 1.34};
-  const int slots[4] = {256, 256, 256, 512};
-  auto ntl = [&](int c) { return (long long)((M + bm[c] - 1) / bm[c]) * ((N + bn[c] - 1) / bn[c]); };
-  int cfg = 3, sk = 1;
-  double best = -1.0;
-  for (int c = 0; c < 4; ++c) {
-    if (g_dq_cfg >= 0 && g_dq_cfg <= 3 && c != g_dq_cfg) continue;  // microbenchmark override (OMX_DQ_CFG)
-    for (int k = 1; k <= 4; ++k) {
-      if (k > 1 && (!P.gws || (long long)k * M * N > P.gws_elems || nks / k < 8)) break;
-      if (g_dq_sk > 0 && k != g_dq_sk) continue;  // microbenchmark override (set_dq_tuning)
-      const long long units = ntl(c) * k;
-      const double waves = (double)((units + slots[c] - 1) / slots[c]);
-      const double t = waves * ((double)nks / k) * cst[c] + (k > 1 ? 2.0 * k * M * N * 4 / 5e6 : 0.0);
-      if (best < 0.0 || t < best) best = t, cfg = c, sk = k;
-    }
+  // tile: 256 x 256 when the grid fills the chip, else narrower N tiles, then 128-token M tiles
+  int cfg;
+  long long tiles;
+  auto ntl = [&](int bm, int bn) { return (long long)((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
+  if (M >= 256 && ntl(256, 256) >= 240) cfg = 0, tiles = ntl(256, 256);
+  else if (M >= 256) cfg = 1, tiles = ntl(256, 128);
+  else if (ntl(128, 256) >= 240) cfg = 2, tiles = ntl(128, 256);
+  else cfg = 3, tiles = ntl(128, 128);
+  if (g_dq_cfg >= 0 && g_dq_cfg <= 3) {  // microbenchmark override (OMX_DQ_CFG)
+    cfg = g_dq_cfg;
+    const int bm[4] = {256, 256, 128, 128}, bn[4] = {256, 128, 256, 128};
+    tiles = ntl(bm[cfg], bn[cfg]);
   }
+  int sk = 1;
+  if (P.gws && P.gws_elems > 0)
+    while (sk < 8 && tiles * sk < 240 && nks / (2 * sk) >= 8 && (long long)(2 * sk) * M * N <= P.gws_elems) sk *= 2;
+  if (g_dq_split > 0 && g_dq_cfg < 0 && M >= 256 && P.gws && P.gws_elems > 0) {
+    // keep the 256 x 256 tile (the most MFMA work per LDS byte) and split K instead of narrowing it:
+    // the fewest waves per unit of work, ties to the smaller split (each split adds a slab write + read)
+    const long long t0 = ntl(256, 256);
+    int best = 0;
+    double bw = 0.0;
+    for (int k = 1; k <= 4; ++k) {
+      if (k > 1 && ((long long)k * M * N > P.gws_elems || nks / k < 8)) break;
+      if (k == 1 && g_dq_split == 1 && t0 < 240) continue;  // narrow grids always split (mode 1)
+      if (k > 1 && g_dq_split == 1 && t0 >= 240) break;
+      const double waves = (double)((t0 * k + 255) / 256) / k;
+      if (best == 0 || waves < bw - 1e-9) best = k, bw = waves;
+    }
+    if (best > 0) cfg = 0, tiles = t0, sk = best;
+  }
+  if (g_dq_sk > 0 && P.gws && (long long)g_dq_sk * M * N <= P.gws_elems && nks / g_dq_sk >= 2) sk = g_dq_sk;
   switch (cfg) {
     case 0: launch_dq<QT, 256, 256, 2, 4>(P, xp, Kp, sk, s); break;
     case 1: launch_dq<QT, 256, 128, 4, 2>(P, xp, Kp, sk, s); break;
