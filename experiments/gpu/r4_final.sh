@@ -11,5 +11,3 @@ timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smo
 tail -1 $O/smoke.log
 timeout -k 10 300 python -u bench.py > $O/bench_default.log 2>&1 || { tail -20 $O/bench_default.log; exit 1; }
 tail -1 $O/bench_default.log
-timeout -k 10 300 python -u scripts/bench_dq_sweep.py > $O/dq_sweep.log 2>&1 || { tail -20 $O/dq_sweep.log; exit 1; }
-cut -c1-140 $O/dq_sweep.log | grep -v amdgpu
