@@ -360,8 +360,8 @@ namespace {
 
 size_t lds8(int K, int KS, int BT = 1) { return BT * x8_bytes(K) + (size_t)BT * (32 + (KS - 1) * GEMV_NT) * 4; }
 
-// batch rows per launch: B = 1, 2, or 3-4 (row 3 of a B = 3 launch is computed, never stored)
-int bt_of(int B) { return B <= 2 ? B : 4; }
+// batch rows per launch: exactly B (1-4)
+int bt_of(int B) { return B; }
 
 // 4 rows fit the register budget of 768 / 1024-thread blocks only without the RMS partials and the
 // Q5_K high-bit planes (kernel-resource-usage: these would spill); such launches are not covered
@@ -431,7 +431,7 @@ bool covered(const GemvParams& P, Geo& G) {
   if (!geometry(P, G)) return false;
   if (em == EM_GLU && G.J != 2) return false;  // a block owns whole groups: two tiles, unsplit K
   if (in != IN_MERGE && (size_t)G.ks * GEMV_NT * X8_NWI * 16 < x8_bytes(P.w.K)) return false;
-  if (bt_of(P.B) == 4 && !bt4_ok(q, G.ks, in)) return false;
+  if (bt_of(P.B) >= 3 && !bt4_ok(q, G.ks, in)) return false;
   return lds8(P.w.K, G.ks, bt_of(P.B)) <= (P.B > 1 ? 160 : 64) * 1024;
 }
 
@@ -459,6 +459,9 @@ void launch_em(const GemvParams& P, int em, int grid, hipStream_t s) {
     switch (bt_of(P.B)) {
       case 1: launch_em_bt<QT, NSB, J, KS, IN, MS, 1>(P, em, grid, s); break;
       case 2: launch_em_bt<QT, NSB, J, KS, IN, MS, 2>(P, em, grid, s); break;
+      case 3:
+        if constexpr (bt4_ok(QT, KS, IN)) launch_em_bt<QT, NSB, J, KS, IN, MS, 3>(P, em, grid, s);
+        break;
       default:
         if constexpr (bt4_ok(QT, KS, IN)) launch_em_bt<QT, NSB, J, KS, IN, MS, 4>(P, em, grid, s);
         break;
@@ -509,6 +512,7 @@ void launch_dual_in(const GemvParams& A, const GemvParams& B, int gxa, int gxb, 
   switch (bt_of(A.B)) {
     case 1: launch_dual_k<QA, QB, IN, 1>(A, B, gxa, gxb, s); break;
     case 2: launch_dual_k<QA, QB, IN, 2>(A, B, gxa, gxb, s); break;
+    case 3: launch_dual_k<QA, QB, IN, 3>(A, B, gxa, gxb, s); break;
     default: launch_dual_k<QA, QB, IN, 4>(A, B, gxa, gxb, s); break;
   }
 }

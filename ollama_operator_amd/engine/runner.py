@@ -100,9 +100,9 @@ class NativeExec:
             return {}
         return dict(x8e=b["x8e"].data_ptr(), x8f=b["x8f"].data_ptr(), x8st=b["x8st"].data_ptr(), x8q=b["x8q"].data_ptr(),
                     x8sync=b["x8sync"].data_ptr(), x8_ok=1, x8_fuse=int(os.environ.get("OMX_X8_FUSE", "0") != "0"),
-                    # batch rows on the chain: B = 2 measured 1.73 vs 2.08 ms per step on the int8 rows; from 3
-                    # rows layout M's MFMA GEMVs win (profiles/r4_batch), so 2 by default
-                    x8_bmax=int(os.environ.get("OMX_X8_BATCH", "2")))
+                    # batch rows on the chain: B = 2 measured 1.73 vs 2.08 ms per step on the int8 rows, B = 3
+                    # 2.15 vs 2.19 ms; at 4 rows layout M's MFMA GEMVs win (profiles/r4_batch), so 3 by default
+                    x8_bmax=int(os.environ.get("OMX_X8_BATCH", "3")))
 
     def ar_fits(self, B: int) -> bool:
         return self.exe.ar_fits(B)
