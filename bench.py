@@ -368,6 +368,10 @@ def main():
     ap.add_argument("--ttft-long", type=int, default=2048,
                     help="also time prefill + first token of a prompt this long (extra.ttft_long_ms; 0 = skip)")
     ap.add_argument("--chunk", type=int, default=2048, help="prefill chunk (MFMA GEMM M) = runner max_batch")
+    ap.add_argument("--long-ctx", default="2048,4096",
+                    help="also measure batch-1 decode tokens/s after a prompt of each of these lengths "
+                         "(extra.long_context: decode_ctx<L>_tok_s; a length past the model's context is "
+                         "clipped to it, minus the timed steps; empty = skip)")
     ap.add_argument("--server-parallel", type=int, default=4,
                     help="OLLAMA_NUM_PARALLEL of the spawned server (concurrent clients measured)")
     a = ap.parse_args()
@@ -411,7 +415,10 @@ def main():
     else:
         ensure_model(path, a.model, a.ftype)
 
-    ctx = max(a.prompt + a.warmup + a.steps + 64, a.ttft_long + 8 if a.ttft_long else 0)
+    long_ctx = [int(x) for x in a.long_ctx.split(",") if x.strip()] if gpu else []
+    LC_WARM, LC_STEPS = 8, 64
+    ctx = max(a.prompt + a.warmup + a.steps + 64, a.ttft_long + 8 if a.ttft_long else 0,
+              max(long_ctx, default=0) + LC_WARM + LC_STEPS + 16)
     t_load = time.perf_counter()
     runner = Runner(path, device=f"cuda:{local}" if gpu else "cpu", max_batch=a.chunk,
                     max_seqs=max(2, a.batch_extra), ctx=ctx)
@@ -469,6 +476,24 @@ def main():
             runner.free_sequence(sid)
             best = dt_l if best is None else min(best, dt_l)
         ttft_long = round(best * 1e3, 2)
+    long_res = {}
+    for L in sorted({min(x, runner.ctx - LC_WARM - LC_STEPS - 4) for x in long_ctx}):
+        # decode after an L-token prompt: every step attends over >= L cached keys (split flash-decode)
+        p = [1] + torch.randint(3, runner.cfg.n_vocab, (L - 1,), generator=g).tolist()
+        sid = runner.new_sequence()
+        gl = runner.generate(sid, p, opts, max_tokens=LC_WARM + LC_STEPS + 2)
+        next(gl)
+        for _ in range(LC_WARM):
+            next(gl)
+        sync()
+        t_l = time.perf_counter()
+        for _ in range(LC_STEPS):
+            next(gl)
+        sync()
+        dt_l = time.perf_counter() - t_l
+        gl.close()
+        runner.free_sequence(sid)
+        long_res[f"decode_ctx{L}_tok_s"] = round(LC_STEPS / dt_l, 2)
     batched = None
     if a.batch_extra > 1 and gpu:
         batched = bench_batched(runner, a, rank, world, sync)
@@ -512,7 +537,7 @@ def main():
                       "load_s": round(load_s, 2),
                       "weights_gb": round(weights_gb, 3), "layout_m_gb": round(layout_m_gb, 3),
                       "resident_weights_gb": round(weights_gb + layout_m_gb, 3),
-                      "continuous_batching": batched, "server": served},
+                      "long_context": long_res or None, "continuous_batching": batched, "server": served},
         }), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -300,6 +300,15 @@ PYBIND11_MODULE(_C, m) {
   m.def("set_dq_gemm", &set_dq_gemm, "1: prefill GEMMs from 128 rows on the stream-order dequant kernel (gemm_dq.hip)");
   m.def("set_dq_tuning", &set_dq_tuning, "microbenchmarks: force the dq GEMM tile config (0..3, -1 auto) and split-K factor (0 auto)");
   m.def("dq_gemm_enabled", &dq_gemm_enabled);
+  // launch counters (ops.h LC_*): tests assert which kernel family a call enqueued
+  m.def("launch_counts", []() {
+    static const char* names[LC_N] = {"dq_gemm", "gemm_tile", "gemm_lib", "gemv8_row1", "gemv8_rows", "gemv8_dual",
+                                      "gemv_mb", "gemv_flight", "attn_decode", "attn_prefill", "qkv_attn"};
+    py::dict d;
+    for (int i = 0; i < LC_N; ++i) d[names[i]] = launch_count(i);
+    return d;
+  });
+  m.def("reset_launch_counts", &reset_launch_counts);
   m.def("gemm_lib_prepare", [](int N, int K, int min_M, int max_M, size_t ws_bytes) {
     blas_prepare(N, K, min_M, max_M, ws_bytes);
   });
@@ -534,6 +543,7 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("x8_bmax", [](const Executor& e) { return e.ws.x8_ok ? e.ws.x8_bmax : 0; })
       .def_property_readonly("n_attn8", [](const Executor& e) { return e.n_attn8; })
       .def_property_readonly("n_ffn8", [](const Executor& e) { return e.n_ffn8; })
+      .def_property_readonly("n_qkv_attn", [](const Executor& e) { return e.n_qkv_attn; })
       .def("set_segments", [](Executor& e, std::vector<std::pair<int, int>> segs) { e.segments = std::move(segs); })
       .def("set_splits", [](Executor& e, int n, int defer, int fuse) {
         e.ws.n_splits = n;
@@ -633,6 +643,14 @@ PYBIND11_MODULE(_C, m) {
     ARParams P = ar_params(d);
     if (slab < 0 || slab >= AR_SLABS || n % 4 || n > P.slab_floats) throw std::runtime_error("ar_allreduce_add: bad slab / n");
     ar_allreduce_add(P, slab, Pp<float>(y), n, S(stream));
+  });
+  m.def("ar_allreduce_add_emit", [](py::dict d, int slab, uintptr_t y, int E, int B, uintptr_t img, uintptr_t nw,
+                                     uintptr_t stat, uintptr_t stream) {
+    ARParams P = ar_params(d);
+    if (slab < 0 || slab >= AR_SLABS || (long long)E * B > P.slab_floats)
+      throw std::runtime_error("ar_allreduce_add_emit: bad slab / shape");
+    if (!ar_allreduce_add_emit(P, slab, Pp<float>(y), E, B, Pp<void>(img), Pp<const float>(nw), Pp<float>(stat), S(stream)))
+      throw std::runtime_error("ar_allreduce_add_emit: shape not covered");
   });
   m.def("ar_allgather", [](py::dict d, int slab, uintptr_t out, int rows, int n_local, int ld_out, uintptr_t stream) {
     ARParams P = ar_params(d);

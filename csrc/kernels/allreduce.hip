@@ -31,6 +31,7 @@
 // Reference parity: the reference has replica parallelism only (pkg/model/model.go:149-186); this is
 // the MI355X-native TP collective the north star adds.
 #include "common.h"
+#include "gemv8_core.h"
 #include "ops.h"
 
 namespace omx {
@@ -84,6 +85,49 @@ __global__ __launch_bounds__(AR_NT) void ar_add_kernel(ARParams P, int slab, flo
   }
 }
 
+// The same sum + residual add, fused with the int8 activation chain's emission (gemv8.hip): thread
+// = one 16-element group of the new residual row, which it also quantises into the next RMSNorm'd
+// GEMV's image (x * norm_w, ops.h x8_bytes layout) with the group's sum of squares -- what the O /
+// down producers emit at TP = 1, so under TP the QKV / gate_up / LM-head GEMVs read an int8 image too
+// and no separate norm or quantisation pass runs. Rows b = 0..B-1 of E each (n = B * E).
+template <int W>
+__global__ __launch_bounds__(AR_NT) void ar_add_emit_kernel(ARParams P, int slab, float* __restrict__ y, int E, int B,
+                                                            void* img, const float* __restrict__ nw, float* stat) {
+  if (!ar_barrier(P)) return;
+  const long long off = (long long)slab * P.slab_floats;
+  const int gpr = E >> 4;  // groups per row
+  for (int gi = blockIdx.x * AR_NT + threadIdx.x; gi < B * gpr; gi += gridDim.x * AR_NT) {
+    const int b = gi / gpr, G = gi - b * gpr;
+    const long long e0 = (long long)b * E + 16LL * G;
+    f32x4 v[W][4];
+#pragma unroll
+    for (int r = 0; r < W; ++r)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[r][j] = *(const f32x4*)(P.data[r] + off + e0 + 4 * j);  // all loads in flight
+    f32x4 yv[4], wv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      yv[j] = *(const f32x4*)(y + e0 + 4 * j);
+      wv[j] = *(const f32x4*)(nw + 16LL * G + 4 * j);
+    }
+    float o[16], sq[16];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      f32x4 sacc = v[0][j];
+#pragma unroll
+      for (int r = 1; r < W; ++r) sacc += v[r][j];  // rank order: identical on every rank
+      const f32x4 nv = yv[j] + sacc;
+      *(f32x4*)(y + e0 + 4 * j) = nv;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        o[4 * j + k] = nv[k] * wv[j][k];
+        sq[4 * j + k] = nv[k] * nv[k];
+      }
+    }
+    emit_group((char*)img + (size_t)b * x8_slots_dev(E) * 24, E, G, o, sq, stat + (size_t)b * x8_stat_ld_dev(E));
+  }
+}
+
 // out[row][r * n_local + j] = slab_r[row][j]  (vocab-sharded logits -> full rows)
 __global__ __launch_bounds__(AR_NT) void ar_gather_kernel(ARParams P, int slab, float* __restrict__ out, int rows,
                                                           int n_local, int ld_out) {
@@ -112,6 +156,19 @@ void ar_allreduce_add(const ARParams& P, int slab, float* y, int n, hipStream_t 
     AR_CASE(1) AR_CASE(2) AR_CASE(3) AR_CASE(4) AR_CASE(5) AR_CASE(6) AR_CASE(7) AR_CASE(8)
 #undef AR_CASE
     default: break;
+  }
+}
+
+bool ar_allreduce_add_emit(const ARParams& P, int slab, float* y, int E, int B, void* img, const float* nw, float* stat,
+                           hipStream_t s) {
+  if (E % 16 || !img || !nw || !stat || B < 1 || B > X8_MAX_B) return false;
+  const int g = ar_grid((long long)B * E / 16);  // one 16-element group per thread
+  switch (P.world) {
+#define AR_CASE(W) \
+  case W: ar_add_emit_kernel<W><<<g, AR_NT, 0, s>>>(P, slab, y, E, B, img, nw, stat); return true;
+    AR_CASE(1) AR_CASE(2) AR_CASE(3) AR_CASE(4) AR_CASE(5) AR_CASE(6) AR_CASE(7) AR_CASE(8)
+#undef AR_CASE
+    default: return false;
   }
 }
 

@@ -542,6 +542,7 @@ void attention_decode(const AttnParams& P0, hipStream_t s) {
   if (P.kps <= 0) P.kps = g_attn_kps;
   if (P.prefill && P.NQ >= 16 && P.D % 16 == 0) {  // one sequence, contiguous positions: MFMA flash
     dim3 grid((P.NQ + PF_BQ - 1) / PF_BQ, P.H);
+    count_launch(LC_ATTN_PREFILL);
     switch (P.D) {
       case 64: hipLaunchKernelGGL(attn_prefill_kernel<64>, grid, dim3(256), 0, s, P); return;
       case 80: hipLaunchKernelGGL(attn_prefill_kernel<80>, grid, dim3(256), 0, s, P); return;
@@ -552,6 +553,7 @@ void attention_decode(const AttnParams& P0, hipStream_t s) {
       default: break;
     }
   }
+  count_launch(LC_ATTN_DECODE);
   switch (P.D) {
     case 64: launch_d<64>(P, s); break;
     case 80: launch_d<80>(P, s); break;

@@ -574,9 +574,13 @@ void gemm(const GemvParams& P, hipStream_t s) {
   const bool lib = lm > 0 && P.B >= lm;
   if (lib) {
     hipLaunchKernelGGL(prep_x16_kernel, dim3(P.B), dim3(256), 0, s, P, x16);
-    if (gemm_lib(P, x16, s)) return;
+    if (gemm_lib(P, x16, s)) {
+      count_launch(LC_GEMM_LIB);
+      return;
+    }
   }
   if (dq_gemm(P, s)) return;
+  count_launch(LC_GEMM_TILE);
   if (!lib) hipLaunchKernelGGL(prep_x16_kernel, dim3(P.B), dim3(256), 0, s, P, x16);
   switch (P.w.qtype) {
     case QT_Q4_K: launch_gemm<QT_Q4_K>(P, x16, s); break;

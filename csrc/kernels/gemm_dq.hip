@@ -46,6 +46,7 @@ bool dq_gemm(const GemvParams& P, hipStream_t s) {
   const long long cap = P.xws_elems ? P.xws_elems : (long long)P.B * P.w.K;
   if ((long long)P.B * Kp > cap) return false;
   f16* xp = (f16*)P.xws;
+  count_launch(LC_DQ_GEMM);
   switch (qt) {
     case QT_Q4_K: run_dq_q4k(P, xp, Kp, s); break;
     case QT_Q5_K: run_dq_q5k(P, xp, Kp, s); break;

@@ -1,3 +1,4 @@
+#include <atomic>
 // Fused quantized GEMV for decode and small batches (M = B <= a few rows) on gfx950.
 //
 // y[b, n] = epilogue( sum_k W[n, k] * norm(x[b, :])[k] )
@@ -831,7 +832,10 @@ void gemv2(const GemvParams& A0, const GemvParams& B0, hipStream_t s) {
       case QT_Q8_0: done = launch_dual_a<QT_Q8_0>(A, Bp, need, s); break;
       default: break;
     }
-    if (done) return;
+    if (done) {
+      count_launch(LC_GEMV_FLIGHT);
+      return;
+    }
   }
   gemv(A, s);
   gemv(Bp, s);
@@ -839,6 +843,13 @@ void gemv2(const GemvParams& A0, const GemvParams& B0, hipStream_t s) {
 
 bool gemv_merge_supported(int B, int K, int D, int S) {
   return B == 1 && K <= 4096 && D % 16 == 0 && K % D == 0 && (S == 2 || S == 4 || S == 8);
+}
+
+static std::atomic<long long> g_launches[LC_N];
+void count_launch(int which) { g_launches[which].fetch_add(1, std::memory_order_relaxed); }
+long long launch_count(int which) { return which >= 0 && which < LC_N ? g_launches[which].load() : -1; }
+void reset_launch_counts() {
+  for (auto& c : g_launches) c.store(0);
 }
 
 void gemv(const GemvParams& P0, hipStream_t s) {
@@ -859,6 +870,7 @@ void gemv(const GemvParams& P0, hipStream_t s) {
     gemm(P, s);
     return;
   }
+  count_launch(LC_GEMV_FLIGHT);
   switch (eff_qtype(P)) {
     case QT_Q6_K8: launch_q<QT_Q6_K8>(P, s); break;
     case QT_Q4_K: launch_q<QT_Q4_K>(P, s); break;

@@ -22,258 +22,9 @@
 // The O projection keeps the deferred flash-decode merge input (IN_MERGE) and emits like down.
 // Reference parity: the decode GEMVs of llama.cpp inside `ollama/ollama` (reference
 // pkg/model/pod.go:10-12); numerics checked against an fp32 torch GEMV (tests/test_gemv8_gpu.py).
-#include "gemv8_core.h"
+#include "gemv8_body.h"
 
 namespace omx {
-
-// One block = KS groups of 4 waves on the same 16-row tiles (group kg owns super-blocks
-// [kg * CH, (kg + 1) * CH)); J consecutive tiles per block, every weight load issued up front.
-// MS: merge slabs of IN_MERGE (1 = plain fp32 input, no merge).
-// BT: batch rows (continuous batching): every weight tile is read once and dotted with BT activation
-// images (row b of the LDS image at b * XSP slots); rows >= P.B are computed but never stored.
-template <int QT, int NSB, int J, int KS, int IN, int MS, int EMIT, bool WT = false, int BT = 1>
-__device__ __forceinline__ void gemv8_body(const GemvParams& P, const int bx) {
-  static_assert(BT == 1 || MS <= 1, "batched rows take the plain fp32 input (no deferred merge)");
-  constexpr int NT = GEMV_NT * KS;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const QMat& w = P.w;
-  const int K = w.K, N = w.N, SB = n_sb(K), XS = SB * XPAD, XSP = x8_slots_dev(K);
-  i32x4* lq = (i32x4*)smem;                           // [BT][XSP]
-  f32x2* lf = (f32x2*)(smem + (size_t)BT * XSP * 16);  // [BT][XSP]
-  float* stage = (float*)(lf + BT * XSP);             // [BT][32]: emitted values, their squares
-  float* part = stage + 32 * BT;                      // [KS - 1][BT][GEMV_NT] partial sums of the K split
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = lane >> 4, s = lane & 15;
-  const int kg = KS > 1 ? wave / GEMV_NW : 0, gtid = tid - kg * GEMV_NT;
-  const int CH = KS > 1 ? (SB + KS - 1) / KS : SB;
-  const int sb0 = kg * CH, se = min(SB, sb0 + CH);
-  const int n_tiles = (N + 15) / 16;
-  const int rbase = (wave - kg * GEMV_NW) * 4 + g;
-  const int tile0 = bx * J;
-
-  // 1. activation operands FIRST (they return ahead of the weight stream)
-  u32x4 xw[BT][X8_NWI];
-  f32x4 stv[BT][X8_NSTW];
-  constexpr int MG = IN == IN_MERGE ? NSB * KS : 1;  // groups per thread of the merge prologue
-  constexpr int MSS = MS > 0 ? MS : 1;
-  constexpr int AR = BT > 1 ? BT : MSS;  // merge slabs (batch 1) or batch rows of plain fp32 input
-  f32x4 av[AR][MG][4];
-  f32x2 ml[MSS][MG];
-  const int nwords = XSP * 3 / 2;
-  const size_t img_b = (size_t)XSP * 24;
-  const int st_ld = x8_stat_ld_dev(K);
-  const int blast = BT > 1 ? min(P.B, BT) - 1 : 0;  // rows >= P.B re-read the last real row (never stored)
-  if constexpr (IN != IN_MERGE) {
-#pragma unroll
-    for (int b = 0; b < BT; ++b)
-#pragma unroll
-      for (int i = 0; i < X8_NWI; ++i)
-        xw[b][i] = ((const u32x4*)((const char*)P.x8 + min(b, blast) * img_b))[min(tid + NT * i, nwords - 1)];
-    if constexpr (IN == IN_X8_RMS) {
-      const int n4 = K / 64;  // f32x4 of partials (K / 16 floats)
-#pragma unroll
-      for (int b = 0; b < BT; ++b)
-#pragma unroll
-        for (int i = 0; i < X8_NSTW; ++i)
-          stv[b][i] = ((const f32x4*)(P.x8_stat + min(b, blast) * st_ld))[min(lane + 64 * i, n4 - 1)];
-    }
-  } else {
-#pragma unroll
-    for (int i = 0; i < MG; ++i) {
-      const int gi = min(tid + NT * i, K / 16 - 1);
-      if constexpr (MS > 1) {
-        const int h = 16 * gi / P.merge_D, nh = K / P.merge_D;
-#pragma unroll
-        for (int sp = 0; sp < MS; ++sp) {
-          ml[sp][i] = *(const f32x2*)(P.merge_ml + 2 * (sp * nh + h));
-#pragma unroll
-          for (int j = 0; j < 4; ++j) av[sp][i][j] = *(const f32x4*)(P.x + (long long)sp * K + 16 * gi + 4 * j);
-        }
-      } else {
-#pragma unroll
-        for (int b = 0; b < BT; ++b)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) av[b][i][j] = *(const f32x4*)(P.x + (long long)min(b, blast) * P.ldx + 16 * gi + 4 * j);
-      }
-    }
-  }
-  __builtin_amdgcn_sched_barrier(0);
-
-  // 2. every weight tile of this block in flight (surplus slots re-read the last tile, unused)
-  WTile<QT, NSB, 1> T[J];
-#pragma unroll
-  for (int j = 0; j < J; ++j) {
-    const int t = min(tile0 + j, n_tiles - 1);
-    load_wtile<QT, NSB, 1>(w, 0, t * 16 + rbase, N, SB, sb0, s, T[j], se);
-  }
-  __builtin_amdgcn_sched_barrier(0);
-
-  // 3. the activation images into LDS (the copy waits for the activation loads only); a row's image
-  //    is [XSP] int8 words then [XSP] (d, d * sum q) pairs, split here into the lq / lf planes
-  float rstd[BT];
-#pragma unroll
-  for (int b = 0; b < BT; ++b) rstd[b] = 1.f;
-  if constexpr (IN != IN_MERGE) {
-#pragma unroll
-    for (int b = 0; b < BT; ++b)
-#pragma unroll
-      for (int i = 0; i < X8_NWI; ++i) {
-        const int wd = tid + NT * i;
-        if (wd < nwords) {
-          u32x4* dst = wd < XSP ? (u32x4*)lq + b * XSP + wd : (u32x4*)(lf + b * XSP) + (wd - XSP);
-          *dst = xw[b][i];
-        }
-      }
-    if constexpr (IN == IN_X8_RMS) {
-      const int n4 = K / 64;
-#pragma unroll
-      for (int b = 0; b < BT; ++b) {
-        float ss = 0.f;
-#pragma unroll
-        for (int i = 0; i < X8_NSTW; ++i)
-          if (lane + 64 * i < n4) ss += stv[b][i].x + stv[b][i].y + stv[b][i].z + stv[b][i].w;
-        rstd[b] = rsqrtf(wave_sum(ss) / K + P.eps);
-      }
-    }
-  } else {
-#pragma unroll
-    for (int i = 0; i < MG; ++i) {
-      const int gi = tid + NT * i;
-#pragma unroll
-      for (int b = 0; b < BT; ++b) {
-        f32x4 xv[4];
-        if constexpr (MS > 1) {  // flash-decode merge: splits without keys carry m = -inf, l = 0
-          float M = -INFINITY;
-#pragma unroll
-          for (int sp = 0; sp < MS; ++sp) M = fmaxf(M, ml[sp][i].x);
-          float L = 0.f;
-          f32x4 a[4] = {};
-#pragma unroll
-          for (int sp = 0; sp < MS; ++sp) {
-            const float c = ml[sp][i].x == -INFINITY ? 0.f : __expf(ml[sp][i].x - M);
-            L += c * ml[sp][i].y;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) a[j] += c * av[sp][i][j];
-          }
-          const float inv = L > 0.f ? 1.f / L : 0.f;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) xv[j] = a[j] * inv;
-        } else {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) xv[j] = av[b][i][j];
-        }
-        const int slot = b * XSP + (gi < SB * 16 ? (gi >> 4) * XPAD + (gi & 15) : XS);
-        float v[16];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          v[4 * j] = xv[j].x; v[4 * j + 1] = xv[j].y; v[4 * j + 2] = xv[j].z; v[4 * j + 3] = xv[j].w;
-        }
-        if (16 * gi >= K) {
-#pragma unroll
-          for (int j = 0; j < 16; ++j) v[j] = 0.f;
-        }
-        float amax = 0.f;
-#pragma unroll
-        for (int j = 0; j < 16; ++j) amax = fmaxf(amax, fabsf(v[j]));
-        const float d = amax / 127.f, id = amax > 0.f ? 127.f / amax : 0.f;
-        int qsum = 0;
-        i32x4 pk;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          int word = 0;
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const int q = (int)rintf(v[4 * j + k] * id);
-            qsum += q;
-            word |= (q & 0xFF) << (8 * k);
-          }
-          pk[j] = word;
-        }
-        lq[slot] = pk;
-        lf[slot] = (f32x2){d, d * (float)qsum};
-      }
-    }
-    // K padding groups beyond the threads' reach stay whatever they were: every group < SB * 16 is
-    // written above (NT * MG >= SB * 16 by the launch rule), the pad / dummy slots are never read
-  }
-  __syncthreads();
-
-  // 4. consume the tiles in issue order; epilogue (+ emission) per tile
-  const int nb = blast + 1;  // rows stored / emitted
-#pragma unroll
-  for (int j = 0; j < J; ++j) {
-    const int t = tile0 + j;
-    if (t >= n_tiles) break;  // block-uniform
-    float acc[1][BT];
-#pragma unroll
-    for (int b = 0; b < BT; ++b) acc[0][b] = 0.f;
-    compute_wtile<QT, NSB, 1, BT>(T[j], SB, sb0, s, lq, lf, XSP, acc, se);
-    if constexpr (KS > 1) {  // partial sums of groups 1.. meet group 0's in LDS
-      if (kg > 0) {
-#pragma unroll
-        for (int b = 0; b < BT; ++b) part[((kg - 1) * BT + b) * GEMV_NT + gtid] = acc[0][b];
-      }
-      __syncthreads();
-      if (kg == 0) {
-#pragma unroll
-        for (int k = 1; k < KS; ++k)
-#pragma unroll
-          for (int b = 0; b < BT; ++b) acc[0][b] += part[((k - 1) * BT + b) * GEMV_NT + gtid];
-      }
-    }
-#pragma unroll
-    for (int b = 0; b < BT; ++b) acc[0][b] *= rstd[b];
-    if constexpr (EMIT == EM_NONE) {
-      if (kg == 0) finish_rows<1, BT>(P, acc, t * 16 + rbase, N, 0, s);
-    } else {
-      const int n = t * 16 + rbase;
-      float v[BT], pv[BT];
-#pragma unroll
-      for (int b = 0; b < BT; ++b) {
-        v[b] = row16_sum(acc[0][b]);
-        pv[b] = __shfl_xor(v[b], 16, OMX_WAVE);  // row rbase ^ 1 (GLU partner)
-      }
-      if constexpr (EMIT == EM_ADD) {
-        if (kg == 0 && s == 0) {
-#pragma unroll
-          for (int b = 0; b < BT; ++b) {
-            float nv = 0.f;
-            if (n < N && b < nb) {
-              float* dst = P.y + (long long)b * P.ldy + n;
-              nv = *dst + v[b] + (P.bias ? P.bias[n] : 0.f);
-              *dst = nv;
-            }
-            stage[32 * b + rbase] = n < N ? nv * P.emit8_nw[n] : 0.f;
-            stage[32 * b + 16 + rbase] = nv * nv;
-          }
-        }
-        __syncthreads();
-        if (tid < nb)
-          emit_group((char*)P.emit8 + (size_t)tid * x8_slots_dev(N) * 24, N, t, stage + 32 * tid, stage + 32 * tid + 16,
-                     P.emit8_stat + tid * x8_stat_ld_dev(N));
-        __syncthreads();  // the stage is reused by the next tile
-      } else {  // EM_GLU: even row = gate, odd = up; 8 outputs per tile, a group per tile pair
-        const int half = (t & 1) * 8;
-        if (kg == 0 && s == 0 && (rbase & 1) == 0) {
-#pragma unroll
-          for (int b = 0; b < BT; ++b) {
-            const float h = n < N ? (P.epi == EPI_GEGLU ? gelu_tanh(v[b]) : silu(v[b])) * pv[b] : 0.f;
-            if (n < N && b < nb) P.y[(long long)b * P.ldy + (n >> 1)] = h;
-            stage[32 * b + half + (rbase >> 1)] = h;
-            if (half == 0 && t + 1 >= n_tiles) stage[32 * b + 8 + (rbase >> 1)] = 0.f;  // trailing half group
-          }
-        }
-        if ((t & 1) || t + 1 >= n_tiles) {
-          __syncthreads();
-          if (tid < nb)
-            emit_group<WT>((char*)P.emit8 + (size_t)tid * x8_slots_dev(N / 2) * 24, N / 2, t >> 1, stage + 32 * tid,
-                           nullptr, nullptr);
-          __syncthreads();
-        }
-      }
-    }
-    if constexpr (KS > 1) __syncthreads();  // part is reused by the next tile
-  }
-}
 
 template <int QT, int NSB, int J, int KS, int IN, int MS, int EMIT, int BT>
 __global__ __launch_bounds__(GEMV_NT * KS) void qgemv8_kernel(GemvParams P) {
@@ -607,6 +358,7 @@ bool gemv8_supported(const GemvParams& P) {
 bool gemv8(const GemvParams& P, hipStream_t s) {
   Geo G;
   if (!covered(P, G) || !launchable(P, G)) return false;
+  count_launch(P.B > 1 ? LC_GEMV8_ROWS : LC_GEMV8_ROW1);
   switch (P.w.qtype) {
     case QT_Q4_K: launch_q<QT_Q4_K>(P, G, s); return true;
     case QT_Q6_K: launch_q<QT_Q6_K>(P, G, s); return true;
@@ -622,6 +374,7 @@ bool gemv8_2(const GemvParams& A, const GemvParams& B, hipStream_t s) {
   if (!A.x8 || !B.x8 || A.x8 != B.x8 || A.emit8 || B.emit8 || A.w.K != B.w.K || A.B != B.B) return false;
   if (!covered(A, GA) || !covered(B, GB) || GA.nsb != 1 || GA.ks != 1 || GB.nsb != 1 || GB.ks != 1) return false;
   const int gxa = (A.w.N + 15) / 16, gxb = (B.w.N + 15) / 16;  // one tile per block on both sides
+  count_launch(LC_GEMV8_DUAL);
   switch (A.w.qtype) {
     case QT_Q4_K: return dual_b<QT_Q4_K>(A, B, gxa, gxb, s);
     case QT_Q5_K: return dual_b<QT_Q5_K>(A, B, gxa, gxb, s);

@@ -187,7 +187,7 @@ __global__ __launch_bounds__(GEMV_NT) void qgemv_batch_kernel(GemvParams P) {
     float acc[1][BT];
 #pragma unroll
     for (int b = 0; b < BT; ++b) acc[0][b] = 0.f;
-    compute_wtile<QT, NSB, 1, BT>(T[j], SB, 0, s, lq, lf, XS, acc);
+    compute_wtile<QT, NSB, 1, BT, false>(T[j], SB, 0, s, lq, lf, XS, acc);
     finish_rows<1, BT>(P, acc, t * ROWS_B + rbase, N, b0, s);
   }
 }

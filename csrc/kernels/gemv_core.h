@@ -59,6 +59,17 @@ struct WTile {
 // its vmcnt wait first); LDS reads (activation fragments) and SALU may
 #define OMX_PIECE_ORDER() __builtin_amdgcn_sched_barrier(0x0104)
 
+// A sched_barrier only binds the machine scheduler: the SelectionDAG scheduler that runs before it
+// still hoists pure VALU across it, and did -- the disassembly of the K-split down GEMV showed every
+// piece's nibble masks hoisted to the top of the tile, behind ONE s_waitcnt vmcnt(0), so no dot
+// product started before the block's last weight byte had landed (Q6_K: vmcnt(3) after piece 0).
+// pin() redefines a loaded register through an empty volatile asm at the point where its piece is
+// consumed: volatile asm statements keep program order, nothing that reads the value can move above
+// its pin, and the waitcnt pass places that load's (counted) vmcnt wait right there.
+__device__ __forceinline__ void pin(u32x4& v) { asm volatile("" : "+v"(v)); }
+__device__ __forceinline__ void pin(u32x2& v) { asm volatile("" : "+v"(v)); }
+__device__ __forceinline__ void pin(unsigned& v) { asm volatile("" : "+v"(v)); }
+
 template <int QT, int NSB, int R>
 __device__ __forceinline__ void load_wtile(const QMat& w, long long row_base, int row0, int N, int SB, int sb0,
                                            int s, WTile<QT, NSB, R>& T, int se = -1) {
@@ -152,15 +163,35 @@ __device__ __forceinline__ void load_x(const i32x4* xq, const f32x2* xf, int XS,
   }
 }
 
-template <int QT, int NSB, int R, int BT>
-__device__ __forceinline__ void compute_wtile(const WTile<QT, NSB, R>& T, int SB, int sb0, int s, const i32x4* xq,
+// PIN: pin each piece where it is consumed (see pin()); off for the register-heaviest instantiations
+// (many batch rows x tiles in flight), where holding every piece until its turn spills
+template <int QT, int NSB, int R, int BT, bool PIN = true>
+__device__ __forceinline__ void compute_wtile(WTile<QT, NSB, R>& T, int SB, int sb0, int s, const i32x4* xq,
                                               const f32x2* xf, int XS, float (&acc)[R][BT], int se = -1) {
   if (se < 0) se = SB;
+  // piece t of super-block i: its weight registers, pinned where the piece is consumed (see pin())
+  auto pin_piece = [&](int i, int t) {
+    if constexpr (!PIN) return;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      pin(T.a[r][i][t]);
+      if constexpr (WTile<QT, NSB, R>::Q8) pin(T.b[r][i][t]);
+      if constexpr (WTile<QT, NSB, R>::Q6) pin(T.h[r][i][t]);
+      if constexpr (WTile<QT, NSB, R>::Q5) pin(T.q5h[r][i][t]);
+    }
+  };
 #pragma unroll
   for (int i = 0; i < NSB; ++i) {
     const int sb = sb0 + s + 16 * i;
     if (sb >= se) continue;
     const int xs0 = sb * XPAD;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if constexpr (PIN) {
+        pin(T.m[r][i]);
+        if constexpr (WTile<QT, NSB, R>::Q6D) pin(T.d[r][i]);
+      }
+    }
     if constexpr (QT == QT_Q5_K) {
       // w = d*sc*q - dmin*m, q = nibble | (5th bit << 4) in 0..31 (unsigned int8 codes)
       float d[R], dm[R];
@@ -190,6 +221,7 @@ __device__ __forceinline__ void compute_wtile(const WTile<QT, NSB, R>& T, int SB
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           const int t = 2 * c + h, gl = 4 * c + h;
+          pin_piece(i, t);
           XFr<BT> x;
           load_x<BT>(xq, xf, XS, xs0 + gl, xs0 + gl + 2, x);
 #pragma unroll
@@ -245,6 +277,7 @@ __device__ __forceinline__ void compute_wtile(const WTile<QT, NSB, R>& T, int SB
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           const int t = 2 * c + h, gl = 4 * c + h;
+          pin_piece(i, t);
           XFr<BT> x;
           load_x<BT>(xq, xf, XS, xs0 + gl, xs0 + gl + 2, x);
 #pragma unroll
@@ -269,6 +302,7 @@ __device__ __forceinline__ void compute_wtile(const WTile<QT, NSB, R>& T, int SB
 #pragma unroll
       for (int t = 0; t < 8; ++t) {
         const int n = t >> 2, sub = t & 3, il_ = 8 * n + sub, ih_ = il_ + 4;
+        pin_piece(i, t);
         XFr<BT> x;
         load_x<BT>(xq, xf, XS, xs0 + il_, xs0 + ih_, x);
 #pragma unroll
@@ -291,6 +325,7 @@ __device__ __forceinline__ void compute_wtile(const WTile<QT, NSB, R>& T, int SB
 #pragma unroll
       for (int t = 0; t < 8; ++t) {
         const int n = t >> 2, sub = t & 3, il_ = 8 * n + sub, ih_ = il_ + 4;
+        pin_piece(i, t);
         XFr<BT> x;
         load_x<BT>(xq, xf, XS, xs0 + il_, xs0 + ih_, x);
 #pragma unroll
@@ -320,6 +355,7 @@ __device__ __forceinline__ void compute_wtile(const WTile<QT, NSB, R>& T, int SB
       // Q4_0: w = d*(n - 8), lo nibble unsigned, hi nibble signed; Q8_0: w = d*q
 #pragma unroll
       for (int t = 0; t < 8; ++t) {
+        pin_piece(i, t);
         XFr<BT> x;
         load_x<BT>(xq, xf, XS, xs0 + 2 * t, xs0 + 2 * t + 1, x);
 #pragma unroll

@@ -829,6 +829,7 @@ bool gemv_mb2(const GemvParams& A, const GemvParams& Bp, hipStream_t s) {
   };
   if (nsbw == 1) go(gemv_mb2_kernel<QT_Q4_K, QT_Q6_K, 1, 4, AM_G16>);
   else go(gemv_mb2_kernel<QT_Q4_K, QT_Q6_K, 2, 3, AM_G16>);
+  count_launch(LC_GEMV_MB);
   return true;
 }
 
@@ -838,7 +839,9 @@ bool gemv_mb(const GemvParams& P, hipStream_t s) {
   const size_t lds = mb_lds_bytes(P.B, P.w.K, am);
   auto go = [&](auto qt) {
     constexpr int QT = decltype(qt)::value;
-    return am == AM_G16 ? mb_q<QT, AM_G16>(P, lds, s) : mb_q<QT, AM_LDS>(P, lds, s);
+    const bool ok = am == AM_G16 ? mb_q<QT, AM_G16>(P, lds, s) : mb_q<QT, AM_LDS>(P, lds, s);
+    if (ok) count_launch(LC_GEMV_MB);
+    return ok;
   };
   switch (P.w.qtype) {
     case QT_Q4_K: return go(std::integral_constant<int, QT_Q4_K>{});

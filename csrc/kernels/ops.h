@@ -109,6 +109,10 @@ bool gemv8_supported(const GemvParams& P);
 // sync: 16 zeroed ints of device memory (counters + error word); false = not covered (two launches)
 bool gemv8_ffn(const GemvParams& G, const GemvParams& D, void* sync, hipStream_t s);
 struct AttnParams;
+// QKV (A: q,k rows or all rows, x8 RMS image in, EPI_QKV; B: v rows or B.w.s0 null) + paged attention in
+// one launch (qkv_attn.hip); the attention output lands as the O projection's int8 image `img`
+// (x8_bytes(H * D), pad slots zero); sync: the x8sync words. false = not covered
+bool qkv_attn(const GemvParams& A, const GemvParams& B, const AttnParams& At, void* img, void* sync, hipStream_t s);
 // QKV (A: q,k rows or all rows; B: v rows or B.w.s0 null) + paged attention + O projection (O.x8 = the
 // attention image, EPI_ADD + emission) in one launch (attn8.hip); false = not covered
 bool attn8(const GemvParams& A, const GemvParams& B, const GemvParams& O, const AttnParams& At, void* sync,
@@ -259,8 +263,33 @@ struct ARParams {
 };
 // y[0:n] += sum_r slab_r[slab][0:n]  (n % 4 == 0), same bits on every rank
 void ar_allreduce_add(const ARParams& P, int slab, float* y, int n, hipStream_t s);
+// the same, then the new residual rows b < B (E each) are emitted as the int8 chain's image of
+// (y * nw) + RMS partials (gemv8.hip consumer layout, row b at b * x8_bytes(E)); false = not covered
+bool ar_allreduce_add_emit(const ARParams& P, int slab, float* y, int E, int B, void* img, const float* nw, float* stat,
+                           hipStream_t s);
 // out[row][r * n_local + j] = slab_r[slab][row * n_local + j]
 void ar_allgather(const ARParams& P, int slab, float* out, int rows, int n_local, int ld_out, hipStream_t s);
+
+// Launch counters: which kernel family a host call actually enqueued (a tested path must not silently
+// become another one -- e.g. dq_gemm() declining and gemm() taking the old tile kernel). Counted on
+// the host per enqueue (a captured graph counts at capture); tests reset, run, and assert.
+enum {
+  LC_DQ_GEMM = 0,    // gemm_dq.hip stream-order MFMA prefill GEMM
+  LC_GEMM_TILE,      // gemm.hip 128 x 128 tile GEMM (< 128 rows, or a declined dq shape)
+  LC_GEMM_LIB,       // hipBLASLt path (OMX_GEMM_LIB_MIN_M)
+  LC_GEMV8_ROW1,     // gemv8.hip int8 chain, one row
+  LC_GEMV8_ROWS,     // gemv8.hip int8 chain, 2..4 batched rows
+  LC_GEMV8_DUAL,     // gemv8.hip q,k + v dual launch
+  LC_GEMV_MB,        // gemv_mfma.hip layout-M matrix-core batched GEMV (single or dual)
+  LC_GEMV_FLIGHT,    // gemv.hip / gemv_batch.hip fp32-prologue GEMVs
+  LC_ATTN_DECODE,    // attention.hip split flash-decode kernel
+  LC_ATTN_PREFILL,   // attention.hip MFMA flash prefill
+  LC_QKV_ATTN,       // qkv_attn.hip fused QKV + attention (batch-1 decode, short context)
+  LC_N
+};
+void count_launch(int which);
+long long launch_count(int which);
+void reset_launch_counts();
 
 // small elementwise helpers
 void add_inplace(float* y, const float* x, long long n, hipStream_t s);

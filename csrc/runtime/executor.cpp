@@ -79,9 +79,11 @@ bool Executor::chain_capable() const {
 // (+ sum-of-squares partials), gate_up emits down's; consumers skip the fp32 activation prologue.
 // Layer 0's QKV reads the embedding rows through gemv.hip's prologue. Batch 1, and up to ws.x8_bmax
 // (<= X8_MAX_B) continuous-batching rows, which then read each weight tile once for every row.
+// Under tensor parallelism the chain runs inside forward_tp only (the custom all-reduce is what emits
+// the QKV / gate_up / LM-head images there: ar_allreduce_add_emit); the RCCL prefill path keeps fp32.
 bool Executor::x8(const StepInputs& in) const {
-  return ws.x8_ok && (in.B == 1 || in.B <= ws.x8_bmax) && !in.prefill && cfg.tp == 1 && cfg.arch == 0 &&
-         cfg.n_expert == 0;
+  return ws.x8_ok && (in.B == 1 || in.B <= ws.x8_bmax) && !in.prefill && (cfg.tp == 1 || ar_active_) &&
+         cfg.arch == 0 && cfg.n_expert == 0;
 }
 
 static void x8_in(GemvParams& P, const void* img, const float* stat) {
@@ -99,8 +101,8 @@ static void x8_emit(GemvParams& P, void* img, const float* nw, float* stat) {
 // residual / GLU rows too); an emitter the int8 kernel does not cover would leave its consumer a stale
 // image, so the chain is on only when every emitter is covered
 bool Executor::x8_capable(int B) const {
-  if (cfg.tp != 1 || cfg.arch != 0 || cfg.n_expert != 0 || layers.empty() || !ws.x8e || !ws.x8f || !ws.x8st)
-    return false;
+  if (cfg.arch != 0 || cfg.n_expert != 0 || layers.empty() || !ws.x8e || !ws.x8f || !ws.x8st) return false;
+  const bool tp = cfg.tp > 1;  // O and down write partial sums to the all-reduce slabs, which emits
   static const float dummy[4] = {0.f, 0.f, 0.f, 0.f};
   for (const LayerW& L : layers) {
     GemvParams O{};
@@ -108,7 +110,7 @@ bool Executor::x8_capable(int B) const {
     O.B = B;
     O.epi = EPI_ADD;
     O.n_sel = 1;
-    x8_emit(O, (void*)dummy, dummy, (float*)dummy);
+    x8_emit(O, (void*)dummy, dummy, (float*)dummy);  // (TP: O only writes slab partials, not checked)
     GemvParams G{};
     G.w = L.wgu;
     G.B = B;
@@ -119,13 +121,14 @@ bool Executor::x8_capable(int B) const {
     GemvParams D{};
     D.w = L.wdown;
     D.B = B;
-    D.epi = EPI_ADD;
+    D.epi = tp ? EPI_STORE : EPI_ADD;
     D.n_sel = 1;
     x8_in(D, dummy, nullptr);
-    x8_emit(D, (void*)dummy, dummy, (float*)dummy);
-    if (!gemv8_supported(O) || !gemv8_supported(G) || !gemv8_supported(D)) return false;
+    if (!tp) x8_emit(D, (void*)dummy, dummy, (float*)dummy);
+    if ((!tp && !gemv8_supported(O)) || !gemv8_supported(G) || !gemv8_supported(D)) return false;
   }
-  return true;
+  // TP: the all-reduce emits the images (ar_allreduce_add_emit covers E % 16 == 0, <= 4 rows)
+  return !tp || (cfg.E % 16 == 0 && B <= 4);
 }
 
 void Executor::embed(const StepInputs& in, hipStream_t s) {
@@ -162,7 +165,46 @@ void Executor::attn_block(int i, const StepInputs& in, hipStream_t s) {
   const bool q8 = x8(in);
   if (ch && i > 0) chain_in(P, ws.xa16, ws.ld_e, ws.st[1], (E + 15) / 16);  // emitted by layer i-1's down
   if (q8 && i > 0) x8_in(P, ws.x8e, ws.x8st);                                 // emitted by layer i-1's down
-  if (q8 && i > 0 && B == 1 && ws.attn_fuse && ws.x8q && !phi) {  // QKV + attention + O in one launch (attn8.hip)
+  if (q8 && i > 0 && B == 1 && ws.attn_fuse == 2 && ws.x8q && !phi) {
+    // QKV + attention in one launch (qkv_attn.hip): the attention lands as O's int8 image
+    GemvParams V{};
+    if (!L.qkv_fused) {
+      V = P;
+      V.w = L.wv;
+      V.row_offset = Eq + Ekv;
+    }
+    AttnParams A{};
+    A.block_table = in.block_table;
+    A.max_blocks = in.max_blocks;
+    A.q_seq = in.q_seq;
+    A.q_len = in.q_len;
+    A.NQ = B;
+    A.H = cfg.H;
+    A.n_kv = cfg.Hkv;
+    A.D = cfg.Dc > 0 ? cfg.Dc : cfg.D;
+    A.Dv = cfg.D;
+    A.bs = in.bs;
+    A.scale = 1.0f / std::sqrt((float)cfg.D);
+    A.window = cfg.window;
+    if (A.D == A.Dv && qkv_attn(P, V, A, ws.x8q, ws.x8sync, s)) {
+      ++n_qkv_attn;
+      GemvParams O = base_params(L.wo, B, ws.abuf, Eq, ws);
+      O.bias = L.bo;
+      O.ldy = E;
+      x8_in(O, ws.x8q, nullptr);
+      if (cfg.tp > 1) {  // partial sums to this rank's all-reduce slab (it emits gate_up's image)
+        O.epi = EPI_STORE;
+        O.y = tp_dst(0, B);
+      } else {
+        O.epi = EPI_ADD;
+        O.y = ws.resid;
+        x8_emit(O, ws.x8e, L.ffn_norm, ws.x8st);  // gate_up's RMSNorm input, int8
+      }
+      gemv(O, s);
+      return;
+    }
+  }
+  if (q8 && i > 0 && B == 1 && ws.attn_fuse == 1 && ws.x8q && !phi) {  // QKV + attention + O in one launch (attn8.hip)
     GemvParams V{};
     if (!L.qkv_fused) {
       V = P;
@@ -281,7 +323,7 @@ void Executor::attn_block(int i, const StepInputs& in, hipStream_t s) {
     chain_in(O, ws.a16, ws.ld_q, nullptr, 0);
     chain_emit(O, ws.xa16, ws.ld_e, L.ffn_norm, ws.st[0]);  // gate_up's RMSNorm input
   }
-  if (q8) x8_emit(O, ws.x8e, L.ffn_norm, ws.x8st);  // gate_up's RMSNorm input, int8
+  if (q8 && cfg.tp == 1) x8_emit(O, ws.x8e, L.ffn_norm, ws.x8st);  // gate_up's RMSNorm input, int8
   gemv(O, s);
 }
 
@@ -412,7 +454,9 @@ void Executor::ffn_block(int i, const StepInputs& in, hipStream_t s) {
     chain_in(Dn, ws.h16, ws.ld_f, nullptr, 0);
     chain_emit(Dn, ws.xa16, ws.ld_e, i + 1 < (int)layers.size() ? layers[i + 1].attn_norm : out_norm, ws.st[1]);
   }
-  if (q8) {
+  if (q8 && cfg.tp > 1) {
+    x8_in(Dn, ws.x8f, nullptr);  // partial sums to the slab: the all-reduce emits the next image
+  } else if (q8) {
     x8_in(Dn, ws.x8f, nullptr);
     x8_emit(Dn, ws.x8e, i + 1 < (int)layers.size() ? layers[i + 1].attn_norm : out_norm, ws.x8st);
     if (ws.x8_fuse && B == 1 && gemv8_ffn(G, Dn, ws.x8sync, s)) {  // one launch, in-kernel hand-off
@@ -467,11 +511,26 @@ void Executor::forward_tp(const StepInputs& in, hipStream_t s) {
     ~Active() { f = 0; }
   } active(ar_active_);
   embed(in, s);
+  const bool q8 = x8(in);
   for (int i = 0; i < cfg.n_layer; ++i) {
     attn_block(i, in, s);
-    ar_allreduce_add(ws.ar, 0, ws.resid, n, s);  // resid += sum of the ranks' O partials
+    // resid += sum of the ranks' O partials; on the int8 chain the same kernel emits gate_up's image
+    // (the consumers read that image whenever the chain is on: an emission the kernel declines must
+    // fail loudly, never leave them a stale one)
+    if (q8) {
+      if (!ar_allreduce_add_emit(ws.ar, 0, ws.resid, cfg.E, in.B, ws.x8e, layers[i].ffn_norm, ws.x8st, s))
+        throw std::runtime_error("forward_tp: int8-chain all-reduce emission not covered");
+    } else {
+      ar_allreduce_add(ws.ar, 0, ws.resid, n, s);
+    }
     ffn_block(i, in, s);
-    ar_allreduce_add(ws.ar, 1, ws.resid, n, s);
+    const float* nxt = i + 1 < cfg.n_layer ? layers[i + 1].attn_norm : out_norm;  // next QKV / LM head
+    if (q8) {
+      if (!ar_allreduce_add_emit(ws.ar, 1, ws.resid, cfg.E, in.B, ws.x8e, nxt, ws.x8st, s))
+        throw std::runtime_error("forward_tp: int8-chain all-reduce emission not covered");
+    } else {
+      ar_allreduce_add(ws.ar, 1, ws.resid, n, s);
+    }
   }
   if (in.n_logits > 0) {
     StepInputs h = in;

@@ -112,7 +112,16 @@ class NativeExec:
         S, defer = self.r.split_plan(B)
         # batch-1 decode over <= 512 keys: QKV + attention + O in one launch (attn8.hip), when the
         # executor covers the shapes (it falls back to the split attention kernel otherwise)
-        fuse = int(B == 1 and self.r._decode_S in (1, 2, 4) and self.r.attn_fuse)
+        # the fused launches stage at most A8_MAXBT = 64 block-table entries: fuse only while S *
+        # defer_kps keys fit. 1: QKV + attention + O (attn8.hip, opt-in OMX_ATTN_FUSE=1); 2: QKV +
+        # attention (qkv_attn.hip, opt-in up to OMX_QKV_ATTN_MAXS splits' worth of keys)
+        S_ = self.r._decode_S
+        fits = S_ * self.r.defer_kps <= 64 * self.r.block_size
+        fuse = 0
+        if B == 1 and fits and S_ in (1, 2, 4) and self.r.attn_fuse:
+            fuse = 1
+        elif B == 1 and fits and 1 <= S_ <= self.r.qkv_attn_maxs:
+            fuse = 2
         self.exe.set_splits(S, defer, fuse)
         self.exe.step(self.stages[stage], layer, B, n_logits, use_idx, prefill, stream_handle() if self.on_gpu else 0)
 
@@ -213,6 +222,16 @@ class Runner:
                                 x8q=torch.zeros(C.x8_bytes(Eq), **u8),
                                 x8sync=torch.zeros(128, device=dev, dtype=torch.int32))
         self.attn_fuse = os.environ.get("OMX_ATTN_FUSE", "0") != "0"
+        # batch-1 decode over <= OMX_QKV_ATTN_MAXS x defer_kps keys: QKV + attention in one launch
+        # (qkv_attn.hip). Off by default: 17.8-18.1 us per layer against 8.0 + 5.7 for the two launches
+        # (profiles/r5_decode): the last arriver's single-block attention trails the QKV tail
+        self.qkv_attn_maxs = int(os.environ.get("OMX_QKV_ATTN_MAXS", "0")) if self.x8_bufs is not None else 0
+        # the in-launch hand-offs of the opt-in fused paths (attn8 / ffn8) report a timeout or an
+        # over-long block table through an error word: checked after every fused decode step
+        self._fused_check = self.x8_bufs is not None and (
+            self.attn_fuse or os.environ.get("OMX_X8_FUSE", "0") != "0")
+        # (qkv_attn can raise the same error word only past the staged block table, which the host's
+        # `fits` bound in NativeExec.run never lets a fused step reach)
         # MoE prefill grouping (csrc/kernels/moe.hip moe_sort -> grouped MFMA GEMM)
         n_pairs = max_batch * ksel
         self.moe_rows = torch.zeros(n_pairs, **i32)
@@ -662,6 +681,13 @@ class Runner:
                     self._decode_body(B)
             if self.is_gpu:
                 self._adv_next = (sids[0], poss[0] + 1) if B == 1 else (tuple(sids), tuple(p + 1 for p in poss))
+            if self._fused_check and B == 1:
+                err = self.x8_error()
+                if err:
+                    self.x8_bufs["x8sync"].zero_()
+                    raise RuntimeError("fused decode step (OMX_ATTN_FUSE / OMX_X8_FUSE): an in-launch hand-off "
+                                       "timed out or the sequence exceeded the staged block table; the step's "
+                                       "logits are invalid")
         finally:
             self._decode_S = 0
 

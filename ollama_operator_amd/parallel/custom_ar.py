@@ -77,6 +77,12 @@ class CustomAllReduce:
     def all_reduce_add(self, slab: int, y_ptr: int, n: int, stream: int) -> None:
         self.C.ar_allreduce_add(self.params, slab, y_ptr, n, stream)
 
+    def all_reduce_add_emit(self, slab: int, y_ptr: int, E: int, B: int, img_ptr: int, nw_ptr: int, stat_ptr: int,
+                            stream: int) -> None:
+        """y[:B*E] += sum of the ranks' slabs, then each new row is written as the int8 activation image
+        of y * nw (+ per-16 sums of squares) for the next GEMV (executor forward_tp, int8 chain)."""
+        self.C.ar_allreduce_add_emit(self.params, slab, y_ptr, E, B, img_ptr, nw_ptr, stat_ptr, stream)
+
     def all_gather(self, slab: int, out_ptr: int, rows: int, n_local: int, ld_out: int, stream: int) -> None:
         self.C.ar_allgather(self.params, slab, out_ptr, rows, n_local, ld_out, stream)
 

@@ -154,6 +154,72 @@ def test_custom_allreduce_stalled_peer_times_out(tmp_path):
     assert raised == 1.0
 
 
+def _emit_worker(rank, world, port, out_dir):
+    """the fused all-reduce + residual + int8-chain emission (ar_allreduce_add_emit), 2 batch rows"""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        from ollama_operator_amd.ops import native
+        from ollama_operator_amd.parallel.custom_ar import CustomAllReduce
+        C = native()
+        E, B = 4096, 2
+        ar = CustomAllReduce(dist.group.WORLD, rank, world, B * E, timeout_s=10)
+        g = torch.Generator().manual_seed(3)
+        parts = [torch.randn(B * E, generator=g) for _ in range(world)]
+        y0 = torch.randn(B * E, generator=g)
+        nw = torch.rand(E, generator=g) + 0.5
+        s = torch.cuda.current_stream().cuda_stream
+        x = parts[rank].cuda()
+        y = y0.cuda()
+        nwd = nw.cuda()
+        img = torch.zeros(B * C.x8_bytes(E), dtype=torch.uint8, device="cuda")
+        st = torch.zeros(B * C.x8_stat_ld(E) + 4, device="cuda")
+        C.copy_d2d(ar.slab_ptr(1), x.data_ptr(), 4 * B * E, s)
+        ar.all_reduce_add_emit(1, y.data_ptr(), E, B, img.data_ptr(), nwd.data_ptr(), st.data_ptr(), s)
+        torch.cuda.synchronize()
+        ar.check()
+        ref = y0.clone()
+        for t in parts:
+            ref = ref + t
+        np.save(os.path.join(out_dir, f"ey{rank}.npy"), y.cpu().numpy())
+        np.save(os.path.join(out_dir, f"eref{rank}.npy"), ref.numpy())
+        np.save(os.path.join(out_dir, f"eimg{rank}.npy"), img.cpu().numpy())
+        np.save(os.path.join(out_dir, f"est{rank}.npy"), st.cpu().numpy())
+        np.save(os.path.join(out_dir, "enw.npy"), nw.numpy())
+        ar.close()
+    finally:
+        dist.barrier()
+        os._exit(0)
+
+
+def test_allreduce_emits_int8_chain_image(tmp_path):
+    """TP decode on the int8 chain: the all-reduce itself writes the next GEMV's image + RMS partials."""
+    from test_gemv8_gpu import decode_image
+    from ollama_operator_amd.ops import native
+    world, E, B = 2, 4096, 2
+    mp.start_processes(_emit_worker, args=(world, _port(), str(tmp_path)), nprocs=world, start_method="spawn",
+                       join=True)
+    C = native()
+    nw = np.load(tmp_path / "enw.npy")
+    img0 = np.load(tmp_path / "eimg0.npy")
+    for r in range(world):
+        y, ref = np.load(tmp_path / f"ey{r}.npy"), np.load(tmp_path / f"eref{r}.npy")
+        np.testing.assert_allclose(y, ref, rtol=1e-6, atol=1e-6)
+        assert np.array_equal(np.load(tmp_path / f"eimg{r}.npy"), img0)  # identical on every rank
+    st = np.load(tmp_path / "est0.npy")
+    nb, sl = C.x8_bytes(E), C.x8_stat_ld(E)
+    import torch
+    for b in range(B):
+        yb = ref[b * E:(b + 1) * E]
+        got = decode_image(torch.from_numpy(img0[b * nb:(b + 1) * nb].copy()), E).numpy()
+        want = yb * nw
+        assert np.linalg.norm(got - want) / np.linalg.norm(want) < 1.5e-2
+        np.testing.assert_allclose(st[b * sl:b * sl + E // 16], (yb.reshape(-1, 16) ** 2).sum(1), rtol=1e-4)
+
+
 PROMPT = [1, 17, 42, 99, 7, 300, 12, 5, 77]
 
 
@@ -176,7 +242,11 @@ def _tp_worker(rank, world, port, path, out_dir, mode="custom"):
             assert r.ar is not None and r.use_graphs
         if mode == "long":
             assert not r.exe.ar_fits(32)
+        from ollama_operator_amd.ops import native
+        native().reset_launch_counts()
         np.save(os.path.join(out_dir, f"p{rank}.npy"), _run(r, LONG_PROMPT if mode == "long" else PROMPT))
+        n = native().launch_counts()  # decode graph captured inside _run: its forward_tp kernels counted
+        np.save(os.path.join(out_dir, f"n{rank}.npy"), np.array([n["gemv8_row1"] + n["gemv8_dual"], r.exe.exe.x8_on]))
         if r.ar is not None:
             r.ar.check()
         r.close()
@@ -214,6 +284,10 @@ def test_tp2_graph_decode_matches_tp1(tmp_path, name, ft):
     mp.start_processes(_tp_worker, args=(2, _port(), path, str(tmp_path)), nprocs=2, start_method="spawn",
                        join=True)
     _check_tp(tmp_path, ref)
+    if "mixtral" not in name:  # dense llama ranks decode on the int8 chain (the all-reduce emits its images)
+        for rank in range(2):
+            n8, on = np.load(tmp_path / f"n{rank}.npy")
+            assert on == 1 and n8 > 0, (rank, n8, on)
 
 
 def _check_tp(tmp_path, ref):

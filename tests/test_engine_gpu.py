@@ -90,7 +90,10 @@ def test_prefill_dq_path_vs_torch(tiny_models, name):
     rng = np.random.default_rng(4)
     toks = [1] + [int(x) for x in rng.integers(3, 500, 229)]
     sg, sc = g.new_sequence(), c.new_sequence()
+    C.reset_launch_counts()
     g.prefill(sg, toks)
+    n = C.launch_counts()  # every dense projection ran on the dq kernel, none fell back to the tile GEMM
+    assert n["dq_gemm"] >= 2 * g.cfg.n_layer and n["gemm_tile"] == 0 and n["gemm_lib"] == 0, n
     c.prefill(sc, toks)
     V = g.cfg.n_vocab
     assert rel(g.logits[0, :V].cpu(), c.logits[0, :V]) < 3e-2

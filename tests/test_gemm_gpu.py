@@ -38,14 +38,21 @@ def gemm(m, x, norm=0, nw=None, nb=None, epi=0, y=None, bias=None, extra=None, e
     old, old_dq = C().gemm_lib_min_m(), C().dq_gemm_enabled()
     C().set_gemm_lib_min_m(16 if lib else 0)
     C().set_dq_gemm(1 if path == "dq" else 0)
+    C().reset_launch_counts()
     try:
         C().gemv(m.tup, B, p(x), K, norm, p(nw), p(nb), eps, epi, p(y), y.shape[1], p(bias), 0, d, S())
         torch.cuda.synchronize()
     finally:
         C().set_gemm_lib_min_m(old)
         C().set_dq_gemm(int(old_dq))
+    n = C().launch_counts()
     if lib:  # the library path really ran: the fp32 slab holds the raw products
         assert not torch.isnan(keep[1]).any()
+        assert n["gemm_lib"] == 1, n
+    elif path == "dq":  # the stream-order kernel ran, not a silent fallback to the tile kernel
+        assert n["dq_gemm"] == 1 and n["gemm_tile"] == 0, n
+    elif B >= 16:
+        assert n["gemm_tile"] == 1 and n["dq_gemm"] == 0, n
 
 
 @pytest.mark.parametrize("qt", QTYPES)

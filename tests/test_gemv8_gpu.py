@@ -51,8 +51,11 @@ def decode_image(img: torch.Tensor, K: int) -> torch.Tensor:
 
 
 def call(m, B, x, y, epi, ops, ldy=None):
+    C().reset_launch_counts()
     C().gemv(m.tup, B, x.data_ptr() if x is not None else 0, m.tup[5], 0, 0, 0, 1e-5, epi, y.data_ptr(),
              ldy or y.shape[-1], 0, 0, ops, S())
+    n = C().launch_counts()  # the int8-chain kernel ran, not the fp32-prologue fallback
+    assert n["gemv8_row1" if B == 1 else "gemv8_rows"] == 1 and n["gemv_flight"] == 0, n
 
 
 @pytest.mark.parametrize("qt", [GGMLType.Q4_K, GGMLType.Q6_K, GGMLType.Q4_0, GGMLType.Q8_0, GGMLType.Q5_K])
@@ -167,10 +170,19 @@ def test_engine_x8_chain_on_and_matches_torch(tmp_path):
     g.prefill(sg, prompt)
     c.prefill(sc, prompt)
     V = g.cfg.n_vocab
-    for t in [8, 9, 10, 11, 12]:
+    L = g.cfg.n_layer
+    for i, t in enumerate([8, 9, 10, 11, 12]):
         g.set_tokens([t])
+        eager = i == 4  # the last step eagerly: launch counters count enqueues, a graph replay enqueues none
+        g.use_graphs = not eager
+        C().reset_launch_counts()
         g.decode_step(sg)
         torch.cuda.synchronize()
+        if eager:
+            n = C().launch_counts()
+            # every projection of every layer on the int8 chain (QKV, O, gate_up, down; LM head); only
+            # layer 0's QKV reads the embedding rows through the fp32 prologue
+            assert n["gemv8_row1"] + n["gemv8_dual"] >= 4 * L and n["gemv_flight"] <= 1, n
         g.kv.seqs[sg].tokens.append(t)
         c.prefill(sc, [t])
         assert rel(g.logits[0, :V].cpu(), c.logits[0, :V]) < 3e-2
