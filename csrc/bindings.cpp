@@ -234,6 +234,7 @@ PYBIND11_MODULE(_C, m) {
     P.emit8 = Pp<void>(ip("emit8"));
     P.emit8_nw = Pp<const float>(ip("emit8_nw"));
     P.emit8_stat = Pp<float>(ip("emit8_stat"));
+    P.dbg8 = ii("dbg8");
     if (qkv.contains("merge_S")) {
       P.merge_S = ii("merge_S");
       P.merge_ml = Pp<const float>(ip("merge_ml"));
@@ -303,7 +304,7 @@ PYBIND11_MODULE(_C, m) {
   // launch counters (ops.h LC_*): tests assert which kernel family a call enqueued
   m.def("launch_counts", []() {
     static const char* names[LC_N] = {"dq_gemm", "gemm_tile", "gemm_lib", "gemv8_row1", "gemv8_rows", "gemv8_dual",
-                                      "gemv_mb", "gemv_flight", "attn_decode", "attn_prefill", "qkv_attn"};
+                                      "gemv_mb", "gemv_flight", "attn_decode", "attn_prefill", "qkv_attn", "attn_o"};
     py::dict d;
     for (int i = 0; i < LC_N; ++i) d[names[i]] = launch_count(i);
     return d;
@@ -531,6 +532,8 @@ PYBIND11_MODULE(_C, m) {
         w.x8sync = Pp<void>(ptr("x8sync"));
         w.x8q = Pp<void>(ptr("x8q"));
         w.x8_fuse = d.contains("x8_fuse") ? d["x8_fuse"].cast<int>() : 1;
+        w.attn_o = d.contains("attn_o") ? d["attn_o"].cast<int>() : 0;
+        w.attn_o_kps = d.contains("attn_o_kps") ? d["attn_o_kps"].cast<int>() : 0;
         w.x8_ok = (d.contains("x8_ok") ? d["x8_ok"].cast<int>() : 0) && e.x8_capable() ? 1 : 0;
         {  // continuous-batching rows on the chain: as many as asked for and every emitter covers
           const int want = d.contains("x8_bmax") ? d["x8_bmax"].cast<int>() : 1;
@@ -544,6 +547,7 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("n_attn8", [](const Executor& e) { return e.n_attn8; })
       .def_property_readonly("n_ffn8", [](const Executor& e) { return e.n_ffn8; })
       .def_property_readonly("n_qkv_attn", [](const Executor& e) { return e.n_qkv_attn; })
+      .def_property_readonly("n_attn_o", [](const Executor& e) { return e.n_attn_o; })
       .def("set_segments", [](Executor& e, std::vector<std::pair<int, int>> segs) { e.segments = std::move(segs); })
       .def("set_splits", [](Executor& e, int n, int defer, int fuse) {
         e.ws.n_splits = n;

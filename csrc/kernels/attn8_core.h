@@ -69,31 +69,42 @@ __device__ __forceinline__ f16x8 kv_load(const f16* p, bool fresh) {
   return __builtin_bit_cast(f16x8, r);
 }
 
-// G query heads of KV group g over keys [0, len) by one 4-wave block: 16 key groups of 16 lanes (8
-// dims each), U keys per group per step, two steps in flight; merged output quantised into the O
-// projection's image (write-through)
-template <int G>
-__device__ void attn_group(const Attn8Params& P, int g, char* smem) {
+// G query heads of KV group g over keys [k0, k1) by one 4-wave block: 16 key groups of 16 lanes (8
+// dims each), U keys per group per step, two steps in flight. Leaves the per-wave (m, l, acc) of each
+// head in sm[4][G][D + 2] (block-synchronised); attn_merge4 folds the 4 waves. SAME: q / k / v of the
+// current token were written by THIS launch (write-through stores): q and the newest key are read
+// with sc1 loads; otherwise every load is plain (an earlier launch wrote them).
+// Staged block-table entries: at most A8_MAXBT; a longer range raises the error word (sync[66]) and
+// attends to none of the keys beyond it rather than writing past the LDS allocation (hosts never
+// launch such a range).
+template <int G, bool SAME>
+__device__ void attn_core(const Attn8Params& P, int g, int k0, int k1, float* sm, int* sbt) {
   constexpr int D = A8_D, DPL = 8, NG = 16, U = A8_U, STEP = NG * U;
   const GemvParams& A = P.A;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, grp = wave * 4 + (lane >> 4), li = lane & 15;
   const int len_all = P.q_len[0];
   const int seq = P.q_seq ? P.q_seq[0] : 0;
   const int bs = A.bs, Dc = A.Dc > 0 ? A.Dc : D, Hkv = P.Hkv;
-  float* sm = (float*)smem;                   // [4][G][D + 2]
-  float* ob = sm + 4 * G * (D + 2);           // [G][D]
-  int* sbt = (int*)(ob + G * D);              // [A8_MAXBT]
-  // the staged block table holds A8_MAXBT entries: a longer sequence (the host fuses only up to
-  // 4 x defer_kps keys, attn8() checks that bound) raises the error word and attends to none of
-  // the blocks beyond it rather than writing past the LDS allocation
-  const int nb_all = (len_all + bs - 1) / bs, nb = min(nb_all, A8_MAXBT), len = min(len_all, nb * bs);
+  const int b0 = k0 / bs, nb_all = k1 > k0 ? (k1 - 1) / bs - b0 + 1 : 0, nb = min(nb_all, A8_MAXBT);
+  const int len = min(k1, (b0 + nb) * bs);
   if (nb_all > A8_MAXBT && tid == 0) __hip_atomic_store((int*)P.sync + 66, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  for (int i = tid; i < nb; i += GEMV_NT) sbt[i] = P.block_table[(long long)seq * P.max_blocks + i];
+  for (int i = tid; i < nb; i += GEMV_NT) sbt[i] = P.block_table[(long long)seq * P.max_blocks + b0 + i];
   float q[G][DPL];
 #pragma unroll
-  for (int gg = 0; gg < G; ++gg)
+  for (int gg = 0; gg < G; ++gg) {
+    const float* qp = A.y + (g * G + gg) * D + li * DPL;
+    if constexpr (SAME) {
 #pragma unroll
-    for (int jj = 0; jj < DPL; ++jj) q[gg][jj] = ld_wt(A.y + (g * G + gg) * D + li * DPL + jj) * P.scale;
+      for (int jj = 0; jj < DPL; ++jj) q[gg][jj] = ld_wt(qp + jj) * P.scale;
+    } else {
+      const f32x4 a = *(const f32x4*)qp, b = *(const f32x4*)(qp + 4);
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        q[gg][jj] = a[jj] * P.scale;
+        q[gg][4 + jj] = b[jj] * P.scale;
+      }
+    }
+  }
   float m[G], l[G], acc[G][DPL];
 #pragma unroll
   for (int gg = 0; gg < G; ++gg) {
@@ -112,8 +123,8 @@ __device__ void attn_group(const Attn8Params& P, int g, char* smem) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int t = min(t0 + u * NG + grp, len - 1);
-      const long long base = (((long long)sbt[t / bs] * Hkv + g) * bs + (t % bs)) * Dc + li * DPL;
-      const bool fresh = t == len - 1;  // the key this launch wrote
+      const long long base = (((long long)sbt[t / bs - b0] * Hkv + g) * bs + (t % bs)) * Dc + li * DPL;
+      const bool fresh = SAME && t == len_all - 1;  // the key this launch wrote
       st.k[u] = kv_load(kc + base, fresh);
       st.v[u] = kv_load(vc + base, fresh);
     }
@@ -156,20 +167,22 @@ __device__ void attn_group(const Attn8Params& P, int g, char* smem) {
       m[gg] = mn;
     }
   };
-  Step S0, S1;
-  int t0 = 0;
-  issue(t0, S0);
-  while (true) {
-    if (t0 + STEP < len) issue(t0 + STEP, S1);
-    consume(t0, S0);
-    t0 += STEP;
-    if (t0 >= len) break;
-    if (t0 + STEP < len) issue(t0 + STEP, S0);
-    consume(t0, S1);
-    t0 += STEP;
-    if (t0 >= len) break;
+  if (len > k0) {
+    Step S0, S1;
+    int t0 = k0;
+    issue(t0, S0);
+    while (true) {
+      if (t0 + STEP < len) issue(t0 + STEP, S1);
+      consume(t0, S0);
+      t0 += STEP;
+      if (t0 >= len) break;
+      if (t0 + STEP < len) issue(t0 + STEP, S0);
+      consume(t0, S1);
+      t0 += STEP;
+      if (t0 >= len) break;
+    }
   }
-  // the 4 key groups of a wave, then the 4 waves (LDS)
+  // the 4 key groups of a wave, then (attn_merge4) the 4 waves through LDS
 #pragma unroll
   for (int sh = 16; sh <= 32; sh <<= 1) {
 #pragma unroll
@@ -196,26 +209,47 @@ __device__ void attn_group(const Attn8Params& P, int g, char* smem) {
     }
   }
   __syncthreads();
-  for (int i = tid; i < G * D; i += GEMV_NT) {
-    const int gg = i / D, d = i % D;
-    float M = -INFINITY;
+}
+
+// output i = gg * D + d of the block: the 4 waves' partials folded -> (M, L, unnormalised A)
+template <int G>
+__device__ __forceinline__ void attn_merge4(const float* sm, int i, float& M, float& L, float& Av) {
+  constexpr int D = A8_D;
+  const int gg = i / D, d = i % D;
+  M = -INFINITY;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) M = fmaxf(M, sm[(w * G + gg) * (D + 2) + D]);
-    float L = 0.f, Av = 0.f;
-    if (M != -INFINITY) {
+  for (int w = 0; w < 4; ++w) M = fmaxf(M, sm[(w * G + gg) * (D + 2) + D]);
+  L = 0.f;
+  Av = 0.f;
+  if (M != -INFINITY) {
 #pragma unroll
-      for (int w = 0; w < 4; ++w) {
-        const float c = __expf(sm[(w * G + gg) * (D + 2) + D] - M);
-        L += sm[(w * G + gg) * (D + 2) + D + 1] * c;
-        Av += sm[(w * G + gg) * (D + 2) + d] * c;
-      }
+    for (int w = 0; w < 4; ++w) {
+      const float c = __expf(sm[(w * G + gg) * (D + 2) + D] - M);
+      L += sm[(w * G + gg) * (D + 2) + D + 1] * c;
+      Av += sm[(w * G + gg) * (D + 2) + d] * c;
     }
+  }
+}
+
+// G query heads of KV group g over ALL keys [0, len) (q / k / v written by this launch); merged output
+// quantised into the O projection's image (write-through: later blocks of the launch read it)
+template <int G>
+__device__ void attn_group(const Attn8Params& P, int g, char* smem) {
+  constexpr int D = A8_D;
+  float* sm = (float*)smem;          // [4][G][D + 2]
+  float* ob = sm + 4 * G * (D + 2);  // [G][D]
+  int* sbt = (int*)(ob + G * D);     // [A8_MAXBT]
+  attn_core<G, true>(P, g, 0, P.q_len[0], sm, sbt);
+  for (int i = threadIdx.x; i < G * D; i += GEMV_NT) {
+    float M, L, Av;
+    attn_merge4<G>(sm, i, M, L, Av);
     ob[i] = L > 0.f ? Av / L : 0.f;
   }
   __syncthreads();
   // the G heads' 16-dim groups -> the O projection's image (write-through: phase B of other blocks)
   const int g0 = g * G * D / 16;
-  if (tid < G * D / 16) emit_group<true>(const_cast<void*>(P.O.x8), P.O.w.K, g0 + tid, ob + 16 * tid, nullptr, nullptr);
+  if (threadIdx.x < G * D / 16)
+    emit_group<true>(const_cast<void*>(P.O.x8), P.O.w.K, g0 + threadIdx.x, ob + 16 * threadIdx.x, nullptr, nullptr);
 }
 
 }  // namespace omx

@@ -312,7 +312,18 @@ __device__ __forceinline__ void gemv8_body(const GemvParams& P, const int bx) {
     float acc[1][BT];
 #pragma unroll
     for (int b = 0; b < BT; ++b) acc[0][b] = 0.f;
-    compute_wtile<QT, NSB, 1, BT, (BT == 1 || KS <= 2)>(T[j], SB, sb0, s, lq, lf, XSP, acc, se);
+    // memory path only (batch-1 microbenchmark): fold the tile's registers (the loads stay live), no dots;
+    // compiled for BT == 1 alone (the branch costs the batched instantiations registers)
+    if (BT == 1 && P.dbg8 == 1) {
+      unsigned f = 0;
+#pragma unroll
+      for (int i = 0; i < NSB; ++i)
+#pragma unroll
+        for (int t = 0; t < 8; ++t) f ^= T[j].a[0][i][t].x ^ T[j].a[0][i][t].w ^ T[j].m[0][i].y;
+      acc[0][0] += (float)(f & 1);
+    } else {
+      compute_wtile<QT, NSB, 1, BT, (BT == 1 || KS <= 2)>(T[j], SB, sb0, s, lq, lf, XSP, acc, se);
+    }
     if constexpr (KS > 1) {  // partial sums of groups 1.. meet group 0's in LDS
       if (kg > 0) {
 #pragma unroll

@@ -95,6 +95,8 @@ struct GemvParams {
   void* emit8;                 // producer: image of this GEMV's output (EPI_ADD: new residual * emit8_nw;
   const float* emit8_nw;       //   EPI_GLU / EPI_GEGLU: the GLU output)
   float* emit8_stat;           //   EPI_ADD: per-16-row sum-of-squares partials of the new residual
+  int dbg8;                    // microbenchmarks only (scripts/bench_gemv8.py): 1 = gemv8 memory path alone
+                               // (weights loaded and folded, no dot products); 0 in production
 };
 // int8 activation image of a K-wide row (gemv8.hip): [slots] i32x4 codes + [slots] {scale, scale * sum}
 // with one pad slot per 256-element super-block and a trailing dummy slot (the GEMV's LDS layout)
@@ -113,6 +115,11 @@ struct AttnParams;
 // one launch (qkv_attn.hip); the attention output lands as the O projection's int8 image `img`
 // (x8_bytes(H * D), pad slots zero); sync: the x8sync words. false = not covered
 bool qkv_attn(const GemvParams& A, const GemvParams& B, const AttnParams& At, void* img, void* sync, hipStream_t s);
+// paged attention (At: NQ == 1, n_splits = split slots per KV group, kps = keys per split, ws / counters
+// the split workspace and tickets) + O projection (O: EPI_ADD with int8 emission) in one launch
+// (attn_o.hip); the attention lands in O's int8 image `img` (x8_bytes(H * D), pad slots zero) inside
+// the launch. false = not covered (shape, or the grid would not be co-resident)
+bool attn_o(const GemvParams& O, const AttnParams& At, void* img, void* sync, hipStream_t s);
 // QKV (A: q,k rows or all rows; B: v rows or B.w.s0 null) + paged attention + O projection (O.x8 = the
 // attention image, EPI_ADD + emission) in one launch (attn8.hip); false = not covered
 bool attn8(const GemvParams& A, const GemvParams& B, const GemvParams& O, const AttnParams& At, void* sync,
@@ -285,6 +292,7 @@ enum {
   LC_ATTN_DECODE,    // attention.hip split flash-decode kernel
   LC_ATTN_PREFILL,   // attention.hip MFMA flash prefill
   LC_QKV_ATTN,       // qkv_attn.hip fused QKV + attention (batch-1 decode, short context)
+  LC_ATTN_O,         // attn_o.hip fused attention + O projection (batch-1 decode)
   LC_N
 };
 void count_launch(int which);

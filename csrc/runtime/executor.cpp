@@ -290,6 +290,22 @@ void Executor::attn_block(int i, const StepInputs& in, hipStream_t s) {
     throw std::runtime_error("deferred attention merge: unsupported (K, D, splits)");
   A.defer = defer;
   if (ch) A.out16 = ws.a16;
+  if (q8 && B == 1 && ws.attn_o && !phi && cfg.tp == 1 && ws.x8q && !in.prefill && ws.attn_ws && ws.attn_cnt) {
+    // attention + O projection in one launch (attn_o.hip): O's weights stream while the attention
+    // runs; the split merge happens inside the attention blocks, O reads a ready int8 image
+    AttnParams Ao = A;
+    Ao.kps = ws.attn_o_kps > 0 ? ws.attn_o_kps : 128;
+    GemvParams O = base_params(L.wo, B, ws.abuf, Eq, ws);
+    O.bias = L.bo;
+    O.epi = EPI_ADD;
+    O.y = ws.resid;
+    O.ldy = E;
+    x8_emit(O, ws.x8e, L.ffn_norm, ws.x8st);  // gate_up's RMSNorm input, int8
+    if (attn_o(O, Ao, ws.x8q, ws.x8sync, s)) {
+      ++n_attn_o;
+      return;
+    }
+  }
   if (in.prefill && !segments.empty()) {  // several sequences' prompts: flash attention per segment
     for (const auto& sg : segments) {
       AttnParams As = A;

@@ -14,3 +14,5 @@ OMX_BENCH_HOT=1 timeout -k 10 200 python -u scripts/bench_gemv8.py > $O/gemv8_ho
 cat $O/gemv8_hot.log | grep -v amdgpu.ids
 timeout -k 10 400 python -u bench.py --steps 20 --warmup 5 > $O/bench20.log 2>&1 || { tail -20 $O/bench20.log; exit 1; }
 tail -1 $O/bench20.log | cut -c1-1600
+OMX_BENCH_DBG8=1 timeout -k 10 200 python -u scripts/bench_gemv8.py > $O/gemv8_cold_memonly.log 2>&1 || { tail -20 $O/gemv8_cold_memonly.log; exit 1; }
+cat $O/gemv8_cold_memonly.log | grep -v amdgpu.ids

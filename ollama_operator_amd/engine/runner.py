@@ -100,6 +100,9 @@ class NativeExec:
             return {}
         return dict(x8e=b["x8e"].data_ptr(), x8f=b["x8f"].data_ptr(), x8st=b["x8st"].data_ptr(), x8q=b["x8q"].data_ptr(),
                     x8sync=b["x8sync"].data_ptr(), x8_ok=1, x8_fuse=int(os.environ.get("OMX_X8_FUSE", "0") != "0"),
+                    # batch-1 decode: attention + O projection in one launch (attn_o.hip)
+                    attn_o=int(os.environ.get("OMX_ATTN_O", "0") != "0"),  # opt-in: slower, profiles/r5_decode
+                    attn_o_kps=int(os.environ.get("OMX_ATTN_O_KPS", "128")),
                     # batch rows on the chain: B = 2 measured 1.73 vs 2.08 ms per step on the int8 rows, B = 3
                     # 2.15 vs 2.19 ms; at 4 rows layout M's MFMA GEMVs win (profiles/r4_batch), so 3 by default
                     x8_bmax=int(os.environ.get("OMX_X8_BATCH", "3")))
@@ -691,11 +694,23 @@ class Runner:
         finally:
             self._decode_S = 0
 
+    def _check_handoffs(self) -> None:
+        """Once per generation (one small read): an in-launch hand-off of the decode graph (attn_o.hip
+        and the opt-in fused paths) that timed out leaves its error word set -- those steps' tokens are
+        invalid, so fail loudly (the server turns it into an error response; the pod restarts)."""
+        if self.x8_bufs is None or self._closed:
+            return
+        err = self.x8_error()
+        if err:
+            self.x8_bufs["x8sync"].zero_()
+            raise RuntimeError("decode step: an in-launch hand-off (attention + O / fused layer halves) timed out; "
+                               "the generated tokens are invalid")
+
     def x8_error(self) -> int:
         """Nonzero when an in-launch hand-off of the int8 chain timed out (gemv8.hip ffn8_kernel): the
         step's results are invalid. Reads device memory (a sync)."""
         b = self.x8_bufs
-        return int(b["x8sync"][2].item() or b["x8sync"][16 + 66].item()) if b else 0
+        return int(b["x8sync"][2].item() or b["x8sync"][16 + 66].item() or b["x8sync"][98].item()) if b else 0
 
     def set_tokens(self, tokens: list[int]) -> None:
         """Host -> d_tokens[:len(tokens)] (batch recomposition: rows' next inputs)."""
@@ -866,6 +881,7 @@ class Runner:
                 ctrl.signal(False)  # generation over (also when the consumer closed us early)
             if ctrl is not None and self.ar is not None:
                 self.ar.check()  # a peer that missed a barrier timed the step out: fail loudly
+            self._check_handoffs()
             if times is not None:
                 times.gen_tokens = n
                 times.gen_s = time.perf_counter() - t1

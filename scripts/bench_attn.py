@@ -77,6 +77,46 @@ def attn_kps_sweep(C):
     C.set_attn_tuning(256)
 
 
+def attn_cold_sweep(C):
+    """Graph-timed decode attention with the KV cache rotated over enough copies to miss the 256 MiB
+    Infinity Cache (a decode step streams every layer's cache once): keys-per-split x split cap, with the
+    in-launch merge (the on-device split rule the runner uses past 1024 keys)."""
+    bs = 16
+    for H, Hkv, D in ((32, 32, 128), (32, 8, 128)):
+        for L in (512, 1024, 2048, 4096, 8192):
+            nblk = (L + bs - 1) // bs
+            per = nblk * Hkv * bs * D * 2 * 2  # K + V bytes
+            copies = max(2, (640 << 20) // per + 1)
+            kcs = [torch.randn(nblk, Hkv, bs, D, device="cuda").half() for _ in range(copies)]
+            vcs = [torch.randn(nblk, Hkv, bs, D, device="cuda").half() for _ in range(copies)]
+            bt = torch.arange(nblk, device="cuda", dtype=torch.int32)
+            qlen = torch.tensor([L], device="cuda", dtype=torch.int32)
+            q = torch.randn(1, H * D, device="cuda")
+            out = torch.empty(1, H * D, device="cuda")
+            row = []
+            for smax in (16, 32):
+                S = max(1, min(smax, 512 // Hkv if smax == 16 else 1024 // Hkv))
+                ws = torch.empty(max(1, C.attention_ws_floats(1, H, D, S)), device="cuda")
+                cnt = torch.zeros(H, device="cuda", dtype=torch.int32)
+                for kps in (64, 128, 256, 512):
+                    C.set_attn_tuning(kps)
+                    it = [0]
+
+                    def fn(st):
+                        i = it[0] % copies
+                        it[0] += 1
+                        C.attention(q.data_ptr(), H * D, kcs[i].data_ptr(), vcs[i].data_ptr(), bt.data_ptr(), nblk, 0,
+                                    qlen.data_ptr(), 1, H, Hkv, D, bs, D ** -0.5, 0, out.data_ptr(), H * D,
+                                    ws.data_ptr(), S, cnt.data_ptr(), st)
+                    t = timeit_graph(fn, n=2 * copies, reps=10)
+                    row.append(f"S<={S},kps={kps}:{t:6.2f}")
+            gbs = per / 1e3
+            print(f"attn(cold) H={H} Hkv={Hkv} L={L:5d} ({per / 1e6:.1f} MB/layer)  " + "  ".join(row) + "  (us)",
+                  flush=True)
+            del kcs, vcs
+    C.set_attn_tuning(256)
+
+
 def attn_hpb_sweep(C):
     """Graph-timed decode attention vs query heads per block (GQA group split) and keys per split."""
     bs = 16
@@ -161,6 +201,9 @@ def main():
         return
     if os.environ.get("OMX_BENCH_KPS"):
         attn_kps_sweep(C)
+        return
+    if os.environ.get("OMX_BENCH_COLD"):
+        attn_cold_sweep(C)
         return
     gemv_fixed(C, s)
     attn_sweep(C, s)

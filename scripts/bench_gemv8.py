@@ -2,7 +2,8 @@
 production input (int8 image + RMS partials, or the plain image) and emission: time per launch inside a
 replayed hipGraph of back-to-back launches, weights rotated over enough copies to miss the 256 MiB
 Infinity Cache (decode streams 4 GB of distinct weights per token). OMX_BENCH_HOT=1: one copy re-read
-(MALL-served: what a perfect weight prefetch would give).
+(MALL-served: what a perfect weight prefetch would give). OMX_BENCH_DBG8=1: the memory path alone (no
+dot products: what the launch + weight stream cost without the compute).
 Run on the GPU box:  python scripts/bench_gemv8.py"""
 import os
 import sys
@@ -27,6 +28,12 @@ SHAPES = [
     ("down_q4k", GGMLType.Q4_K, 4096, 11008, EPI_ADD, False, True),
     ("down_q6k", GGMLType.Q6_K, 4096, 11008, EPI_ADD, False, True),
     ("lm_head", GGMLType.Q6_K, 32000, 4096, EPI_STORE, True, False),
+]
+# OMX_BENCH_ALIGN=1: down-shaped probes at K = 12288 (48 super-blocks: each K group of the 3-way split
+# gets exactly 16, piece segments 128-B aligned) vs the real K = 11008 (43: 15 + 15 + 13, 688-B strides)
+ALIGN = [
+    ("down_q4k_k12288", GGMLType.Q4_K, 4096, 12288, EPI_ADD, False, True),
+    ("down_q6k_k12288", GGMLType.Q6_K, 4096, 12288, EPI_ADD, False, True),
 ]
 
 
@@ -54,7 +61,7 @@ def main():
         big.add_(1)
     torch.cuda.synchronize()
     del big
-    for name, qt, N, K, epi, rms, emits in SHAPES:
+    for name, qt, N, K, epi, rms, emits in SHAPES + (ALIGN if os.environ.get("OMX_BENCH_ALIGN") else []):
         if only and name not in only:
             continue
         tups, keep, nbytes = make(qt, N, K, hot)
@@ -70,7 +77,7 @@ def main():
         nw = torch.rand(max(N, K), device="cuda") + 0.5
         out = torch.zeros(C.x8_bytes(Ny), dtype=torch.uint8, device="cuda")
         ost = torch.zeros(Ny // 16 + 4, device="cuda")
-        ops = {"x8": img.data_ptr()}
+        ops = {"x8": img.data_ptr(), "dbg8": int(os.environ.get("OMX_BENCH_DBG8", "0"))}
         if rms:
             ops["x8_stat"] = st.data_ptr()
         if emits:
@@ -79,6 +86,45 @@ def main():
                 ops["emit8_stat"] = ost.data_ptr()
         s = torch.cuda.Stream()
         n_launch = 64
+        if os.environ.get("OMX_BENCH_PF") and not hot:
+            # MALL prefetch probe: while launch i runs on the main stream, a side stream reads copy i + 1
+            # (torch.sum over its planes = a streaming read that allocates the lines in the Infinity
+            # Cache), so launch i + 1 finds its weights on-die. Eager launches, events order the streams.
+            side = torch.cuda.Stream()
+            planes = [[t.view(torch.int32) for t in kp] for kp in keep]
+            sink = torch.zeros(len(planes[0]) + 1, dtype=torch.int64, device="cuda")
+
+            def run(n, pf):
+                evs = []
+                with torch.cuda.stream(s):
+                    sh = s.cuda_stream
+                    for i in range(n):
+                        C.gemv(tups[i % len(tups)], 1, 0, K, 0, 0, 0, 1e-5, epi, y.data_ptr(), Ny, 0, 0, ops, sh)
+                        e = torch.cuda.Event()
+                        e.record(s)
+                        evs.append(e)
+                        if pf:
+                            with torch.cuda.stream(side):
+                                if i >= 1:
+                                    side.wait_event(evs[i - 1])  # starts as launch i starts
+                                for j, t in enumerate(planes[(i + 1) % len(planes)]):
+                                    sink[j] += t.sum()
+            for pf in (0, 1):
+                run(8, pf)
+                torch.cuda.synchronize()
+                ts = []
+                for _ in range(5):
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record(s)
+                    run(n_launch, pf)
+                    e1.record(s)
+                    torch.cuda.synchronize()
+                    ts.append(e0.elapsed_time(e1) * 1e3 / n_launch)
+                t = float(np.median(ts))
+                print(f"{name:9s} cold eager {'+ side-stream MALL prefetch' if pf else '(no prefetch)'} {t:7.2f} us/launch",
+                      flush=True)
+            del tups, keep
+            continue
         with torch.cuda.stream(s):
             sh = s.cuda_stream
             for i in range(3):  # warm (instantiation, lds attributes)
@@ -100,7 +146,8 @@ def main():
             torch.cuda.synchronize()
             ts.append(e0.elapsed_time(e1) * 1e3 / n_launch)
         t = float(np.median(ts))
-        print(f"{name:9s} {'hot ' if hot else 'cold'} {t:7.2f} us/launch  {nbytes / t / 1e3:7.1f} GB/s  "
+        tag = ("hot " if hot else "cold") + (" mem-only" if ops["dbg8"] else "")
+        print(f"{name:9s} {tag} {t:7.2f} us/launch  {nbytes / t / 1e3:7.1f} GB/s  "
               f"({len(tups)} copies, {nbytes / 1e6:.1f} MB)", flush=True)
         del g, tups, keep
 
