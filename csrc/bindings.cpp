@@ -304,7 +304,7 @@ PYBIND11_MODULE(_C, m) {
   // launch counters (ops.h LC_*): tests assert which kernel family a call enqueued
   m.def("launch_counts", []() {
     static const char* names[LC_N] = {"dq_gemm", "gemm_tile", "gemm_lib", "gemv8_row1", "gemv8_rows", "gemv8_dual",
-                                      "gemv_mb", "gemv_flight", "attn_decode", "attn_prefill", "qkv_attn", "attn_o"};
+                                      "gemv_mb", "gemv_flight", "attn_decode", "attn_prefill", "qkv_attn", "attn_o", "mall_prefetch"};
     py::dict d;
     for (int i = 0; i < LC_N; ++i) d[names[i]] = launch_count(i);
     return d;
@@ -647,6 +647,9 @@ PYBIND11_MODULE(_C, m) {
     ARParams P = ar_params(d);
     if (slab < 0 || slab >= AR_SLABS || n % 4 || n > P.slab_floats) throw std::runtime_error("ar_allreduce_add: bad slab / n");
     ar_allreduce_add(P, slab, Pp<float>(y), n, S(stream));
+  });
+  m.def("mall_prefetch", [](uintptr_t p, size_t bytes, int blocks, uintptr_t sink, uintptr_t stream) {
+    mall_prefetch(Pp<const void>(p), bytes, blocks, Pp<unsigned>(sink), S(stream));
   });
   m.def("ar_allreduce_add_emit", [](py::dict d, int slab, uintptr_t y, int E, int B, uintptr_t img, uintptr_t nw,
                                      uintptr_t stat, uintptr_t stream) {

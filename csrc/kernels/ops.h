@@ -120,6 +120,9 @@ bool qkv_attn(const GemvParams& A, const GemvParams& B, const AttnParams& At, vo
 // (attn_o.hip); the attention lands in O's int8 image `img` (x8_bytes(H * D), pad slots zero) inside
 // the launch. false = not covered (shape, or the grid would not be co-resident)
 bool attn_o(const GemvParams& O, const AttnParams& At, void* img, void* sync, hipStream_t s);
+// reads [p, p + bytes) on `blocks` workgroups so the lines land in the MALL (prefetch.hip); sink: >= 256
+// words, written only on a practically impossible fold value
+void mall_prefetch(const void* p, size_t bytes, int blocks, unsigned* sink, hipStream_t s);
 // QKV (A: q,k rows or all rows; B: v rows or B.w.s0 null) + paged attention + O projection (O.x8 = the
 // attention image, EPI_ADD + emission) in one launch (attn8.hip); false = not covered
 bool attn8(const GemvParams& A, const GemvParams& B, const GemvParams& O, const AttnParams& At, void* sync,
@@ -293,6 +296,7 @@ enum {
   LC_ATTN_PREFILL,   // attention.hip MFMA flash prefill
   LC_QKV_ATTN,       // qkv_attn.hip fused QKV + attention (batch-1 decode, short context)
   LC_ATTN_O,         // attn_o.hip fused attention + O projection (batch-1 decode)
+  LC_MALL_PREFETCH,  // prefetch.hip side-stream weight reader
   LC_N
 };
 void count_launch(int which);

@@ -34,6 +34,11 @@ SHAPES = [
 ALIGN = [
     ("down_q4k_k12288", GGMLType.Q4_K, 4096, 12288, EPI_ADD, False, True),
     ("down_q6k_k12288", GGMLType.Q6_K, 4096, 12288, EPI_ADD, False, True),
+    # K = 10240: 40 super-blocks (piece runs 128-B aligned, the last K group 8 of 16 lanes): alignment
+    # alone; K = 11264: 44 (64-B aligned runs)
+    ("down_q4k_k10240", GGMLType.Q4_K, 4096, 10240, EPI_ADD, False, True),
+    ("down_q6k_k10240", GGMLType.Q6_K, 4096, 10240, EPI_ADD, False, True),
+    ("down_q6k_k11264", GGMLType.Q6_K, 4096, 11264, EPI_ADD, False, True),
 ]
 
 
@@ -43,11 +48,19 @@ def make(qt, N, K, hot):
     st = repack(raw, qt, N, K)
     copies = 1 if hot else max(2, (768 << 20) // raw.nbytes)
     tups, keep = [], []
+    planes = [np.ascontiguousarray(st[n]).view(np.uint8).reshape(-1) for n in STREAMS[qt]]
+    offs, tot = [], 0
+    for a in planes:
+        offs.append(tot)
+        tot += (a.size + 255) // 256 * 256
     for _ in range(copies):
-        ts = [torch.from_numpy(np.ascontiguousarray(st[n])).cuda() for n in STREAMS[qt]]
-        p = [t.data_ptr() for t in ts] + [0] * (4 - len(ts))
+        # one buffer per copy, planes at 256-B aligned offsets (the prefetch probe streams the whole copy)
+        flat = torch.zeros(tot, dtype=torch.uint8, device="cuda")
+        for a, o in zip(planes, offs):
+            flat[o: o + a.size].copy_(torch.from_numpy(a))
+        p = [flat.data_ptr() + o for o in offs] + [0] * (4 - len(offs))
         tups.append((p[0], p[1], p[2], p[3], N, K, int(qt)))
-        keep.append(ts)
+        keep.append(flat)
     return tups, keep, raw.nbytes
 
 
@@ -87,42 +100,61 @@ def main():
         s = torch.cuda.Stream()
         n_launch = 64
         if os.environ.get("OMX_BENCH_PF") and not hot:
-            # MALL prefetch probe: while launch i runs on the main stream, a side stream reads copy i + 1
-            # (torch.sum over its planes = a streaming read that allocates the lines in the Infinity
-            # Cache), so launch i + 1 finds its weights on-die. Eager launches, events order the streams.
+            # MALL prefetch probe (prefetch.hip): while launch i runs on the main stream, a side stream reads
+            # copy i + 1 (its lines land in the 256 MiB Infinity Cache), so launch i + 1 finds its weights
+            # on-die. Both streams captured into ONE graph (fork / join by events: the prefetch of copy
+            # i + 1 depends on launch i - 1 only, so it can run beside launch i).
             side = torch.cuda.Stream()
-            planes = [[t.view(torch.int32) for t in kp] for kp in keep]
-            sink = torch.zeros(len(planes[0]) + 1, dtype=torch.int64, device="cuda")
+            sink = torch.zeros(256, dtype=torch.int32, device="cuda")
+            tot = keep[0].numel()
 
-            def run(n, pf):
-                evs = []
-                with torch.cuda.stream(s):
-                    sh = s.cuda_stream
-                    for i in range(n):
-                        C.gemv(tups[i % len(tups)], 1, 0, K, 0, 0, 0, 1e-5, epi, y.data_ptr(), Ny, 0, 0, ops, sh)
-                        e = torch.cuda.Event()
-                        e.record(s)
-                        evs.append(e)
-                        if pf:
-                            with torch.cuda.stream(side):
-                                if i >= 1:
-                                    side.wait_event(evs[i - 1])  # starts as launch i starts
-                                for j, t in enumerate(planes[(i + 1) % len(planes)]):
-                                    sink[j] += t.sum()
-            for pf in (0, 1):
-                run(8, pf)
+            def timed(g):
+                for _ in range(3):
+                    g.replay()
                 torch.cuda.synchronize()
                 ts = []
-                for _ in range(5):
+                for _ in range(10):
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                    e0.record(s)
-                    run(n_launch, pf)
-                    e1.record(s)
+                    e0.record()
+                    g.replay()
+                    e1.record()
                     torch.cuda.synchronize()
                     ts.append(e0.elapsed_time(e1) * 1e3 / n_launch)
-                t = float(np.median(ts))
-                print(f"{name:9s} cold eager {'+ side-stream MALL prefetch' if pf else '(no prefetch)'} {t:7.2f} us/launch",
-                      flush=True)
+                return float(np.median(ts))
+            for pf in [0] + [int(x) for x in os.environ.get("OMX_BENCH_PF_BLOCKS", "32,64,128,256").split(",")]:
+                with torch.cuda.stream(s):
+                    sh, sd = s.cuda_stream, side.cuda_stream
+                    for i in range(3):
+                        C.gemv(tups[i % len(tups)], 1, 0, K, 0, 0, 0, 1e-5, epi, y.data_ptr(), Ny, 0, 0, ops, sh)
+                        C.mall_prefetch(keep[i].data_ptr(), tot, 64, sink.data_ptr(), sh)
+                    torch.cuda.synchronize()
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g, stream=s):
+                        prev = torch.cuda.Event()
+                        prev.record(s)
+                        for i in range(n_launch):
+                            if pf:
+                                side.wait_event(prev)
+                                C.mall_prefetch(keep[(i + 1) % len(keep)].data_ptr(), tot, pf, sink.data_ptr(), sd)
+                            C.gemv(tups[i % len(tups)], 1, 0, K, 0, 0, 0, 1e-5, epi, y.data_ptr(), Ny, 0, 0, ops, sh)
+                            prev = torch.cuda.Event()
+                            prev.record(s)
+                        if pf:
+                            s.wait_stream(side)
+                t = timed(g)
+                del g
+                tag = f"+ MALL prefetch on {pf:3d} blocks" if pf else "(no prefetch)              "
+                line = f"{name:9s} cold graph {tag} {t:7.2f} us/launch  {nbytes / t / 1e3:7.1f} GB/s"
+                if pf:  # the prefetch reader alone over the rotated copies
+                    with torch.cuda.stream(s):
+                        g = torch.cuda.CUDAGraph()
+                        with torch.cuda.graph(g, stream=s):
+                            for i in range(n_launch):
+                                C.mall_prefetch(keep[i % len(keep)].data_ptr(), tot, pf, sink.data_ptr(), s.cuda_stream)
+                    ta = timed(g)
+                    del g
+                    line += f"   | reader alone {ta:7.2f} us/copy {nbytes / ta / 1e3:7.1f} GB/s"
+                print(line, flush=True)
             del tups, keep
             continue
         with torch.cuda.stream(s):
