@@ -288,6 +288,11 @@ class Runner:
         # deferred flash-decode merge (B == 1): attention leaves S <= 8 partial slabs, the O GEMV
         # merges them in its activation prologue (no in-launch ticket + re-read)
         self.defer_kps = int(os.environ.get("OMX_DEFER_KPS", "128"))
+        # past 8 x defer_kps keys, up to 8 x 512: 8 deferred splits of ceil(len / 8) keys (OMX_DEFER_LONG=1,
+        # default: attention 14.4 -> 11.6 us at 2k keys, the O prologue's 8-slab merge 4.9 -> 7.1 us, net
+        # decode_ctx2048 593 -> 602 tok/s, profiles/r5_decode) or the on-device split rule with the
+        # in-launch ticket merge (0; always past 4096 keys)
+        self.defer_long = os.environ.get("OMX_DEFER_LONG", "1") != "0"
         self._defer_ok = (self.is_gpu and os.environ.get("OMX_DEFER_MERGE", "1") != "0" and
                           native().gemv_merge_supported(1, Eq, loc["D"], 8) and self.n_splits(1) >= 8)
         self._decode_S = 0
@@ -366,7 +371,7 @@ class Runner:
         S = 1
         while S < 8 and length > S * self.defer_kps:
             S *= 2
-        return S if length <= S * self.defer_kps else 0
+        return S if length <= S * self.defer_kps or (self.defer_long and length <= 8 * 512) else 0
 
     def _ws_floats(self, B: int) -> int:
         loc = self.w.local

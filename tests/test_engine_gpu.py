@@ -168,7 +168,7 @@ def test_deferred_split_merge_decode(tmp_path, monkeypatch, name):
             r.free_sequence(sid)
         assert rel(outs[0], outs[1]) < 2e-3, L
         assert rel(outs[0], outs[2]) < 3e-2, L
-    assert seen == {1, 2, 4, 8, 0}
+    assert seen == {1, 2, 4, 8}  # 1050 keys: 8 deferred splits of 132 (OMX_DEFER_LONG, default on)
 
 
 @pytest.mark.parametrize("name", ["tiny-llama", "tiny-mixtral", "tiny-phi2", "tiny-gemma"])
