@@ -740,12 +740,12 @@ class Runner:
         self.kv.truncate(sid, keep)
 
     def admit(self, sid: int, keep: int, tokens: list[int], opts: SamplingOptions, history: list[int],
-              seed: int) -> None:
+              seed: int, n_sampled: int = 0) -> None:
         """Start row 0 of a new request: keep `keep` cached tokens of `sid`, prefill `tokens`, seed the
-        sampler and sample the first token into s_out[0]."""
+        sampler (n_sampled draws already made) and sample the first token into s_out[0]."""
         self._keep_prefix(sid, keep, history)
         self.prefill(sid, tokens)
-        self._set_sampler(0, opts, history, seed, 0)
+        self._set_sampler(0, opts, history, seed, n_sampled)
         self._sample(1)
 
     def check_admit(self, sid: int, keep: int, tokens: list[int]) -> None:
@@ -759,20 +759,24 @@ class Runner:
         self._device_tokens(tokens)
 
     def admit_many(self, items: list[tuple]) -> list[int]:
-        """Start several requests with ONE forward: items[i] = (sid, keep, tokens, opts, history, seed).
-        Their prompt rows go through the step as independent rows (own position / KV slot / block-table
-        row; the multi-sequence paged attention, as a batched decode step), so queued requests prefill
-        together instead of stalling the running batch once each. Returns the first sampled tokens
-        (row i = items[i]). Falls back to one `admit` per item when the rows exceed max_batch."""
+        """Start several requests with ONE forward: items[i] = (sid, keep, tokens, opts, history, seed
+        [, n_sampled]). Their prompt rows go through the step as independent rows (own position / KV
+        slot / block-table row; the multi-sequence paged attention, as a batched decode step), so queued
+        requests prefill together instead of stalling the running batch once each. Returns the sampled
+        tokens (row i = items[i]). An item may also be a running request's decode row (tokens = its next
+        input, keep = its length, n_sampled = its sampler's draws so far) or one chunk of a prompt (its
+        sample is the caller's to ignore): the scheduler's interleaved admission mixes both into one
+        forward. Falls back to one `admit` per item when the rows exceed max_batch."""
+        items = [tuple(it) + (0,) * (7 - len(it)) for it in items]
         total = sum(len(it[2]) for it in items)
         if len(items) == 1 or total > self.max_batch or len(items) > self.max_batch:
             out = []
-            for sid, keep, tokens, opts, history, seed in items:
-                self.admit(sid, keep, tokens, opts, history, seed)
+            for sid, keep, tokens, opts, history, seed, n_s in items:
+                self.admit(sid, keep, tokens, opts, history, seed, n_s)
                 out.append(int(self.s_out[0].item()))
             return out
         pos_l, slot_l, row_l, toks, last = [], [], [], [], []
-        for sid, keep, tokens, _o, history, _sd in items:
+        for sid, keep, tokens, _o, history, _sd, _n in items:
             self._keep_prefix(sid, keep, history)
             s = self.kv.seqs[sid]
             start = s.length
@@ -794,7 +798,7 @@ class Runner:
         self._upload(arr.astype(np.int32), self._device_tokens(toks))
         # each admitted prompt is one sequence's contiguous positions: flash (MFMA) attention per segment
         segs, at = [], 0
-        for _sid, _k, tokens, _o, _h, _sd in items:
+        for _sid, _k, tokens, _o, _h, _sd, _n in items:
             segs.append((at, len(tokens)))
             at += len(tokens)
         seg_exe = getattr(getattr(self.exe, "exe", None), "set_segments", None) if self.is_gpu else None
@@ -807,9 +811,9 @@ class Runner:
                     seg_exe([])
             else:  # torch twin / CPU backend: their attention serves any row -> sequence mapping
                 self.forward(B, n, use_idx=True, prefill=False)
-        for i, (sid, _k, tokens, opts, history, seed) in enumerate(items):
+        for i, (sid, _k, tokens, opts, history, seed, n_s) in enumerate(items):
             self.kv.seqs[sid].tokens.extend(tokens)
-            self._set_sampler(i, opts, history, seed, 0)
+            self._set_sampler(i, opts, history, seed, n_s)
         self._sample(n)
         return [int(t) for t in self.s_out[:n].tolist()]
 

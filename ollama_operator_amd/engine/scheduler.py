@@ -7,7 +7,14 @@ loaded model owns the `Runner` and
 
 * admits queued requests into free rows (up to `max_parallel`), reusing the idle sequence whose KV holds
   the longest common prefix with the new prompt (multi-turn chats skip the shared history);
-* prefills the new prompt, samples its first token with the request's own sampler state;
+* prefills the new prompt, samples its first token with the request's own sampler state; while other
+  rows are decoding, admission is INTERLEAVED: the new prompts go through in chunks of `chunk` tokens, and
+  every chunk's forward also carries each running row's next decode token (one more row of the same
+  step), so running streams keep producing a token per chunk instead of stalling for the whole burst's
+  prefill;
+* coalesces a burst: when nothing is decoding, the first arrival waits (at most `coalesce_ms`, and only
+  while requests keep arriving within `quiet_ms`) for the rest of the burst, so simultaneous clients
+  prefill in one forward and start decoding together;
 * runs batched decode steps for every active row (`Runner.decode_batch`: B rows through the batched
   GEMV + paged GQA attention + per-row on-device sampling, one hipGraph per B), keeping two steps in
   flight while the batch composition is stable -- the sampled tokens feed back on device, exactly as
@@ -24,6 +31,7 @@ The same code drives the torch twin on CPU (tests), where steps are simply synch
 from __future__ import annotations
 
 import collections
+import os
 import queue
 import threading
 import time
@@ -67,7 +75,8 @@ class _Req:
 class BatchScheduler:
     """Per-model continuous-batching loop (see module docstring)."""
 
-    def __init__(self, runner: Runner, max_parallel: int = 4, depth: int = 2):
+    def __init__(self, runner: Runner, max_parallel: int = 4, depth: int = 2, chunk: int | None = None,
+                 coalesce_ms: float | None = None, quiet_ms: float | None = None):
         # tensor parallel: `runner` is the leader's TPRunnerProxy; every runner call below is mirrored to
         # the follower ranks (parallel/tp.py), which replay the leader's decisions step for step
         self.r = runner
@@ -75,6 +84,13 @@ class BatchScheduler:
         self.max_parallel = max(1, min(max_parallel, runner.max_batch, runner.max_seqs - 1))
         self.max_idle = max(0, runner.max_seqs - self.max_parallel - 1)  # prefix cache rows
         self.depth = depth if runner.is_gpu else 1  # steps in flight
+        # interleaved admission: prompt tokens per mixed forward (0 = one forward for the whole burst)
+        env = os.environ.get
+        self.chunk = int(env("OMX_ADMIT_CHUNK", "256")) if chunk is None else chunk
+        # burst coalescing (0 = admit the first arrival at once)
+        self.coalesce_ms = float(env("OMX_ADMIT_COALESCE_MS", "10")) if coalesce_ms is None else coalesce_ms
+        self.quiet_ms = float(env("OMX_ADMIT_QUIET_MS", "3")) if quiet_ms is None else quiet_ms
+        self.interleaved_chunks = 0  # mixed forwards run (tests, /api/ps diagnostics)
         self.cv = threading.Condition()
         self.pending: collections.deque[_Req] = collections.deque()
         self.jobs: collections.deque = collections.deque()  # exclusive runner work (embeddings)
@@ -158,6 +174,7 @@ class BatchScheduler:
                         self.cv.wait()
                     if self.closed:
                         break
+                    self._coalesce()
                     jobs = list(self.jobs)
                     self.jobs.clear()
                 for fn, box in jobs:
@@ -174,6 +191,21 @@ class BatchScheduler:
             raise
         finally:
             self._shutdown(err)
+
+    def _coalesce(self) -> None:
+        """(cv held) Nothing decodes and requests are queued: give a burst's stragglers up to
+        coalesce_ms to arrive, ending early once no new request came for quiet_ms or the rows are full."""
+        if self.coalesce_ms <= 0 or self.active or not self.pending or self.jobs:
+            return
+        deadline = time.perf_counter() + self.coalesce_ms / 1e3
+        while not self.closed and len(self.pending) < self.max_parallel:
+            n = len(self.pending)
+            left = deadline - time.perf_counter()
+            if left <= 0:
+                return
+            self.cv.wait(min(left, self.quiet_ms / 1e3))
+            if len(self.pending) == n:  # quiet: the burst is over
+                return
 
     def _run_job(self, fn, box) -> None:
         kv = self.r.kv
@@ -256,6 +288,9 @@ class BatchScheduler:
                     ok.append((req, keep))
                 except ValueError as e:
                     self._fail_req(req, e)
+            if ok and self.active and self.chunk > 0:
+                self._admit_interleaved(ok, t0)
+                continue
             done, firsts = [], []
             if len(ok) <= 1 or sum(len(q.prompt) - k for q, k in ok) > r.max_batch or len(ok) > r.max_batch:
                 for req, keep in ok:  # one forward each: a failure stays with its request
@@ -273,23 +308,78 @@ class BatchScheduler:
                 except BaseException as e:  # noqa: BLE001 -- the shared forward failed: its requests fail
                     for req, _ in ok:
                         self._fail_req(req, e)
-            ready = done
             t1 = time.perf_counter()
-            for (req, keep), first in zip(ready, firsts):
-                req.n_sampled = 1
-                req.history = list(req.prompt) + [first]
-                req.pos = r.kv.seqs[req.sid].length
-                req.max_tokens = min(req.max_tokens, r.ctx - req.pos)
-                req.last_input = first
-                req.t_gen0 = t1
-                if req.times is not None:
-                    req.times.prompt_tokens = len(req.prompt) - keep
-                    req.times.prompt_s = t1 - t0
-                self._deliver(req, first)
-                if req.finished():
-                    self._retire(req)
-                else:
-                    self.active.append(req)
+            for (req, keep), first in zip(done, firsts):
+                self._started(req, keep, first, t0, t1)
+
+    def _started(self, req: _Req, keep: int, first: int, t0: float, t1: float) -> None:
+        """A request's prompt is in: record its first token and make it a decoding row."""
+        req.n_sampled = 1
+        req.history = list(req.prompt) + [first]
+        req.pos = self.r.kv.seqs[req.sid].length
+        req.max_tokens = min(req.max_tokens, self.r.ctx - req.pos)
+        req.last_input = first
+        req.t_gen0 = t1
+        if req.times is not None:
+            req.times.prompt_tokens = len(req.prompt) - keep
+            req.times.prompt_s = t1 - t0
+        self._deliver(req, first)
+        if req.finished():
+            self._retire(req)
+        else:
+            self.active.append(req)
+
+    def _admit_interleaved(self, ok: list[tuple[_Req, int]], t0: float) -> None:
+        """Admit `ok` while rows are decoding: their prompts in chunks of self.chunk tokens, each chunk
+        ONE forward (Runner.admit_many) that also carries every running row's next decode token. A
+        running row gets its token from each chunk; an admitted request joins the running rows (and the
+        next chunks) as soon as its last chunk is in."""
+        r = self.r
+        work = [[req, keep, 0] for req, keep in ok]  # request, prefix kept, prompt tokens done
+        while work:
+            rows = [q for q in self.active if not q.finished() and q.issued < q.max_tokens - 1]
+            budget = max(1, min(self.chunk, r.max_batch - len(rows)))
+            items, roles = [], []
+            for q in rows:
+                items.append((q.sid, r.kv.seqs[q.sid].length, [q.last_input], q.opts, q.history, q.seed, q.n_sampled))
+                roles.append(q)
+            for w in work:
+                if budget <= 0:
+                    break
+                req, keep, off = w
+                rest = len(req.prompt) - keep - off
+                take = min(rest, budget)
+                items.append((req.sid, keep + off, req.prompt[keep + off: keep + off + take], req.opts, req.prompt,
+                              req.seed, 0))
+                roles.append((w, take == rest))
+                w[2] += take
+                budget -= take
+            try:
+                outs = r.admit_many(items)
+            except BaseException as e:  # noqa: BLE001 -- the shared forward failed: every row in it fails
+                for w in work:
+                    self._fail_req(w[0], e)
+                self._fail_active(e)
+                return
+            self.interleaved_chunks += 1
+            t1 = time.perf_counter()
+            for role, tok in zip(roles, outs):
+                if isinstance(role, _Req):  # a running row's decode step
+                    q = role
+                    q.pos += 1
+                    q.issued += 1
+                    q.last_input = tok
+                    q.history.append(tok)
+                    q.n_sampled += 1
+                    if not q.cancelled.is_set():
+                        self._deliver(q, tok)
+                elif role[1]:  # the request's last chunk: its first token
+                    w = role[0]
+                    work.remove(w)
+                    self._started(w[0], w[1], tok, t0, t1)
+            for q in [q for q in self.active if q.finished()]:
+                self.active.remove(q)
+                self._retire(q)
 
     def _fail_req(self, req: _Req, e: BaseException) -> None:
         if req.sid is not None and req.sid in self.r.kv.seqs:

@@ -386,13 +386,14 @@ class TPRunnerProxy:
         seqs = self.r.kv.seqs
         return {str(sid): list(seqs[sid].tokens) for sid in sids if sid in seqs and seqs[sid].tokens}
 
-    def admit(self, sid: int, keep: int, tokens: list[int], opts, history: list[int], seed: int) -> None:
+    def admit(self, sid: int, keep: int, tokens: list[int], opts, history: list[int], seed: int,
+              n_sampled: int = 0) -> None:
         self._mirror("admit", sid=sid, keep=keep, tokens=list(tokens), opts=opts, history=list(history), seed=seed,
-                     prefixes=self._prefixes([sid]))
-        self.r.admit(sid, keep, tokens, opts, history, seed)
+                     n_sampled=n_sampled, prefixes=self._prefixes([sid]))
+        self.r.admit(sid, keep, tokens, opts, history, seed, n_sampled)
 
     def admit_many(self, items: list[tuple]) -> list[int]:
-        items = [(sid, keep, list(t), o, list(h), sd) for sid, keep, t, o, h, sd in items]
+        items = [(it[0], it[1], list(it[2]), it[3], list(it[4]), *it[5:]) for it in items]
         self._mirror("admit_many", items=items, prefixes=self._prefixes([it[0] for it in items]))
         return self.r.admit_many(items)
 
@@ -479,7 +480,8 @@ def worker_main() -> None:
                 pass
         elif op == "admit":
             adopt_prefixes(runner, cmd.get("prefixes"))
-            runner.admit(cmd["sid"], cmd["keep"], cmd["tokens"], cmd["opts"], cmd["history"], cmd["seed"])
+            runner.admit(cmd["sid"], cmd["keep"], cmd["tokens"], cmd["opts"], cmd["history"], cmd["seed"],
+                         cmd.get("n_sampled", 0))
         elif op == "admit_many":
             adopt_prefixes(runner, cmd.get("prefixes"))
             runner.admit_many(cmd["items"])

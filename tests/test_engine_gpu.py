@@ -257,6 +257,35 @@ def _scheduler_concurrent(tiny_models, invariant):
         assert sum(a == b for a, b in zip(solo, first[i])) >= lens[i] // 2, i
 
 
+def test_interleaved_admission_gpu(tiny_models):
+    """A burst admitted while a row decodes (scheduler chunk = 16): each chunk's forward carries the
+    running row's decode token (mixed prefill + decode segments through the MFMA flash / split decode
+    attention). Streams complete at their lengths, the running row kept stepping during the admission,
+    and each burst request's first token matches its solo prefill."""
+    from ollama_operator_amd.engine.scheduler import BatchScheduler
+    g = Runner(tiny_models["tiny-llama"], device="cuda", max_batch=32, max_seqs=8, ctx=256)
+    g.warmup()
+    g.capture_batch_graphs(4)
+    sch = BatchScheduler(g, max_parallel=4, chunk=16)
+    p1, p2 = [1] + list(range(40, 80)), [1] + list(range(100, 133))
+    g0 = sch.submit([1, 5, 9], SamplingOptions(temperature=0.7, seed=1), 40)
+    head = [next(g0), next(g0)]
+    with sch.cv:
+        g1 = sch.submit(p1, SamplingOptions(temperature=0), 10)
+        g2 = sch.submit(p2, SamplingOptions(temperature=0), 10)
+    out = [head + list(g0), list(g1), list(g2)]
+    sch.close()
+    assert [len(o) for o in out] == [40, 10, 10]
+    assert all(0 <= t < g.cfg.n_vocab for o in out for t in o)
+    assert sch.interleaved_chunks >= (40 + 33) // 16
+    s = Runner(tiny_models["tiny-llama"], device="cuda", max_batch=64, max_seqs=2, ctx=256)
+    for p, o in ((p1, out[1]), (p2, out[2])):
+        sid = s.new_sequence()
+        solo = list(s.generate(sid, p, SamplingOptions(temperature=0), max_tokens=2))
+        s.free_sequence(sid)
+        assert solo[0] == o[0]
+
+
 @pytest.mark.parametrize("name", ["tiny-llama", "tiny-mixtral"])
 def test_admit_many_gpu_matches_sequential(tiny_models, name):
     """Queued requests prefilled together (Runner.admit_many: one forward over every prompt row,

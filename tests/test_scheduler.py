@@ -175,3 +175,56 @@ def test_bad_request_in_a_burst_fails_alone(runner):
     with pytest.raises(ValueError):
         list(bad)
     sch.close()
+
+
+@pytest.mark.parametrize("chunk", [4, 0])
+def test_interleaved_admission_matches_solo(runner, chunk):
+    """A burst arriving while a row decodes: with chunk > 0 its prompts go through in chunks of `chunk`
+    tokens, each chunk's forward also stepping the running row (Runner.admit_many mixed items). Every
+    request must still produce exactly what it produces alone; chunk = 0 is the one-forward burst."""
+    p0, p1, p2 = [1, 5, 9, 13], [1] + list(range(40, 57)), [1] + list(range(80, 91))
+    o0, o1, o2 = SamplingOptions(temperature=0.8, seed=3), SamplingOptions(temperature=0), \
+        SamplingOptions(temperature=1.0, top_k=20, seed=9)
+    want = [solo(runner, p, o, n) for p, o, n in ((p0, o0, 30), (p1, o1, 12), (p2, o2, 9))]
+    r = Runner(runner, device="cpu", max_batch=16, max_seqs=8, ctx=256)
+    sch = BatchScheduler(r, max_parallel=4, chunk=chunk)
+    g0 = sch.submit(p0, o0, 30)
+    head = [next(g0), next(g0)]  # the first request is decoding
+    with sch.cv:  # the burst lands together
+        g1 = sch.submit(p1, o1, 12)
+        g2 = sch.submit(p2, o2, 9)
+    got = [head + list(g0), list(g1), list(g2)]
+    sch.close()
+    assert got == want
+    if chunk:
+        # 18 + 12 prompt tokens in chunks of 4 (the running row's token rides along in each)
+        assert sch.interleaved_chunks >= (17 + 11) // 4
+    else:
+        assert sch.interleaved_chunks == 0
+
+
+def test_burst_coalescing_admits_together(runner):
+    """Nothing decoding: requests arriving within the quiet window are admitted in one forward."""
+    r = Runner(runner, device="cpu", max_batch=16, max_seqs=8, ctx=256)
+    sch = BatchScheduler(r, max_parallel=4, coalesce_ms=500, quiet_ms=200)
+    calls = []
+    orig = r.admit_many
+
+    def spy(items):
+        calls.append(len(items))
+        return orig(items)
+
+    r.admit_many = spy
+    out = {}
+    th = []
+    for i in range(3):
+        t = threading.Thread(target=lambda i=i: out.setdefault(i, list(sch.submit([1, 10 + i, 20 + i],
+                                                                                 SamplingOptions(temperature=0), 3))))
+        t.start()
+        th.append(t)
+        time.sleep(0.02)
+    for t in th:
+        t.join(60)
+    sch.close()
+    assert calls and calls[0] == 3, calls
+    assert all(len(v) == 3 for v in out.values())
