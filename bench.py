@@ -39,17 +39,20 @@ MODEL_LABELS = {"llama2-7b": "Llama-2-7B", "llama2-13b": "Llama-2-13B", "llama2-
                 "gemma-2b": "Gemma-2B", "gemma-7b": "Gemma-7B"}
 
 
-def ensure_model(path: str, preset_name: str, ftype_name: str) -> str:
+def ensure_model(path: str, preset_name: str, ftype_name: str, ctx_len: int = 0) -> str:
+    """ctx_len > 0: the preset's architecture with its context length metadata replaced (random-init
+    weights carry no trained context; e.g. Llama-2-7B shapes at 8192 keys, --model-ctx)."""
     from ollama_operator_amd.gguf.constants import FileType
     from ollama_operator_amd.models.config import preset
     from ollama_operator_amd.models.random_init import write_random_gguf
-    tag = hashlib.sha1(f"{preset_name}:{ftype_name}:v1".encode()).hexdigest()[:10]
+    tag = hashlib.sha1(f"{preset_name}:{ftype_name}:{ctx_len}:v1".encode()).hexdigest()[:10]
     marker = path + "." + tag + ".ok"
     if os.path.exists(path) and os.path.exists(marker):
         return path
     os.makedirs(os.path.dirname(path), exist_ok=True)
     tmp = path + f".tmp{os.getpid()}"
-    write_random_gguf(tmp, preset(preset_name), FileType[f"MOSTLY_{ftype_name}"], seed=0)
+    cfg = preset(preset_name, ctx_len=ctx_len) if ctx_len > 0 else preset(preset_name)
+    write_random_gguf(tmp, cfg, FileType[f"MOSTLY_{ftype_name}"], seed=0)
     os.replace(tmp, path)
     open(marker, "w").close()
     return path
@@ -242,7 +245,7 @@ def launch_ranks(a) -> int:
         print(f"bench.py: --gpus {n} requested but only {have} GPU(s) are visible; refusing to report a "
               f"{have}-GPU number as {n}", file=sys.stderr, flush=True)
         return 2
-    ensure_model(model_path(a), a.model, a.ftype)
+    ensure_model(model_path(a), a.model, a.ftype, a.model_ctx)
     port = free_port()
     procs = []
     for r in range(n):
@@ -266,7 +269,8 @@ def launch_ranks(a) -> int:
 
 
 def model_path(a) -> str:
-    return os.path.join(a.dir, f"{a.model}-{a.ftype.lower()}.gguf")
+    ctx = f"-ctx{a.model_ctx}" if getattr(a, "model_ctx", 0) else ""
+    return os.path.join(a.dir, f"{a.model}-{a.ftype.lower()}{ctx}.gguf")
 
 
 def bench_tp(a) -> None:
@@ -282,7 +286,7 @@ def bench_tp(a) -> None:
         print(f"bench.py: --tp {T} needs {T} GPUs, {have} visible (pass --allow-shared to rehearse on fewer)",
               file=sys.stderr, flush=True)
         sys.exit(2)
-    path = ensure_model(model_path(a), a.model, a.ftype)
+    path = ensure_model(model_path(a), a.model, a.ftype, a.model_ctx)
     if shared or a.device == "cpu":
         os.environ["OMX_TP_BACKEND"] = "gloo"
     from ollama_operator_amd.parallel import tp
@@ -323,7 +327,7 @@ def bench_tp(a) -> None:
         r.close()
     finally:
         tp.shutdown_leader(world)
-    label = MODEL_LABELS.get(a.model, a.model) + " " + a.ftype
+    label = MODEL_LABELS.get(a.model, a.model) + " " + a.ftype + (f" (ctx {a.model_ctx})" if a.model_ctx else "")
     print(json.dumps({
         "metric": f"output tokens/sec {label}",
         "value": round(a.steps / dt, 2),
@@ -358,6 +362,9 @@ def main():
     ap.add_argument("--prompt", type=int, default=128)
     ap.add_argument("--model", default="llama2-7b")
     ap.add_argument("--ftype", default="Q4_K_M", type=str.upper)
+    ap.add_argument("--model-ctx", type=int, default=0,
+                    help="replace the preset's context length (random-init weights), e.g. 8192 for Llama-2-7B "
+                         "shapes at an 8k context; 0 = the preset's (Llama-2: 4096)")
     ap.add_argument("--dir", default=os.environ.get("OMX_BENCH_DIR", "/tmp/omx_bench"))
     ap.add_argument("--batch-extra", type=int, default=4,
                     help="also measure continuous-batching throughput with this many concurrent sequences per "
@@ -409,11 +416,11 @@ def main():
     from ollama_operator_amd.engine.sampling import SamplingOptions
 
     if local == 0:
-        ensure_model(path, a.model, a.ftype)
+        ensure_model(path, a.model, a.ftype, a.model_ctx)
     if world > 1:
         dist.barrier()
     else:
-        ensure_model(path, a.model, a.ftype)
+        ensure_model(path, a.model, a.ftype, a.model_ctx)
 
     long_ctx = [int(x) for x in a.long_ctx.split(",") if x.strip()] if gpu else []
     LC_WARM, LC_STEPS = 8, 64
@@ -514,7 +521,7 @@ def main():
             stop_server(server[0])
     else:
         weights_gb = runner.w.nbytes / 1e9
-    label = MODEL_LABELS.get(a.model, a.model) + " " + a.ftype
+    label = MODEL_LABELS.get(a.model, a.model) + " " + a.ftype + (f" (ctx {a.model_ctx})" if a.model_ctx else "")
     if rank == 0:
         print(json.dumps({
             "metric": f"output tokens/sec {label}",

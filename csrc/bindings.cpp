@@ -453,6 +453,7 @@ PYBIND11_MODULE(_C, m) {
         k.embed_scale = c.contains("embed_scale") ? c["embed_scale"].cast<float>() : 1.f;
         k.glu_act = c.contains("glu_act") ? c["glu_act"].cast<int>() : 0;
         k.Dc = c.contains("Dc") ? c["Dc"].cast<int>() : k.D;
+        k.kv8 = c.contains("kv8") ? c["kv8"].cast<int>() : 0;
         check_attn(k.H, k.Hkv, k.Dc, k.D);
         e.layers.assign(k.n_layer, LayerW{});
       })

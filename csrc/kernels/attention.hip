@@ -86,6 +86,35 @@ __device__ __forceinline__ void load_krow(const f16* p, KRow<DPL>& r) {
   }
 }
 
+// fp8 KV cache (OCP e4m3fn): four bytes -> four fp16
+__device__ __forceinline__ void e4m3x4_to_f16(unsigned w, f16* o) {
+  const auto a = __builtin_amdgcn_cvt_pk_f32_fp8(w, false), b = __builtin_amdgcn_cvt_pk_f32_fp8(w, true);
+  o[0] = (f16)a[0];
+  o[1] = (f16)a[1];
+  o[2] = (f16)b[0];
+  o[3] = (f16)b[1];
+}
+// one key's D/16 fp8 values for this lane (half the bytes of the fp16 row), widened to fp16
+template <int DPL>
+__device__ __forceinline__ void load_krow8(const uint8_t* p, KRow<DPL>& r) {
+  if constexpr (DPL == 8) {
+    const u32x2 t = __builtin_nontemporal_load((const u32x2*)p);
+    e4m3x4_to_f16(t.x, r.v);
+    e4m3x4_to_f16(t.y, r.v + 4);
+  } else if constexpr (DPL == 16) {
+    const u32x4 t = __builtin_nontemporal_load((const u32x4*)p);
+    e4m3x4_to_f16(t.x, r.v);
+    e4m3x4_to_f16(t.y, r.v + 4);
+    e4m3x4_to_f16(t.z, r.v + 8);
+    e4m3x4_to_f16(t.w, r.v + 12);
+  } else if constexpr (DPL == 4) {
+    e4m3x4_to_f16(*(const unsigned*)p, r.v);
+  } else {  // 5 / 6 / 7 (head dims 80 / 96 / 112): byte loads
+#pragma unroll
+    for (int j = 0; j < DPL; ++j) r.v[j] = (f16)__builtin_amdgcn_cvt_f32_fp8((unsigned)p[j], 0);
+  }
+}
+
 template <int DPL, int U>
 struct KVStep {
   KRow<DPL> k[U], v[U];
@@ -93,7 +122,7 @@ struct KVStep {
 
 // U key slots per lane group per step: 4, or 2 when 8 query heads share a KV head or the head dim is
 // 256 (registers: 4 slots of D = 256 spilled 188 B per lane)
-template <int D, int G, int U = (G >= 8 || D > 128 ? 2 : 4)>
+template <int D, int G, bool KV8 = false, int U = (G >= 8 || D > 128 ? 2 : 4)>
 __global__ __launch_bounds__(ATT_NT) void attn_decode_kernel(AttnParams P) {
   constexpr int DPL = D / 16;
   constexpr int ATT_U = U, ATT_STEP = ATT_NG * U;
@@ -161,8 +190,13 @@ __global__ __launch_bounds__(ATT_NT) void attn_decode_kernel(AttnParams P) {
         const long long blk = sbt[t / bs - b0];
         OMX_KASSERT(t >= 0 && t / bs - b0 < nb && blk >= 0);
         const long long base = ((blk * P.n_kv + kvh) * bs + (t % bs)) * D + li * DPL;
-        load_krow<DPL>(kc + base, st.k[u]);
-        load_krow<DPL>(vc + base, st.v[u]);
+        if constexpr (KV8) {
+          load_krow8<DPL>((const uint8_t*)P.kc + base, st.k[u]);
+          load_krow8<DPL>((const uint8_t*)P.vc + base, st.v[u]);
+        } else {
+          load_krow<DPL>(kc + base, st.k[u]);
+          load_krow<DPL>(vc + base, st.v[u]);
+        }
       }
     };
     auto consume = [&](int ts, const KVStep<DPL, U>& st) {
@@ -353,7 +387,7 @@ __device__ __forceinline__ int vswz(int row, int ch) {
   return VROW * row + 256 * (ch >> 4) + 16 * ((ch & 15) ^ (((row & 3) << 2) | ((row >> 2) & 3)));
 }
 
-template <int D>
+template <int D, bool KV8 = false>
 __global__ __launch_bounds__(256) void attn_prefill_kernel(AttnParams P) {
   constexpr int NKS = D / 16;             // k-steps of S^T over the head dim
   constexpr int NDT = (D + 31) / 32;      // 32-row d tiles of O^T
@@ -419,9 +453,25 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(AttnParams P) {
       const int row = min(i / KCH, PF_BK - 1), ch = i % KCH;
       const int t = min(kt0 + row, len_max - 1);
       const long long base = (((long long)bt[t / bs] * P.n_kv + kvh) * bs + (t % bs)) * D + 8 * ch;
-      kr[c] = *(const u32x4*)(kc + base);
-      vr[c] = *(const u32x4*)(vc + base);
+      if constexpr (KV8) {  // 8 fp8 bytes in .x / .y, widened at the LDS write
+        const u32x2 k8 = *(const u32x2*)((const uint8_t*)P.kc + base), v8 = *(const u32x2*)((const uint8_t*)P.vc + base);
+        kr[c] = (u32x4){k8.x, k8.y, 0u, 0u};
+        vr[c] = (u32x4){v8.x, v8.y, 0u, 0u};
+      } else {
+        kr[c] = *(const u32x4*)(kc + base);
+        vr[c] = *(const u32x4*)(vc + base);
+      }
     }
+  };
+  auto widen = [](const u32x4& r) -> u32x4 {  // KV8: 8 e4m3 bytes -> 8 fp16
+    if constexpr (!KV8) return r;
+    f16x8 h;
+    f16 t[8];
+    e4m3x4_to_f16(r.x, t);
+    e4m3x4_to_f16(r.y, t + 4);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) h[j] = t[j];
+    return __builtin_bit_cast(u32x4, h);
   };
   issue(k_lo);
   for (int kt0 = k_lo; kt0 < len_max; kt0 += PF_BK) {
@@ -431,8 +481,8 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(AttnParams P) {
       const int i = tid + 256 * c;
       if (i < PF_BK * KCH) {
         const int row = i / KCH, ch = i % KCH;
-        *(u32x4*)(Ks + row * LDK + 8 * ch) = kr[c];
-        *(u32x4*)(Vs + vswz<VROW>(row, ch)) = vr[c];
+        *(u32x4*)(Ks + row * LDK + 8 * ch) = widen(kr[c]);
+        *(u32x4*)(Vs + vswz<VROW>(row, ch)) = widen(vr[c]);
       }
     }
     __syncthreads();
@@ -523,17 +573,27 @@ static int heads_per_block(const AttnParams& P) {
   return hpb < 1 ? 1 : hpb;
 }
 
-template <int D>
-static void launch_d(const AttnParams& P, hipStream_t s) {
+template <int D, bool KV8>
+static void launch_dk(const AttnParams& P, hipStream_t s) {
   const int G = heads_per_block(P);
   dim3 grid(P.NQ, P.H / G, P.n_splits);
   switch (G) {
-    case 1: hipLaunchKernelGGL((attn_decode_kernel<D, 1>), grid, dim3(ATT_NT), 0, s, P); break;
-    case 2: hipLaunchKernelGGL((attn_decode_kernel<D, 2>), grid, dim3(ATT_NT), 0, s, P); break;
-    case 4: if constexpr (D <= 128) hipLaunchKernelGGL((attn_decode_kernel<D, 4>), grid, dim3(ATT_NT), 0, s, P); break;
-    case 8: if constexpr (D <= 128) hipLaunchKernelGGL((attn_decode_kernel<D, 8>), grid, dim3(ATT_NT), 0, s, P); break;
+    case 1: hipLaunchKernelGGL((attn_decode_kernel<D, 1, KV8>), grid, dim3(ATT_NT), 0, s, P); break;
+    case 2: hipLaunchKernelGGL((attn_decode_kernel<D, 2, KV8>), grid, dim3(ATT_NT), 0, s, P); break;
+    case 4: if constexpr (D <= 128) hipLaunchKernelGGL((attn_decode_kernel<D, 4, KV8>), grid, dim3(ATT_NT), 0, s, P); break;
+    case 8: if constexpr (D <= 128) hipLaunchKernelGGL((attn_decode_kernel<D, 8, KV8>), grid, dim3(ATT_NT), 0, s, P); break;
     default: break;
   }
+}
+template <int D>
+static void launch_d(const AttnParams& P, hipStream_t s) {
+  if (P.kv8) launch_dk<D, true>(P, s);
+  else launch_dk<D, false>(P, s);
+}
+template <int D>
+static void launch_pf(const AttnParams& P, dim3 grid, hipStream_t s) {
+  if (P.kv8) hipLaunchKernelGGL((attn_prefill_kernel<D, true>), grid, dim3(256), 0, s, P);
+  else hipLaunchKernelGGL((attn_prefill_kernel<D, false>), grid, dim3(256), 0, s, P);
 }
 
 void attention_decode(const AttnParams& P0, hipStream_t s) {
@@ -544,12 +604,12 @@ void attention_decode(const AttnParams& P0, hipStream_t s) {
     dim3 grid((P.NQ + PF_BQ - 1) / PF_BQ, P.H);
     count_launch(LC_ATTN_PREFILL);
     switch (P.D) {
-      case 64: hipLaunchKernelGGL(attn_prefill_kernel<64>, grid, dim3(256), 0, s, P); return;
-      case 80: hipLaunchKernelGGL(attn_prefill_kernel<80>, grid, dim3(256), 0, s, P); return;
-      case 96: hipLaunchKernelGGL(attn_prefill_kernel<96>, grid, dim3(256), 0, s, P); return;
-      case 112: hipLaunchKernelGGL(attn_prefill_kernel<112>, grid, dim3(256), 0, s, P); return;  // Orca (100)
-      case 128: hipLaunchKernelGGL(attn_prefill_kernel<128>, grid, dim3(256), 0, s, P); return;
-      case 256: hipLaunchKernelGGL(attn_prefill_kernel<256>, grid, dim3(256), 0, s, P); return;  // Gemma
+      case 64: launch_pf<64>(P, grid, s); return;
+      case 80: launch_pf<80>(P, grid, s); return;
+      case 96: launch_pf<96>(P, grid, s); return;
+      case 112: launch_pf<112>(P, grid, s); return;  // Orca (100)
+      case 128: launch_pf<128>(P, grid, s); return;
+      case 256: launch_pf<256>(P, grid, s); return;  // Gemma
       default: break;
     }
   }

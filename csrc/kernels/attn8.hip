@@ -209,7 +209,7 @@ bool a8_g(const Attn8Params& P, int grid, size_t lds, hipStream_t s) {
 
 bool attn8(const GemvParams& A, const GemvParams& B, const GemvParams& O, const AttnParams& At, void* sync,
            hipStream_t s) {
-  if (!sync || A.B != 1 || !A.x8 || !A.x8_stat || A.epi != EPI_QKV || A.D != A8_D || At.D != A8_D || At.window > 0 ||
+  if (!sync || At.kv8 || A.kv8 || A.B != 1 || !A.x8 || !A.x8_stat || A.epi != EPI_QKV || A.D != A8_D || At.D != A8_D || At.window > 0 ||
       At.NQ != 1 || O.B != 1 || !O.x8 || !O.emit8 || !O.emit8_nw || !O.emit8_stat || O.epi != EPI_ADD ||
       O.w.K != At.H * A8_D || A.w.K % 64 || A.w.K > 8192 || O.w.N % 16 || At.H % At.n_kv)
     return false;

@@ -227,7 +227,7 @@ bool ao_g(const AttnOParams& Q, int G, int grid, size_t lds, hipStream_t s) {
 }  // namespace
 
 bool attn_o(const GemvParams& O, const AttnParams& At, void* img, void* sync, hipStream_t s) {
-  if (!img || !sync || !At.ws || !At.counters || O.B != 1 || O.epi != EPI_ADD || !O.emit8 || !O.emit8_nw ||
+  if (!img || !sync || At.kv8 || !At.ws || !At.counters || O.B != 1 || O.epi != EPI_ADD || !O.emit8 || !O.emit8_nw ||
       !O.emit8_stat || At.D != A8_D || (At.Dv != 0 && At.Dv != A8_D) || At.window > 0 || At.NQ != 1 ||
       At.H % At.n_kv || At.n_kv > 64 || O.w.K != At.H * A8_D || O.w.N % 16 || At.n_splits < 1 || At.n_splits > 32)
     return false;

@@ -32,6 +32,17 @@ __device__ __forceinline__ float h2f(uint16_t h) {
   return (float)v;
 }
 
+// fp8 KV cache (OMX_KV_CACHE_TYPE=fp8): one OCP e4m3fn byte per element (gfx950 v_cvt_pk_fp8_f32),
+// saturated to the format's +-448 (the conversion itself does not clamp)
+__device__ __forceinline__ uint8_t f2e4m3(float v) {
+  return (uint8_t)(__builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(v, -448.f), 448.f), 0.f, 0, false) & 0xFF);
+}
+// element idx of a K or V cache row: fp16 or fp8 by kv8
+__device__ __forceinline__ void kv_store(void* base, long long idx, float v, int kv8) {
+  if (kv8) ((uint8_t*)base)[idx] = f2e4m3(v);
+  else ((f16*)base)[idx] = (f16)v;
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, OMX_WAVE);

@@ -118,8 +118,8 @@ __device__ __forceinline__ void epi_rows(const GemvParams& P, float (&acc)[1][BT
           if (which == 1) __hip_atomic_store((unsigned short*)P.kc + idx, bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           else __hip_atomic_store((unsigned short*)P.vc + idx, bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else {
-          if (which == 1) ((f16*)P.kc)[idx] = (f16)out;
-          else ((f16*)P.vc)[idx] = (f16)out;
+          if (which == 1) kv_store(P.kc, idx, out, P.kv8);
+          else kv_store(P.vc, idx, out, P.kv8);
         }
       }
     } else {

@@ -36,6 +36,7 @@ struct GemvParams {
   const float* inv_freq;       // [n_rot/2]
   int Eq, Ekv, D, n_rot, n_kv, bs;
   int Dc;                      // KV cache row stride (head dim padded to 16 on the GPU; 0 = D)
+  int kv8;                     // KV cache elements are fp8 e4m3 (OCP e4m3fn, 1 byte) instead of fp16
   // MoE: blockIdx.z = k-th selected expert of batch row b
   const int* expert_ids;       // [B][n_sel] or null
   const float* expert_w;       // [B][n_sel] routing weights (EPI_ADD scale) or null
@@ -210,6 +211,7 @@ struct AttnParams {
   int kps;                     // target keys per split (0 -> g_attn_kps)
   int defer;                   // write exactly n_splits unmerged partials (attention_ws_floats layout
                                // [NQ][S][H*D] then [NQ][S][H][2] {m, l}); the consumer merges them
+  int kv8;                     // kc / vc hold fp8 e4m3 (OCP e4m3fn) instead of fp16
 };
 void attention_decode(const AttnParams& P, hipStream_t s);
 size_t attention_ws_floats(int NQ, int H, int D, int n_splits);

@@ -85,7 +85,7 @@ bool qtype_ok(int q) { return q == QT_Q4_K || q == QT_Q6_K || q == QT_Q4_0 || q 
 }  // namespace
 
 bool qkv_attn(const GemvParams& A, const GemvParams& B, const AttnParams& At, void* img, void* sync, hipStream_t s) {
-  if (!sync || !img || A.B != 1 || !A.x8 || !A.x8_stat || A.epi != EPI_QKV || A.emit8 || A.D != A8_D ||
+  if (!sync || !img || At.kv8 || A.kv8 || A.B != 1 || !A.x8 || !A.x8_stat || A.epi != EPI_QKV || A.emit8 || A.D != A8_D ||
       At.D != A8_D || At.window > 0 || At.NQ != 1 || A.w.K % 64 || A.w.K > 8192 || At.H % At.n_kv ||
       At.n_kv > 64 || A.row_offset != 0 || !qtype_ok(A.w.qtype))
     return false;

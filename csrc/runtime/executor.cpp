@@ -158,6 +158,7 @@ void Executor::attn_block(int i, const StepInputs& in, hipStream_t s) {
   P.Ekv = Ekv;
   P.D = cfg.D;
   P.Dc = cfg.Dc;
+  P.kv8 = cfg.kv8;
   P.n_rot = cfg.n_rot;
   P.n_kv = cfg.Hkv;
   P.bs = in.bs;  // the next GEMV of the step (gemv.hip cross-launch prefetch)
@@ -182,6 +183,7 @@ void Executor::attn_block(int i, const StepInputs& in, hipStream_t s) {
     A.H = cfg.H;
     A.n_kv = cfg.Hkv;
     A.D = cfg.Dc > 0 ? cfg.Dc : cfg.D;
+    A.kv8 = cfg.kv8;
     A.Dv = cfg.D;
     A.bs = in.bs;
     A.scale = 1.0f / std::sqrt((float)cfg.D);
@@ -231,6 +233,7 @@ void Executor::attn_block(int i, const StepInputs& in, hipStream_t s) {
     A.H = cfg.H;
     A.n_kv = cfg.Hkv;
     A.D = cfg.Dc > 0 ? cfg.Dc : cfg.D;
+    A.kv8 = cfg.kv8;
     A.Dv = cfg.D;
     A.bs = in.bs;
     A.scale = 1.0f / std::sqrt((float)cfg.D);
@@ -274,6 +277,7 @@ void Executor::attn_block(int i, const StepInputs& in, hipStream_t s) {
   A.H = cfg.H;
   A.n_kv = cfg.Hkv;
   A.D = cfg.Dc > 0 ? cfg.Dc : cfg.D;
+  A.kv8 = cfg.kv8;
   A.Dv = cfg.D;
   A.bs = in.bs;
   A.scale = 1.0f / std::sqrt((float)cfg.D);

@@ -16,6 +16,7 @@ struct ExecConfig {
   int arch = 0;          // 0 llama-family (llama/mistral/mixtral), 1 phi2
   int E = 0, H = 0, Hkv = 0, D = 0, n_rot = 0, F = 0, n_layer = 0, V = 0;  // per-rank (TP) sizes
   int Dc = 0;            // KV cache row stride (head dim padded to a multiple of 16; 0 = D)
+  int kv8 = 0;           // fp8 e4m3 KV cache (OMX_KV_CACHE_TYPE=fp8), else fp16
   float eps = 1e-5f;
   int n_expert = 0, n_expert_used = 0;
   int window = 0;

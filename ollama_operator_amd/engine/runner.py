@@ -48,7 +48,8 @@ class NativeExec:
         e.configure(dict(arch=1 if cfg.arch == "phi2" else 0, E=loc["E"], H=loc["H"], Hkv=loc["Hkv"], D=loc["D"], Dc=r.Dc,
                          n_rot=cfg.n_rot, F=loc["F"], n_layer=cfg.n_layer, V=loc["V"], eps=float(cfg.norm_eps),
                          n_expert=cfg.n_expert, n_expert_used=cfg.n_expert_used, window=cfg.sliding_window,
-                         tp=r.tp_size, embed_scale=float(cfg.embed_scale), glu_act=int(cfg.gelu_glu)))
+                         tp=r.tp_size, embed_scale=float(cfg.embed_scale), glu_act=int(cfg.gelu_glu),
+                         kv8=int(getattr(r, "kv8", False))))
         p = lambda t: t.data_ptr() if t is not None else 0  # noqa: E731
         e.set_globals(w.tok_embd.tup, p(w.out_norm), p(w.out_norm_b), w.lm_head.tup, p(w.lm_bias), p(w.inv_freq))
         for i, L in enumerate(w.layers):
@@ -129,6 +130,13 @@ class NativeExec:
         self.exe.step(self.stages[stage], layer, B, n_logits, use_idx, prefill, stream_handle() if self.on_gpu else 0)
 
 
+def kv_cache_type() -> str:
+    """GPU KV cache element type from OMX_KV_CACHE_TYPE / OLLAMA_KV_CACHE_TYPE: "fp8" (e4m3; also for
+    Ollama's "q8_0", the 8-bit setting) or "f16" (default; "q4_0" falls back to it)."""
+    v = (os.environ.get("OMX_KV_CACHE_TYPE") or os.environ.get("OLLAMA_KV_CACHE_TYPE") or "f16").strip().lower()
+    return "fp8" if v in ("fp8", "e4m3", "q8_0") else "f16"
+
+
 @dataclass
 class StepTimes:
     prompt_tokens: int = 0
@@ -189,9 +197,15 @@ class Runner:
         # GPU cache rows are as wide as an attention kernel's head dim (Orca Mini's 100 -> 112, zero pad);
         # the CPU backends keep the model's head dim
         self.Dc = cache_head_dim(loc["D"]) if self.is_gpu else loc["D"]
-        self.kc = [kv_alloc(n_blocks, loc["Hkv"], block_size, self.Dc, device=dev, dtype=torch.float16)
+        # KV cache element type: fp16 (Ollama's default f16) or, on the GPU, fp8 e4m3 (OCP e4m3fn, half the
+        # bytes every decode step streams: OMX_KV_CACHE_TYPE=fp8, or Ollama's OLLAMA_KV_CACHE_TYPE=q8_0,
+        # served by this 8-bit format instead of q8_0 blocks)
+        self.kv_type = kv_cache_type() if self.is_gpu else "f16"
+        self.kv8 = self.kv_type == "fp8"
+        kv_dt = torch.uint8 if self.kv8 else torch.float16
+        self.kc = [kv_alloc(n_blocks, loc["Hkv"], block_size, self.Dc, device=dev, dtype=kv_dt)
                    for _ in range(cfg.n_layer)]
-        self.vc = [kv_alloc(n_blocks, loc["Hkv"], block_size, self.Dc, device=dev, dtype=torch.float16)
+        self.vc = [kv_alloc(n_blocks, loc["Hkv"], block_size, self.Dc, device=dev, dtype=kv_dt)
                    for _ in range(cfg.n_layer)]
         self.resid = torch.zeros(max_batch, E, **f32)
         self.qbuf = torch.zeros(max_batch, Eq, **f32)
