@@ -21,6 +21,7 @@
 //    in the same launch. The grid is fixed, so the launch is hipGraph-capturable for any length.
 // Causal prefill uses the same kernel: each prompt token is a query with length pos + 1.
 #include <stdexcept>
+#include <type_traits>
 #include <string>
 
 #include "common.h"
@@ -48,6 +49,15 @@ __device__ __forceinline__ float row16_sum_a(float v) {
   v += dppf<0x4E>(v);
   v += dppf<0x141>(v);
   v += dppf<0x140>(v);
+  return v;
+}
+// sum over the LPK (16 or 8) lanes of one key: quad sums, then row_half_mirror (8), then row_mirror (16)
+template <int LPK>
+__device__ __forceinline__ float key_sum(float v) {
+  v += dppf<0xB1>(v);
+  v += dppf<0x4E>(v);
+  v += dppf<0x141>(v);
+  if constexpr (LPK == 16) v += dppf<0x140>(v);
   return v;
 }
 
@@ -115,17 +125,59 @@ __device__ __forceinline__ void load_krow8(const uint8_t* p, KRow<DPL>& r) {
   }
 }
 
-template <int DPL, int U>
+// fp8 rows whose lane width is a multiple of 4 stay raw in registers (DPL / 4 dwords, half the staging
+// registers of the widened fp16 row) and are widened to fp32 where they are consumed
+template <int DPL>
+struct KRow8 {
+  unsigned w[DPL / 4];
+};
+template <int DPL>
+__device__ __forceinline__ void load_krow8_raw(const uint8_t* p, KRow8<DPL>& r) {
+  if constexpr (DPL == 16) {
+    const u32x4 t = __builtin_nontemporal_load((const u32x4*)p);
+    r.w[0] = t.x, r.w[1] = t.y, r.w[2] = t.z, r.w[3] = t.w;
+  } else if constexpr (DPL == 8) {
+    const u32x2 t = __builtin_nontemporal_load((const u32x2*)p);
+    r.w[0] = t.x, r.w[1] = t.y;
+  } else {
+#pragma unroll
+    for (int i = 0; i < DPL / 4; ++i) r.w[i] = ((const unsigned*)p)[i];
+  }
+}
+template <int DPL>
+__device__ __forceinline__ void row_f32(const KRow<DPL>& r, float (&o)[DPL]) {
+#pragma unroll
+  for (int j = 0; j < DPL; ++j) o[j] = (float)r.v[j];
+}
+template <int DPL>
+__device__ __forceinline__ void row_f32(const KRow8<DPL>& r, float (&o)[DPL]) {
+#pragma unroll
+  for (int i = 0; i < DPL / 4; ++i) {
+    const auto a = __builtin_amdgcn_cvt_pk_f32_fp8(r.w[i], false), b = __builtin_amdgcn_cvt_pk_f32_fp8(r.w[i], true);
+    o[4 * i] = a[0], o[4 * i + 1] = a[1], o[4 * i + 2] = b[0], o[4 * i + 3] = b[1];
+  }
+}
+
+// RAW: fp8 rows kept as KRow8 (KV8 with DPL % 4 == 0), else fp16 KRow (fp8 rows widened at load)
+template <int DPL, int U, bool RAW = false>
 struct KVStep {
-  KRow<DPL> k[U], v[U];
+  typedef typename std::conditional<RAW, KRow8<DPL>, KRow<DPL>>::type Row;
+  Row k[U], v[U];
 };
 
 // U key slots per lane group per step: 4, or 2 when 8 query heads share a KV head or the head dim is
-// 256 (registers: 4 slots of D = 256 spilled 188 B per lane)
-template <int D, int G, bool KV8 = false, int U = (G >= 8 || D > 128 ? 2 : 4)>
+// 256 (registers: 4 slots of D = 256 spilled 188 B per lane).
+// LPK lanes per key: 16 (D / 16 dims per lane: one 16-B fp16 load at D = 128), or 8 for the fp8 cache at
+// D = 128 (16 dims per lane: again one 16-B load, so a wave keeps the same bytes per load instruction in
+// flight; 16 lanes per key would move 8 B per load and stay load-issue bound, profiles/r5_kv8)
+template <int D, int G, bool KV8 = false, int LPK = 16, int U = (G >= 8 || D > 128 ? 2 : 4)>
 __global__ __launch_bounds__(ATT_NT) void attn_decode_kernel(AttnParams P) {
-  constexpr int DPL = D / 16;
-  constexpr int ATT_U = U, ATT_STEP = ATT_NG * U;
+  static_assert(LPK == 16 || (LPK == 8 && D % 8 == 0), "lanes per key");
+  constexpr int DPL = D / LPK;
+  constexpr int KPW = 64 / LPK;                 // keys (lane groups) per wave
+  constexpr int NG = KPW * ATT_NW;              // lane groups per block
+  constexpr int ATT_U = U, ATT_STEP = NG * U;
+  constexpr bool RAW = KV8 && DPL % 4 == 0;
   __shared__ float sm[ATT_NW][G][D + 2];
   __shared__ int sbt[ATT_BTW];
   const int qi = blockIdx.x, split = blockIdx.z;
@@ -142,8 +194,8 @@ __global__ __launch_bounds__(ATT_NT) void attn_decode_kernel(AttnParams P) {
   const int chunk = (nk + S - 1) / S;
   const int t0 = kstart + split * chunk;
   const int t1 = min(len, t0 + chunk);
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, tg = lane >> 4, li = lane & 15;
-  const int grp = wave * 4 + tg;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, tg = lane / LPK, li = lane % LPK;
+  const int grp = wave * KPW + tg;
 
   const int Dv = P.Dv > 0 ? P.Dv : D;  // valid dims: q / output head stride; dims >= Dv are padding
   float q[G][DPL];
@@ -183,14 +235,17 @@ __global__ __launch_bounds__(ATT_NT) void attn_decode_kernel(AttnParams P) {
     for (int i = threadIdx.x; i < nb; i += ATT_NT) sbt[i] = bt[b0 + i];
     __syncthreads();
 
-    auto issue = [&](int ts, KVStep<DPL, U>& st) {
+    auto issue = [&](int ts, KVStep<DPL, U, RAW>& st) {
 #pragma unroll
       for (int u = 0; u < ATT_U; ++u) {
-        const int t = min(ts + u * ATT_NG + grp, w1 - 1);  // clamped; masked at use
+        const int t = min(ts + u * NG + grp, w1 - 1);  // clamped; masked at use
         const long long blk = sbt[t / bs - b0];
         OMX_KASSERT(t >= 0 && t / bs - b0 < nb && blk >= 0);
         const long long base = ((blk * P.n_kv + kvh) * bs + (t % bs)) * D + li * DPL;
-        if constexpr (KV8) {
+        if constexpr (RAW) {
+          load_krow8_raw<DPL>((const uint8_t*)P.kc + base, st.k[u]);
+          load_krow8_raw<DPL>((const uint8_t*)P.vc + base, st.v[u]);
+        } else if constexpr (KV8) {
           load_krow8<DPL>((const uint8_t*)P.kc + base, st.k[u]);
           load_krow8<DPL>((const uint8_t*)P.vc + base, st.v[u]);
         } else {
@@ -199,46 +254,58 @@ __global__ __launch_bounds__(ATT_NT) void attn_decode_kernel(AttnParams P) {
         }
       }
     };
-    auto consume = [&](int ts, const KVStep<DPL, U>& st) {
+    auto consume = [&](int ts, const KVStep<DPL, U, RAW>& st) {
       float sc[ATT_U][G];
 #pragma unroll
       for (int u = 0; u < ATT_U; ++u) {
-        const bool ok = ts + u * ATT_NG + grp < w1;  // uniform within the 16-lane group
+        const bool ok = ts + u * NG + grp < w1;  // uniform within the key's lane group
+        float kf[DPL];
+        row_f32(st.k[u], kf);
 #pragma unroll
         for (int g = 0; g < G; ++g) {
           float s = 0.f;
 #pragma unroll
-          for (int j = 0; j < DPL; ++j) s += q[g][j] * (float)st.k[u].v[j];
-          s = row16_sum_a(s);
+          for (int j = 0; j < DPL; ++j) s += q[g][j] * kf[j];
+          s = key_sum<LPK>(s);
           sc[u][g] = ok ? s : -INFINITY;
         }
       }
+      float p[ATT_U][G];
 #pragma unroll
       for (int g = 0; g < G; ++g) {
         float mn = m[g];
 #pragma unroll
         for (int u = 0; u < ATT_U; ++u) mn = fmaxf(mn, sc[u][g]);
-        if (mn == -INFINITY) continue;  // nothing visible yet in this group
+        if (mn == -INFINITY) {  // nothing visible yet in this group
+#pragma unroll
+          for (int u = 0; u < ATT_U; ++u) p[u][g] = 0.f;
+          continue;
+        }
         const float corr = __expf(m[g] - mn);
-        float p[ATT_U], ps = 0.f;
+        float ps = 0.f;
 #pragma unroll
         for (int u = 0; u < ATT_U; ++u) {
-          p[u] = __expf(sc[u][g] - mn);
-          ps += p[u];
+          p[u][g] = __expf(sc[u][g] - mn);
+          ps += p[u][g];
         }
         l[g] = l[g] * corr + ps;
 #pragma unroll
-        for (int j = 0; j < DPL; ++j) {
-          float a = acc[g][j] * corr;
-#pragma unroll
-          for (int u = 0; u < ATT_U; ++u) a += p[u] * (float)st.v[u].v[j];
-          acc[g][j] = a;
-        }
+        for (int j = 0; j < DPL; ++j) acc[g][j] *= corr;
         m[g] = mn;
+      }
+      // P.V one key slot at a time: a row is widened once and feeds every head of the group
+#pragma unroll
+      for (int u = 0; u < ATT_U; ++u) {
+        float vf[DPL];
+        row_f32(st.v[u], vf);
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+          for (int j = 0; j < DPL; ++j) acc[g][j] += p[u][g] * vf[j];
       }
     };
 
-    KVStep<DPL, U> A, B;
+    KVStep<DPL, U, RAW> A, B;
     int ts = w0;
     issue(ts, A);
     while (true) {
@@ -253,9 +320,9 @@ __global__ __launch_bounds__(ATT_NT) void attn_decode_kernel(AttnParams P) {
     }
   }
 
-  // merge the 4 key groups of the wave (lanes li, li+16, li+32, li+48)
+  // merge the key groups of the wave (lanes li, li + LPK, ...)
 #pragma unroll
-  for (int sh = 16; sh <= 32; sh <<= 1) {
+  for (int sh = LPK; sh <= 32; sh <<= 1) {
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       const float mo = __shfl_xor(m[g], sh, 64), lo = __shfl_xor(l[g], sh, 64);
@@ -268,7 +335,7 @@ __global__ __launch_bounds__(ATT_NT) void attn_decode_kernel(AttnParams P) {
       m[g] = mn;
     }
   }
-  if (lane < 16) {
+  if (lane < LPK) {
 #pragma unroll
     for (int g = 0; g < G; ++g) {
 #pragma unroll
@@ -577,9 +644,10 @@ template <int D, bool KV8>
 static void launch_dk(const AttnParams& P, hipStream_t s) {
   const int G = heads_per_block(P);
   dim3 grid(P.NQ, P.H / G, P.n_splits);
+  constexpr int LPK8 = KV8 && D == 128 ? 8 : 16;  // fp8 rows at D = 128: 8 lanes x 16 B per key
   switch (G) {
-    case 1: hipLaunchKernelGGL((attn_decode_kernel<D, 1, KV8>), grid, dim3(ATT_NT), 0, s, P); break;
-    case 2: hipLaunchKernelGGL((attn_decode_kernel<D, 2, KV8>), grid, dim3(ATT_NT), 0, s, P); break;
+    case 1: hipLaunchKernelGGL((attn_decode_kernel<D, 1, KV8, LPK8>), grid, dim3(ATT_NT), 0, s, P); break;
+    case 2: hipLaunchKernelGGL((attn_decode_kernel<D, 2, KV8, LPK8>), grid, dim3(ATT_NT), 0, s, P); break;
     case 4: if constexpr (D <= 128) hipLaunchKernelGGL((attn_decode_kernel<D, 4, KV8>), grid, dim3(ATT_NT), 0, s, P); break;
     case 8: if constexpr (D <= 128) hipLaunchKernelGGL((attn_decode_kernel<D, 8, KV8>), grid, dim3(ATT_NT), 0, s, P); break;
     default: break;
