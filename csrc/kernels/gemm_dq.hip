@@ -10,6 +10,7 @@ namespace omx {
 int g_dq_enable = -1;  // -1: OMX_GEMM_DQ (default on), read once
 int g_dq_cfg = -2;     // OMX_DQ_CFG: force tile config 0..3 (microbenchmarks); -2 = not read yet
 int g_dq_sk = 0;       // > 0: force the split-K factor (microbenchmarks, set_dq_tuning)
+int g_dq_dbg = 0;      // OMX_DQ_DBG=1: no operand reloads after the first K step (timing probe only)
 
 void run_dq_q4k(const GemvParams& P, f16* xp, int Kp, hipStream_t s);  // gemm_dq_q4k.hip
 void run_dq_q5k(const GemvParams& P, f16* xp, int Kp, hipStream_t s);  // gemm_dq_q5k.hip
@@ -26,6 +27,8 @@ bool dq_gemm_enabled() {
   if (g_dq_cfg == -2) {
     const char* c = getenv("OMX_DQ_CFG");
     g_dq_cfg = c ? atoi(c) : -1;
+    const char* d = getenv("OMX_DQ_DBG");
+    g_dq_dbg = d ? atoi(d) : 0;
   }
   return g_dq_enable != 0;
 }

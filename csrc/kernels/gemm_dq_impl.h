@@ -296,7 +296,8 @@ __device__ __forceinline__ void dq_out(const GemvParams& P, const f32x16 (&acc)[
 
 // ------------------------------------------------------------------------------------------------
 template <int QT, int BM, int BN, int WM, int WN>
-__global__ __launch_bounds__(DQ_NT, 1) void dq_gemm_kernel(GemvParams P, const f16* __restrict__ X, int Kp, int sk) {
+__global__ __launch_bounds__(DQ_NT, 1) void dq_gemm_kernel(GemvParams P, const f16* __restrict__ X, int Kp, int sk,
+                                                            int dbg) {
   static_assert(WM * WN == 8, "8 waves");
   constexpr int TM = BM / WM / 32, TN = BN / WN / 32;  // 32 x 32 accumulator tiles per wave
   constexpr int XS = BM * DQ_BK, WS = BN * DQ_BK;      // halves per LDS buffer (128-B rows, swizzled)
@@ -339,10 +340,14 @@ __global__ __launch_bounds__(DQ_NT, 1) void dq_gemm_kernel(GemvParams P, const f
   typedef __attribute__((address_space(1))) void glb_void;
 
   Piece<QT> wreg;
+  // dbg (microbenchmark only, OMX_DQ_DBG=1): after the first step no operand is re-loaded -- the
+  // pipeline's compute, LDS and barrier time alone (garbage results)
   auto issue_w = [&](int ks) {
+    if (dbg && ks > ks0 + 1) return;
     if (wact) load_piece<QT>(w, wrow, SB, 2 * ks + wh, wreg);
   };
   auto issue_x = [&](int ks, int buf) {
+    if (dbg && ks > ks0 + 1) return;
 #pragma unroll
     for (int i = 0; i < XL; ++i)
       __builtin_amdgcn_global_load_lds((glb_void*)(xsrc[i] + ks * DQ_BK), (lds_void*)(Xs + buf * XS + (64 * i + 8 * wave) * DQ_BK),
@@ -454,6 +459,7 @@ constexpr size_t dq_lds() { return (size_t)(2 * BM + 2 * BN) * DQ_BK * sizeof(f1
 }  // namespace
 
 extern int g_dq_cfg;  // gemm_dq.hip: forced tile config (microbenchmarks), -1 auto
+extern int g_dq_dbg;  // gemm_dq.hip: OMX_DQ_DBG microbenchmark mode (no operand reloads), 0 in production
 extern int g_dq_sk;   // gemm_dq.hip: forced split-K factor (microbenchmarks), 0 auto
 
 namespace {
@@ -462,7 +468,8 @@ template <int QT, int BM, int BN, int WM, int WN>
 void launch_dq(const GemvParams& P, const f16* xp, int Kp, int sk, hipStream_t s) {
   const int mt = (P.B + BM - 1) / BM, nt = (P.w.N + BN - 1) / BN;
   const size_t lds = dq_lds<BM, BN>();
-  hipLaunchKernelGGL((dq_gemm_kernel<QT, BM, BN, WM, WN>), dim3(mt * nt * sk), dim3(DQ_NT), lds, s, P, xp, Kp, sk);
+  hipLaunchKernelGGL((dq_gemm_kernel<QT, BM, BN, WM, WN>), dim3(mt * nt * sk), dim3(DQ_NT), lds, s, P, xp, Kp, sk,
+                     g_dq_dbg);
 }
 
 template <int QT>
