@@ -95,3 +95,18 @@ def test_unsupported_head_dim_fails_at_load(tmp_path):
                       FileType.MOSTLY_Q8_0, seed=1)
     with pytest.raises(UnsupportedArchitecture):
         Runner(p, device="cpu", max_batch=4, max_seqs=1, ctx=32)
+
+
+def test_kv_cache_type_env(tiny_models, monkeypatch):
+    """OMX_KV_CACHE_TYPE / OLLAMA_KV_CACHE_TYPE select the GPU KV element type (fp8 for the 8-bit settings,
+    f16 otherwise); the CPU backends always keep fp16 rows."""
+    from ollama_operator_amd.engine.runner import kv_cache_type
+    for env, val, want in (("OMX_KV_CACHE_TYPE", "fp8", "fp8"), ("OLLAMA_KV_CACHE_TYPE", "q8_0", "fp8"),
+                           ("OLLAMA_KV_CACHE_TYPE", "q4_0", "f16"), ("OLLAMA_KV_CACHE_TYPE", "F16", "f16")):
+        monkeypatch.delenv("OMX_KV_CACHE_TYPE", raising=False)
+        monkeypatch.delenv("OLLAMA_KV_CACHE_TYPE", raising=False)
+        monkeypatch.setenv(env, val)
+        assert kv_cache_type() == want, (env, val)
+    monkeypatch.setenv("OMX_KV_CACHE_TYPE", "fp8")
+    r = Runner(tiny_models["tiny-llama"], device="cpu", max_batch=8, max_seqs=1, ctx=64)
+    assert not r.kv8 and r.kc[0].dtype == torch.float16
