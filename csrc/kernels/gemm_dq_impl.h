@@ -83,24 +83,39 @@ __host__ __device__ __forceinline__ int piece_off(int t, int sb, int g) {
 // byte i = 4 ((p & 15) / 4) + (0, 2, 1, 3)[p & 3] -> natural k = piece_off(t, sb, g) + i
 template <int QT>
 __global__ __launch_bounds__(256) void prep_xp_kernel(GemvParams P, f16* out, int Kp) {
+  // K-quant / Q4_0 / Q8_0 rows: the normalised row is staged in LDS in natural order (coalesced global
+  // reads of x and the norm weights), then every thread gathers its 8 stream positions from LDS and
+  // writes them as one 16-B store. Gathering straight from global memory made every x read a scattered
+  // 4-B load: 36 us per call at 2048 rows, 10 % of the 2048-token TTFT (profiles/r5_gemm prefill trace)
+  extern __shared__ float xs[];  // [Kp] (quantized rows; F16 rows do not use it)
   __shared__ float red[4];
   const int b = blockIdx.x, K = P.w.K, SB = Kp >> 8;
   const float* x = P.x + (long long)b * P.ldx;
   float mean = 0.f, rstd = 1.f;
-  if (P.norm != NORM_NONE) {
+  constexpr bool STAGE = QT != QT_F16;
+  if (P.norm != NORM_NONE || STAGE) {
     float s = 0.f, ss = 0.f;
     for (int i = threadIdx.x; i < K / 4; i += 256) {
       const f32x4 v = *(const f32x4*)(x + 4 * i);
+      if constexpr (STAGE) *(f32x4*)(xs + 4 * i) = v;
       s += v.x + v.y + v.z + v.w;
       ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
     }
-    ss = block_sum<256>(ss, red);
-    if (P.norm == NORM_LAYER) {
-      s = block_sum<256>(s, red);
-      mean = s / K;
-      rstd = rsqrtf(fmaxf(ss / K - mean * mean, 0.f) + P.eps);
-    } else {
-      rstd = rsqrtf(ss / K + P.eps);
+    for (int k = (K & ~3) + threadIdx.x; k < K; k += 256) {  // K % 4 tail
+      const float v = x[k];
+      if constexpr (STAGE) xs[k] = v;
+      s += v;
+      ss += v * v;
+    }
+    if (P.norm != NORM_NONE) {
+      ss = block_sum<256>(ss, red);
+      if (P.norm == NORM_LAYER) {
+        s = block_sum<256>(s, red);
+        mean = s / K;
+        rstd = rsqrtf(fmaxf(ss / K - mean * mean, 0.f) + P.eps);
+      } else {
+        rstd = rsqrtf(ss / K + P.eps);
+      }
     }
   }
   f16* o = out + (long long)b * Kp;
@@ -123,6 +138,20 @@ __global__ __launch_bounds__(256) void prep_xp_kernel(GemvParams P, f16* out, in
       *(f16x8*)(o + 8 * c) = v;
     }
   } else {
+    // the norm in place (natural order, coalesced weight reads), zero padding past K
+    __syncthreads();  // the staged row (and block_sum's broadcast) are visible
+    for (int k = threadIdx.x; k < Kp; k += 256) {
+      float e = 0.f;
+      if (k < K) {
+        e = xs[k];
+        if (P.norm != NORM_NONE) {
+          e = (e - mean) * rstd * P.norm_w[k];
+          if (P.norm == NORM_LAYER && P.norm_b) e += P.norm_b[k];
+        }
+      }
+      xs[k] = e;
+    }
+    __syncthreads();
     for (int c = threadIdx.x; c < Kp / 8; c += 256) {
       const int kp = 8 * c, pc = kp >> 5, p0 = kp & 31;
       const int t = pc / SB, sb = pc - t * SB;
@@ -131,16 +160,7 @@ __global__ __launch_bounds__(256) void prep_xp_kernel(GemvParams P, f16* out, in
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int r = j & 3;
-        const int k = base + 4 * (j >> 2) + (r == 1 ? 2 : r == 2 ? 1 : r);
-        float e = 0.f;
-        if (k < K) {
-          e = x[k];
-          if (P.norm != NORM_NONE) {
-            e = (e - mean) * rstd * P.norm_w[k];
-            if (P.norm == NORM_LAYER && P.norm_b) e += P.norm_b[k];
-          }
-        }
-        v[j] = (f16)e;
+        v[j] = (f16)xs[base + 4 * (j >> 2) + (r == 1 ? 2 : r == 2 ? 1 : r)];
       }
       *(f16x8*)(o + kp) = v;
     }
@@ -474,7 +494,7 @@ void launch_dq(const GemvParams& P, const f16* xp, int Kp, int sk, hipStream_t s
 
 template <int QT>
 void run_dq(const GemvParams& P, f16* xp, int Kp, hipStream_t s) {
-  hipLaunchKernelGGL(prep_xp_kernel<QT>, dim3(P.B), dim3(256), 0, s, P, xp, Kp);
+  hipLaunchKernelGGL(prep_xp_kernel<QT>, dim3(P.B), dim3(256), QT == QT_F16 ? 0 : (size_t)Kp * sizeof(float), s, P, xp, Kp);
   const int M = P.B, N = P.w.N, nks = Kp / DQ_BK;
   // tile x split-K from a wave model calibrated on MI355X (scripts/bench_dq_sweep.py, profiles/r4_gemm):
   // time = waves * (K steps per split) * c[cfg] + split-K slab traffic, waves = ceil(units / slots);

@@ -3,14 +3,25 @@
 Usage: python scripts/ktrace_prefill.py gpurun_out/prof/bench_kernel_trace.csv"""
 import collections
 import csv
+import re
 import sys
 
 from ktrace_step import short
 
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
-first = next(i for i, r in enumerate(rows) if "sample_kernel" in r["Kernel_Name"])
-# the prompt pass: from the embedding gather that precedes the first sampler
-start = max(i for i in range(first) if "embed_rows" in rows[i]["Kernel_Name"])
+samp = [i for i, r in enumerate(rows) if re.search(r"sample(_fast)?_kernel", r["Kernel_Name"])]
+# the prompt pass: the longest span from an embedding gather to the next sampler launch (warm-up
+# graph captures and decode steps are short; the timed prompt is the long one)
+best = None
+for a, b in zip([-1] + samp[:-1], samp):
+    emb = [i for i in range(a + 1, b) if "embed_rows" in rows[i]["Kernel_Name"]]
+    if not emb:
+        continue
+    st = emb[0]
+    dur = int(rows[b]["End_Timestamp"]) - int(rows[st]["Start_Timestamp"])
+    if best is None or dur > best[0]:
+        best = (dur, st, b)
+_, start, first = best
 seg = rows[start:first + 1]
 span = int(seg[-1]["End_Timestamp"]) - int(seg[0]["Start_Timestamp"])
 busy = collections.Counter()
