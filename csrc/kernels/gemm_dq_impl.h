@@ -138,29 +138,41 @@ __global__ __launch_bounds__(256) void prep_xp_kernel(GemvParams P, f16* out, in
       *(f16x8*)(o + 8 * c) = v;
     }
   } else {
-    // the norm in place (natural order, coalesced weight reads), zero padding past K
+    // a 16-B output chunk is 8 CONSECUTIVE natural positions base .. base + 7 in the order
+    // 0 2 1 3 4 6 5 7: two 16-B LDS reads (+ two of the norm weights), permuted in registers
     __syncthreads();  // the staged row (and block_sum's broadcast) are visible
-    for (int k = threadIdx.x; k < Kp; k += 256) {
-      float e = 0.f;
-      if (k < K) {
-        e = xs[k];
-        if (P.norm != NORM_NONE) {
-          e = (e - mean) * rstd * P.norm_w[k];
-          if (P.norm == NORM_LAYER && P.norm_b) e += P.norm_b[k];
-        }
-      }
-      xs[k] = e;
-    }
-    __syncthreads();
+    const bool nrm = P.norm != NORM_NONE, lnb = P.norm == NORM_LAYER && P.norm_b;
     for (int c = threadIdx.x; c < Kp / 8; c += 256) {
       const int kp = 8 * c, pc = kp >> 5, p0 = kp & 31;
       const int t = pc / SB, sb = pc - t * SB;
       const int base = piece_off<QT>(t, sb, p0 >> 4) + 4 * ((p0 & 15) >> 2);
       f16x8 v;
+      if (base + 8 <= K) {
+        f32x4 a = *(const f32x4*)(xs + base), b = *(const f32x4*)(xs + base + 4);
+        if (nrm) {
+          const f32x4 wa = *(const f32x4*)(P.norm_w + base), wb = *(const f32x4*)(P.norm_w + base + 4);
+          a = (a - mean) * rstd * wa;
+          b = (b - mean) * rstd * wb;
+          if (lnb) {
+            a += *(const f32x4*)(P.norm_b + base);
+            b += *(const f32x4*)(P.norm_b + base + 4);
+          }
+        }
+        v = (f16x8){(f16)a.x, (f16)a.z, (f16)a.y, (f16)a.w, (f16)b.x, (f16)b.z, (f16)b.y, (f16)b.w};
+      } else {  // the row's K padding (Q4_0 / Q8_0 with K % 256 != 0)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int r = j & 3;
-        v[j] = (f16)xs[base + 4 * (j >> 2) + (r == 1 ? 2 : r == 2 ? 1 : r)];
+        for (int j = 0; j < 8; ++j) {
+          const int r = j & 3, k = base + 4 * (j >> 2) + (r == 1 ? 2 : r == 2 ? 1 : r);
+          float e = 0.f;
+          if (k < K) {
+            e = xs[k];
+            if (nrm) {
+              e = (e - mean) * rstd * P.norm_w[k];
+              if (lnb) e += P.norm_b[k];
+            }
+          }
+          v[j] = (f16)e;
+        }
       }
       *(f16x8*)(o + kp) = v;
     }
@@ -494,7 +506,8 @@ void launch_dq(const GemvParams& P, const f16* xp, int Kp, int sk, hipStream_t s
 
 template <int QT>
 void run_dq(const GemvParams& P, f16* xp, int Kp, hipStream_t s) {
-  hipLaunchKernelGGL(prep_xp_kernel<QT>, dim3(P.B), dim3(256), QT == QT_F16 ? 0 : (size_t)Kp * sizeof(float), s, P, xp, Kp);
+  hipLaunchKernelGGL(prep_xp_kernel<QT>, dim3(P.B), dim3(256), QT == QT_F16 ? 0 : (size_t)P.w.K * sizeof(float), s, P, xp,
+                     Kp);
   const int M = P.B, N = P.w.N, nks = Kp / DQ_BK;
   // tile x split-K from a wave model calibrated on MI355X (scripts/bench_dq_sweep.py, profiles/r4_gemm):
   // time = waves * (K steps per split) * c[cfg] + split-K slab traffic, waves = ceil(units / slots);
