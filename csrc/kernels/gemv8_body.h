@@ -367,9 +367,11 @@ __device__ __forceinline__ void gemv8_body(const GemvParams& P, const int bx) {
           }
         }
         __syncthreads();
-        if (tid < nb)
-          emit_group((char*)P.emit8 + (size_t)tid * x8_slots_dev(N) * 24, N, t, stage + 32 * tid, stage + 32 * tid + 16,
-                     P.emit8_stat + tid * x8_stat_ld_dev(N));
+        if (tid < 16 * nb) {  // batch row tid / 16 on 16 lanes of wave 0
+          const int b = tid >> 4, i = tid & 15;
+          emit_group16((char*)P.emit8 + (size_t)b * x8_slots_dev(N) * 24, N, t, stage[32 * b + i], stage[32 * b + 16 + i],
+                       P.emit8_stat + b * x8_stat_ld_dev(N), i);
+        }
         __syncthreads();  // the stage is reused by the next tile
       } else {  // EM_GLU: even row = gate, odd = up; 8 outputs per tile, a group per tile pair
         const int half = (t & 1) * 8;
@@ -384,9 +386,15 @@ __device__ __forceinline__ void gemv8_body(const GemvParams& P, const int bx) {
         }
         if ((t & 1) || t + 1 >= n_tiles) {
           __syncthreads();
-          if (tid < nb)
-            emit_group<WT>((char*)P.emit8 + (size_t)tid * x8_slots_dev(N / 2) * 24, N / 2, t >> 1, stage + 32 * tid,
-                           nullptr, nullptr);
+          if constexpr (WT) {  // write-through hand-off inside the launch (ffn8): the one-lane form
+            if (tid < nb)
+              emit_group<WT>((char*)P.emit8 + (size_t)tid * x8_slots_dev(N / 2) * 24, N / 2, t >> 1, stage + 32 * tid,
+                             nullptr, nullptr);
+          } else if (tid < 16 * nb) {
+            const int b = tid >> 4, i = tid & 15;
+            emit_group16((char*)P.emit8 + (size_t)b * x8_slots_dev(N / 2) * 24, N / 2, t >> 1, stage[32 * b + i], 0.f,
+                         nullptr, i);
+          }
           __syncthreads();
         }
       }

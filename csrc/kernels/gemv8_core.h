@@ -61,6 +61,31 @@ __device__ __forceinline__ void emit_group(void* img, int Kc, int G, const float
   }
 }
 
+// emit_group spread over the 16 lanes of a row group (lane i holds staged value i): max and code sum by
+// 16-lane shuffles, one byte store per lane, lane 0 writes the scale pair and the RMS partial. The same
+// codes and scales as emit_group (integer sum, exact max); the partial's float sum is a tree. The
+// producers' tails ran the one-lane form: ~0.6 us of gate_up's 12 us (scripts/bench_gemv8.py NOEMIT)
+__device__ __forceinline__ void emit_group16(void* img, int Kc, int G, float v, float sq, float* stat, int i) {
+  float amax = fabsf(v);
+#pragma unroll
+  for (int m = 8; m >= 1; m >>= 1) amax = fmaxf(amax, __shfl_xor(amax, m, 16));
+  const float d = amax / 127.f, id = amax > 0.f ? 127.f / amax : 0.f;
+  const int q = (int)rintf(v * id);
+  int qsum = q;
+#pragma unroll
+  for (int m = 8; m >= 1; m >>= 1) qsum += __shfl_xor(qsum, m, 16);
+  const int XSP = x8_slots_dev(Kc);
+  const int slot = (G >> 4) * XPAD + (G & 15);
+  ((int8_t*)img)[16 * slot + i] = (int8_t)q;
+  if (i == 0) ((f32x2*)((char*)img + (size_t)XSP * 16))[slot] = (f32x2){d, d * (float)qsum};
+  if (stat) {
+    float ss = sq;
+#pragma unroll
+    for (int m = 8; m >= 1; m >>= 1) ss += __shfl_xor(ss, m, 16);
+    if (i == 0) stat[G] = ss;
+  }
+}
+
 // In-launch hand-off (MI355X_MICROARCH.md "Valid forms" table row 1): every storing wave waits for
 // its (sc1, write-through) stores, the workgroup barriers, one lane adds to an agent-scope counter; the
 // consumer polls it with sc1 loads, its other waves load after a barrier, every handed-off byte is

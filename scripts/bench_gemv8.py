@@ -93,7 +93,7 @@ def main():
         ops = {"x8": img.data_ptr(), "dbg8": int(os.environ.get("OMX_BENCH_DBG8", "0"))}
         if rms:
             ops["x8_stat"] = st.data_ptr()
-        if emits:
+        if emits and not os.environ.get("OMX_BENCH_NOEMIT"):  # NOEMIT: the producer without its int8 emission
             ops.update(emit8=out.data_ptr(), emit8_nw=nw.data_ptr())
             if epi == EPI_ADD:
                 ops["emit8_stat"] = ost.data_ptr()
@@ -178,7 +178,8 @@ def main():
             torch.cuda.synchronize()
             ts.append(e0.elapsed_time(e1) * 1e3 / n_launch)
         t = float(np.median(ts))
-        tag = ("hot " if hot else "cold") + (" mem-only" if ops["dbg8"] else "")
+        tag = ("hot " if hot else "cold") + (" mem-only" if ops["dbg8"] else "") + \
+            (" no-emit" if emits and os.environ.get("OMX_BENCH_NOEMIT") else "")
         print(f"{name:9s} {tag} {t:7.2f} us/launch  {nbytes / t / 1e3:7.1f} GB/s  "
               f"({len(tups)} copies, {nbytes / 1e6:.1f} MB)", flush=True)
         del g, tups, keep
