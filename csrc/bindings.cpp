@@ -224,6 +224,10 @@ PYBIND11_MODULE(_C, m) {
     P.ld_emit = ii("ld_emit");
     P.emit_nw = Pp<const float>(ip("emit_nw"));
     P.emit_stat = Pp<float>(ip("emit_stat"));
+    P.emit_prev = Pp<const float>(ip("emit_prev"));
+    P.emit_prev_n = ii("emit_prev_n");
+    P.emit_scale = Pp<float>(ip("emit_scale"));
+    P.xscale = Pp<const float>(ip("xscale"));
     P.y16 = Pp<void>(ip("y16"));
     P.ld16y = ii("ld16y");
     if ((P.x16 || P.emit16 || P.y16) && !gemv_mb_supported(P))

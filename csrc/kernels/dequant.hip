@@ -7,37 +7,57 @@ namespace omx {
 
 // one block per gathered row; each thread dequantises 32-weight pieces. A negative row id -(j + 1)
 // takes row j of `ext` ([*][K] fp32, unscaled) instead: multimodal inputs (projected image patches,
-// models/clip.py) enter the sequence as such rows
+// models/clip.py) enter the sequence as such rows.
+// stat (optional, the batched fp16 decode chain): per-16-element sum-of-squares partials [n][K / 16] of
+// the gathered rows, the "residual before the add" of layer 0's O emission (gemv_mfma.hip range scale)
 __global__ __launch_bounds__(256) void embed_rows_kernel(QMat w, const int* rows, float* out, int ldo, float scale,
-                                                         const float* ext) {
+                                                         const float* ext, float* stat) {
   const int b = blockIdx.x;
   const long long row = rows[b];
   const int P = w.K / 32;
   float* o = out + (long long)b * ldo;
+  float* st = stat ? stat + (long long)b * (w.K / 16) : nullptr;
   if (row < 0) {
     const float* src = ext + (-row - 1) * (long long)w.K;
     OMX_KASSERT(ext != nullptr);
     for (int i = threadIdx.x; i < w.K; i += blockDim.x) o[i] = ext ? src[i] : 0.f;
+    if (st) {
+      for (int g = threadIdx.x; g < w.K / 16; g += blockDim.x) {
+        float s = 0.f;
+        for (int i = 0; i < 16; ++i) s += ext ? src[16 * g + i] * src[16 * g + i] : 0.f;
+        st[g] = s;
+      }
+    }
     return;
   }
   for (int p = threadIdx.x; p < P; p += blockDim.x) {
     float lo[16], hi[16];
     int olo, ohi;
     dequant_piece(w, row, p, lo, hi, olo, ohi);
+    float slo = 0.f, shi = 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      lo[j] *= scale;
+      hi[j] *= scale;
+      slo += lo[j] * lo[j];
+      shi += hi[j] * hi[j];
+    }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      *(f32x4*)(o + olo + 4 * j) =
-          (f32x4){lo[4 * j], lo[4 * j + 1], lo[4 * j + 2], lo[4 * j + 3]} * scale;
-      *(f32x4*)(o + ohi + 4 * j) =
-          (f32x4){hi[4 * j], hi[4 * j + 1], hi[4 * j + 2], hi[4 * j + 3]} * scale;
+      *(f32x4*)(o + olo + 4 * j) = (f32x4){lo[4 * j], lo[4 * j + 1], lo[4 * j + 2], lo[4 * j + 3]};
+      *(f32x4*)(o + ohi + 4 * j) = (f32x4){hi[4 * j], hi[4 * j + 1], hi[4 * j + 2], hi[4 * j + 3]};
+    }
+    if (st) {  // 16-element pieces: every group of the row written once (only the row total is used)
+      st[olo >> 4] = slo;
+      st[ohi >> 4] = shi;
     }
   }
 }
 
 void embed_rows(const QMat& w, const int* rows, int n, float* out, int ldo, hipStream_t s, float scale,
-                const float* ext) {
+                const float* ext, float* stat) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(embed_rows_kernel, dim3(n), dim3(256), 0, s, w, rows, out, ldo, scale, ext);
+  hipLaunchKernelGGL(embed_rows_kernel, dim3(n), dim3(256), 0, s, w, rows, out, ldo, scale, ext, stat);
 }
 
 // rows on blockIdx.y (grid-stride), pieces of a row on x (no 64-bit index division per piece); PERM:

@@ -209,6 +209,14 @@ struct MUnit {
 //   eo[0]: EPI_ADD old y | eo[1]: bias[vn] | eo[2]: EPI_QKV bias[vn ^ 1] |
 //   eo[3]: emit_nw[vn] (residual emission) or inv_freq[d / 2] (EPI_QKV)
 constexpr int MB_EO = 4;
+
+// emission range exponent e of a residual row from its old mean square: the row is stored times 2^-e,
+// e = floor(log2(rms)) - 2 clamped to [0, 30], so fp16 keeps values up to ~2^18 x the row RMS (a
+// random-init 32-layer stack grows its residual past fp16's 65504; trained rows keep e = 0)
+__device__ __forceinline__ int emit_range_exp(float ms) {
+  const int k = (int)floorf(0.5f * __log2f(fminf(fmaxf(ms, 1e-30f), 1e30f)));
+  return min(max(k - 2, 0), 30);
+}
 __device__ __forceinline__ void mb_epi_load(const GemvParams& P, int tile, float (&eo)[MB_EO]) {
   const int lane = threadIdx.x & 63, j = lane & 15, q = lane >> 4, wave = threadIdx.x >> 6;
   const int row = min(tile * 16 + j, P.w.N - 1), vn = row + P.row_offset;
@@ -496,6 +504,9 @@ __device__ __forceinline__ void mb_body(const GemvParams& P, const int bx, const
   const int n_units = my_tiles * upt;
   const bool av = j < B;         // A-operand lane: batch row j
   const bool rs = G16 && P.xstat != nullptr && !(DBG & 2);
+  const bool es = P.emit16 != nullptr && P.emit_prev != nullptr;  // emission range scale (never with rs)
+  const float* sx = rs ? P.xstat : P.emit_prev;
+  const int sxn = rs ? P.xstat_n : P.emit_prev_n;
 
   // per-row epilogue operands (EPI_QKV) of this lane's batch row 4 q + (wave & 3), first
   int e_pos = 0, e_slot = 0;
@@ -504,13 +515,14 @@ __device__ __forceinline__ void mb_body(const GemvParams& P, const int bx, const
     e_pos = P.pos[b];
     e_slot = P.slot[b];
   }
-  // 0. (AM_G16) RMS partials [16][xstat_n] of this wave's batch rows w, w + 8 (coalesced rows)
+  // 0. (AM_G16) RMS partials [16][xstat_n] of this wave's batch rows w, w + 8 (coalesced rows); for an
+  // emitting producer with emit_prev, the partials of the residual before the add (the range scale)
   float sp[2][MB_SPL];
 #pragma unroll
   for (int h = 0; h < 2; ++h)
 #pragma unroll
     for (int k = 0; k < MB_SPL; ++k) sp[h][k] = 0.f;
-  if (rs) {
+  if (rs || es) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int b = wave + 8 * h;
@@ -518,8 +530,8 @@ __device__ __forceinline__ void mb_body(const GemvParams& P, const int bx, const
 #pragma unroll
         for (int k = 0; k < MB_SPL; ++k) {
           const int p = lane + 64 * k;
-          const float v = P.xstat[(long long)b * P.xstat_n + min(p, P.xstat_n - 1)];
-          sp[h][k] = p < P.xstat_n ? v : 0.f;
+          const float v = sx[(long long)b * sxn + min(p, sxn - 1)];
+          sp[h][k] = p < sxn ? v : 0.f;
         }
       }
     }
@@ -603,17 +615,28 @@ __device__ __forceinline__ void mb_body(const GemvParams& P, const int bx, const
 #pragma unroll
     for (int r = 0; r < RD; ++r) load_unit(U[r], r);
   }
-  // 4. per-row RMS scale from the producer's partials
-  if (rs) {
+  // 4. per-row RMS scale from the producer's partials (times the producer's range scale), or this
+  // producer's own emission range scale 2^-e (srstd doubles as its LDS slot)
+  if (rs || es) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       float s = 0.f;
 #pragma unroll
       for (int k = 0; k < MB_SPL; ++k) s += sp[h][k];
       s = wave_sum(s);
-      if (lane == 0 && wave + 8 * h < B) srstd[wave + 8 * h] = rsqrtf(s / K + P.eps);
+      const int b = wave + 8 * h;
+      if (lane == 0 && b < B) {
+        if (rs) {
+          srstd[b] = rsqrtf(s / K + P.eps) * (P.xscale ? P.xscale[b] : 1.f);
+        } else {
+          const int e = emit_range_exp(s / N);
+          srstd[b] = __builtin_ldexpf(1.f, -e);
+          if (bx == 0 && P.emit_scale) P.emit_scale[b] = __builtin_ldexpf(1.f, e);
+        }
+      }
     }
   }
+  if (!es && P.emit16 && P.emit_scale && bx == 0 && tid < B) P.emit_scale[tid] = 1.f;
   // staged rows and srstd visible to every wave
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 
@@ -641,7 +664,8 @@ __device__ __forceinline__ void mb_body(const GemvParams& P, const int bx, const
         if (P.bias) x += eo[1];
         const float nv = eo[0] + x;
         P.y[(long long)b * P.ldy + vn] = nv;
-        ((f16*)P.emit16)[(long long)b * P.ld_emit + vn] = (f16)(nv * eo[3]);
+        const float c = es ? srstd[b] : 1.f;  // range scale 2^-e of the emitted row (exact)
+        ((f16*)P.emit16)[(long long)b * P.ld_emit + vn] = (f16)(nv * eo[3] * c);
         sq = nv * nv;
       }
       sq = mb_row16_sum(sq);  // the 16 lanes of a DPP row hold the tile's 16 rows of batch row b
@@ -795,6 +819,7 @@ bool gemv_mb_supported(const GemvParams& P) {
   if (q != QT_Q4_K && q != QT_Q6_K && q != QT_Q4_0 && q != QT_Q8_0) return false;
   if ((n_sb_host(P.w.K) + MB_NW - 1) / MB_NW > 8) return false;
   if (P.emit16 && (P.epi != EPI_ADD || !P.emit_nw || !P.emit_stat)) return false;
+  if (P.emit_prev && (!P.emit16 || P.xstat || P.emit_prev_n < 1 || P.emit_prev_n > 64 * MB_SPL)) return false;
   if (P.y16 && P.epi != EPI_GLU && P.epi != EPI_GEGLU) return false;
   const int am = mb_am(P);
   if (am == AM_G16) {  // activations already normalised (times norm_w) and fp16 in global memory

@@ -85,6 +85,14 @@ struct GemvParams {
   int ld_emit;
   const float* emit_nw;
   float* emit_stat;            //   and its per-16-row-tile sum-of-squares partials [tiles][16]
+  // fp16 range guard of the emission: row b is stored times 2^-e_b, with e_b from the RMS of the residual
+  // BEFORE the add (emit_prev: that row's partials [B][emit_prev_n], the previous emission's slab), and
+  // 2^e_b goes to emit_scale[b]; the consumer multiplies its outputs by xscale[b] (= that emit_scale).
+  // e_b = 0 while the old RMS is below 8, so ordinary rows are stored exactly as without it.
+  const float* emit_prev;
+  int emit_prev_n;
+  float* emit_scale;
+  const float* xscale;
   void* y16;                   // EPI_GLU / EPI_GEGLU: fp16 output [B][ld16y] instead of y
   int ld16y;
   // batch-1 int8 activation chain (gemv8.hip): the producer of a GEMV's input writes it already
@@ -184,7 +192,7 @@ void set_gemv_tuning(int blocks_per_cu, int rows, int debug, int ks = -1, int xf
 // Dequantize rows of a repacked matrix (embedding gather / fp16 copies)
 // rows[i] < 0: row -(rows[i] + 1) of ext [*][w.K] (external embeddings, e.g. image patches)
 void embed_rows(const QMat& w, const int* rows, int n, float* out, int ldo, hipStream_t s, float scale = 1.f,
-                const float* ext = nullptr);
+                const float* ext = nullptr, float* stat = nullptr);
 // rows [row0, row0 + w.N) of w (an expert's slice of a stacked MoE matrix); perm: prep_x16 K order
 void dequant_f16(const QMat& w, void* out_f16, hipStream_t s, int perm = 0, long long row0 = 0);
 

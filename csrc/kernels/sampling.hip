@@ -283,6 +283,9 @@ __device__ void legacy_select(const SampleParams& P, int b, float* lg, int V, in
 }
 
 __device__ __forceinline__ void finish_sample(const SampleParams& P, int b, int chosen, float chosen_lp) {
+  // a non-finite logit row (an overflowed activation upstream) must not turn into an out-of-range id:
+  // the id is the next step's embedding row, read on device without a host check
+  if ((unsigned)chosen >= (unsigned)P.V) chosen = 0;
   const int seen = P.hist_count[b];
   P.out[b] = chosen;
   if (P.out_logprob) P.out_logprob[b] = chosen_lp;
@@ -372,6 +375,7 @@ __global__ __launch_bounds__(SAMPLE_NT) void sample_fast_kernel(SampleParams P) 
   if (fast) {
     const int ix = base + lane;
     float v = ix < V ? lg[ix] : -INFINITY;
+    if (v != v) v = -INFINITY;  // NaN ranks last (every comparison with it is false)
     // penalties for the tokens of this slice (counts via LDS, applied in registers)
     const int seen = P.hist_count[b];
     const int win = min(min(seen, P.repeat_last_n[b]), P.hist_cap);

@@ -34,19 +34,27 @@ bool Executor::chain(const StepInputs& in) const {
          cfg.n_expert == 0 && ws.xa16 && ws.h16 && ws.a16 && ws.st[0] && ws.st[1];
 }
 
+// a partial slab st[0] / st[1] is [16][n] sum-of-squares partials followed by 16 row scales 2^e (the
+// emission range guard, gemv_mfma.hip emit_range_exp); the runner sizes it 16 * n + 16 floats
 static void chain_in(GemvParams& P, const void* x16, int ld16, const float* xstat, int n_stat) {
   P.x16 = x16;
   P.ld16 = ld16;
   P.zrow16 = MB_CHAIN_MAX;
   P.xstat = xstat;
   P.xstat_n = n_stat;
+  P.xscale = xstat ? xstat + 16 * n_stat : nullptr;
 }
 
-static void chain_emit(GemvParams& P, void* e16, int ld, const float* nw, float* st) {
+// prev: the slab holding the partials of the residual before this producer's add (null: scale 1)
+static void chain_emit(GemvParams& P, void* e16, int ld, const float* nw, float* st, const float* prev) {
+  const int n = (P.w.N + 15) / 16;
   P.emit16 = e16;
   P.ld_emit = ld;
   P.emit_nw = nw;
   P.emit_stat = st;
+  P.emit_scale = st + 16 * n;
+  P.emit_prev = prev;
+  P.emit_prev_n = prev ? n : 0;
 }
 
 // every projection of the chain takes the matrix-core kernel (a fallback kernel would neither emit nor
@@ -62,7 +70,7 @@ bool Executor::chain_capable() const {
     P.norm = norm;
     P.n_sel = 1;
     if (x16) chain_in(P, dummy, 256, norm == NORM_RMS ? dummy : nullptr, (cfg.E + 15) / 16);
-    if (emit) chain_emit(P, (void*)dummy, 256, dummy, (float*)dummy);
+    if (emit) chain_emit(P, (void*)dummy, 256, dummy, (float*)dummy, nullptr);
     return gemv_mb_supported(P);
   };
   for (const LayerW& L : layers) {
@@ -132,7 +140,8 @@ bool Executor::x8_capable(int B) const {
 }
 
 void Executor::embed(const StepInputs& in, hipStream_t s) {
-  embed_rows(tok_embd, in.tokens, in.B, ws.resid, cfg.E, s, cfg.embed_scale, ws.ext);
+  // the batched fp16 chain: the embedded rows' partials go to st[1], read by layer 0's O emission
+  embed_rows(tok_embd, in.tokens, in.B, ws.resid, cfg.E, s, cfg.embed_scale, ws.ext, chain(in) ? ws.st[1] : nullptr);
 }
 
 void Executor::attn_block(int i, const StepInputs& in, hipStream_t s) {
@@ -341,7 +350,8 @@ void Executor::attn_block(int i, const StepInputs& in, hipStream_t s) {
   O.ldy = E;
   if (ch) {
     chain_in(O, ws.a16, ws.ld_q, nullptr, 0);
-    chain_emit(O, ws.xa16, ws.ld_e, L.ffn_norm, ws.st[0]);  // gate_up's RMSNorm input
+    // the residual before O: its partials are in st[1] (layer i - 1's down emission, or the embedding's)
+    chain_emit(O, ws.xa16, ws.ld_e, L.ffn_norm, ws.st[0], ws.st[1]);  // gate_up's RMSNorm input
   }
   if (q8 && cfg.tp == 1) x8_emit(O, ws.x8e, L.ffn_norm, ws.x8st);  // gate_up's RMSNorm input, int8
   gemv(O, s);
@@ -472,7 +482,8 @@ void Executor::ffn_block(int i, const StepInputs& in, hipStream_t s) {
   Dn.ldy = E;
   if (ch) {  // the next RMSNorm'd GEMV: layer i+1's QKV, or the LM head
     chain_in(Dn, ws.h16, ws.ld_f, nullptr, 0);
-    chain_emit(Dn, ws.xa16, ws.ld_e, i + 1 < (int)layers.size() ? layers[i + 1].attn_norm : out_norm, ws.st[1]);
+    chain_emit(Dn, ws.xa16, ws.ld_e, i + 1 < (int)layers.size() ? layers[i + 1].attn_norm : out_norm, ws.st[1],
+               ws.st[0]);
   }
   if (q8 && cfg.tp > 1) {
     x8_in(Dn, ws.x8f, nullptr);  // partial sums to the slab: the all-reduce emits the next image

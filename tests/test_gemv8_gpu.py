@@ -327,3 +327,31 @@ def test_engine_batched_x8_chain_matches_single(tiny_models, B, monkeypatch):
         g.decode_batch([sid], [len(p)])
         torch.cuda.synchronize()
         assert rel(batched[b], g.logits[0, :V].float().cpu()) < 3e-2, b
+
+
+@pytest.mark.parametrize("qd", [GGMLType.Q4_0, GGMLType.Q4_K, GGMLType.Q6_K])
+def test_batched_rows_down_ks4(qd):
+    """2 batch rows on the residual producer at K = 14336 (Mistral-7B / Llama-3-8B down: 56 super-blocks,
+    the in-block K split over 4 wave groups, 1024-thread blocks)"""
+    B, E, F = 2, 4096, 14336
+    h = torch.randn(B, F, device="cuda")
+    nbF = C().x8_bytes(F)
+    himg = torch.zeros(B * nbF, dtype=torch.uint8, device="cuda")
+    for b in range(B):
+        img, _ = make_image(h[b])
+        himg[b * nbF:(b + 1) * nbF] = img
+    md = QM(qd, E, F, seed=35)
+    resid0 = torch.randn(B, E, device="cuda") * 4
+    resid = resid0.clone()
+    nw2 = torch.rand(E, device="cuda") + 0.5
+    out = torch.zeros(B * C().x8_bytes(E), dtype=torch.uint8, device="cuda")
+    ld = C().x8_stat_ld(E)
+    sto = torch.zeros(B * ld + 4, device="cuda")
+    call(md, B, None, resid, EPI_ADD, {"x8": himg.data_ptr(), "emit8": out.data_ptr(), "emit8_nw": nw2.data_ptr(),
+                                       "emit8_stat": sto.data_ptr()})
+    torch.cuda.synchronize()
+    hq = torch.stack([decode_image(himg[b * nbF:(b + 1) * nbF], F) for b in range(B)]).cuda()
+    assert rel(resid - resid0, hq @ md.w.T) < 1.5e-2, qd
+    nbE = C().x8_bytes(E)
+    for b in range(B):
+        assert rel(decode_image(out[b * nbE:(b + 1) * nbE], E), (resid[b] * nw2).cpu()) < 1e-2, (qd, b)

@@ -244,3 +244,76 @@ def test_mb_glu_fp16_output():
     ref = torch.nn.functional.silu(gu[:, 0::2]) * gu[:, 1::2]
     assert rel(h16[:B].float(), ref) < 5e-3
     assert float(y.abs().max()) == 0.0  # the fp16 output replaces the fp32 one
+
+
+@pytest.mark.parametrize("qt", [GGMLType.Q4_0, GGMLType.Q4_K])
+def test_mb_chain_range_scale(qt):
+    """A residual past fp16's range (random-init 32-layer stacks reach ~6e4 by layer 21; Mistral-7B at
+    B = 4 went NaN there): the producer stores row b times 2^-e_b, e_b from the RMS of the residual
+    before its add (emit_prev), writes 2^e_b after the partials, and the consumer folds it back in
+    (xscale). Rows with an old RMS below 8 keep e = 0 (bit-identical to the unscaled emission)."""
+    B, E, F = 5, 4096, 512
+    n = E // 16
+    mo = QMM(qt, E, E, seed=41)
+    mg = QMM(GGMLType.Q6_K, F, E, seed=42)
+    a = torch.randn(B, E, device="cuda")
+    mag = torch.tensor([1.0, 3e2, 4e3, 3e4, 9e4], device="cuda")[:, None]
+    resid = torch.randn(B, E, device="cuda") * mag
+    prev = torch.zeros(16 * n + 16, device="cuda")  # partials of the residual before the add
+    prev[:B * n] = resid.pow(2).reshape(B, n, 16).sum(-1).reshape(-1)
+    rms_old = resid.pow(2).mean(-1).sqrt()
+    nw = torch.rand(E, device="cuda") + 0.5
+    e16 = torch.zeros(B + 1, E, device="cuda", dtype=torch.float16)
+    st = torch.zeros(16 * n + 16, device="cuda")
+    gemv(mo, a, epi=1, y=resid, extra=dict(emit16=e16.data_ptr(), ld_emit=E, emit_nw=nw.data_ptr(),
+                                           emit_stat=st.data_ptr(), emit_prev=prev.data_ptr(), emit_prev_n=n,
+                                           emit_scale=st[16 * n:].data_ptr()))
+    torch.cuda.synchronize()
+    scale = st[16 * n:16 * n + B]
+    want = torch.clamp(torch.floor(torch.log2(rms_old)) - 2, 0, 30).exp2()
+    assert torch.equal(scale, want), (scale, want)
+    assert bool(torch.isfinite(e16[:B].float()).all())
+    assert rel(e16[:B].float() * scale[:, None], resid * nw) < 1e-3
+    y_chain = torch.zeros(B, F, device="cuda")
+    gemv(mg, resid, norm=1, nw=nw, y=y_chain, extra=dict(x16=e16.data_ptr(), ld16=E, zrow16=B, xstat=st.data_ptr(),
+                                                         xstat_n=n, xscale=st[16 * n:].data_ptr()))
+    y_lds = torch.zeros(B, F, device="cuda")
+    gemv(mg, resid, norm=1, nw=nw, y=y_lds)
+    for b in range(B):
+        assert rel(y_chain[b], y_lds[b]) < 2e-3, b
+
+
+def test_mb_engine_batched_decode_large_residual(tmp_path, monkeypatch):
+    """Engine level: a residual stream far past fp16's range (the token embeddings scaled by 1e7) decodes
+    a layout-M batch with finite logits that match the fp32-activation batch step."""
+    from ollama_operator_amd.engine.runner import Runner
+    from ollama_operator_amd.gguf.constants import FileType
+    from ollama_operator_amd.models.config import ModelConfig, preset
+    from ollama_operator_amd.models.random_init import write_random_gguf
+    p = str(tmp_path / "m.gguf")
+    write_random_gguf(p, preset("tiny-llama"), FileType.MOSTLY_Q4_0, seed=5)
+    monkeypatch.setattr(ModelConfig, "embed_scale", property(lambda self: 1e7))
+    g = Runner(p, device="cuda", max_batch=32, max_seqs=4, ctx=256)
+    assert g.exe.exe.mb_chain
+    B = 4
+    sids = []
+    for b in range(B):
+        sid = g.new_sequence()
+        g.prefill(sid, [1] + [3 + 7 * b + i for i in range(12)])
+        sids.append(sid)
+    V = g.cfg.n_vocab
+    outs = []
+    for on in (1, 0):
+        C().reset_launch_counts()
+        C().set_mb_enable(on)
+        try:
+            g.set_tokens(list(range(7, 7 + B)))
+            g.decode_batch(sids, [13] * B)
+            torch.cuda.synchronize()
+        finally:
+            C().set_mb_enable(1)
+        assert (C().launch_counts()["gemv_mb"] > 0) == bool(on)
+        outs.append(g.logits[:B, :V].float().cpu().clone())
+    assert float(g.resid[:B].abs().max()) > 1e5  # the rows did outgrow fp16
+    assert bool(torch.isfinite(outs[0]).all())
+    assert rel(outs[0], outs[1]) < 2e-2
