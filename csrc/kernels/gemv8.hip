@@ -160,7 +160,15 @@ bool geometry(const GemvParams& P, Geo& G) {
     G.J = (tiles + want - 1) / want;
     G.J = G.J < 1 ? 1 : G.J > 2 ? 2 : G.J;
     if (emit_mode(P) == EM_GLU) G.J = 2;  // a block owns whole groups (two tiles each)
-    if (G.nsb == 2 && G.J > 1) return false;
+    // two super-blocks per lane and two tiles: the GLU producer at 4096 < K <= 8192 only (Llama-2-13B
+    // gate_up, K = 5120), from the RMS image, at most 2 batch rows (launch_glu_nsb2)
+    if (G.nsb == 2 && G.J > 1) {
+      if (emit_mode(P) == EM_GLU) {
+        if (in_mode(P) != IN_X8_RMS || P.B > 2) return false;
+      } else {
+        G.J = 1;  // > 512 tiles: one tile per block still fills the chip (QKV at K = 5120: 960 blocks)
+      }
+    }
   }
   G.grid = (tiles + G.J - 1) / G.J;
   return true;
@@ -173,13 +181,16 @@ bool covered(const GemvParams& P, Geo& G) {
   if (P.B > 1 && in == IN_MERGE && P.merge_S > 0) return false;  // batched rows: plain fp32 attention rows
   if (!P.x8 && !P.emit8) return false;  // nothing for this path to do
   if (in == IN_MERGE && P.merge_S > 0 && !(P.merge_S == 2 || P.merge_S == 4 || P.merge_S == 8)) return false;
-  if (in == IN_MERGE && (P.w.K > 4096 * 1 || P.w.K % 16)) return false;  // merge prologue: one group per thread
+  if (in == IN_MERGE && P.w.K % 16) return false;
   if (in == IN_X8_RMS && (P.w.K > 8192 || P.w.K % 64)) return false;
   if (em == EM_ADD && (!P.emit8_nw || !P.emit8_stat || P.w.N % 16)) return false;
   if (em == EM_GLU && P.w.N % 32) return false;
   const int q = P.w.qtype;
   if (!(q == QT_Q4_K || q == QT_Q6_K || q == QT_Q4_0 || q == QT_Q8_0 || q == QT_Q5_K)) return false;
   if (!geometry(P, G)) return false;
+  // merge prologue: one 16-element group per thread and group slot (NSB slots); the deferred merge
+  // (merge_S > 1) exists for the unsplit geometry only
+  if (in == IN_MERGE && (P.w.K > GEMV_NT * G.ks * G.nsb * 16 || (P.merge_S > 1 && G.ks > 1))) return false;
   if (em == EM_GLU && G.J != 2) return false;  // a block owns whole groups: two tiles, unsplit K
   if (in != IN_MERGE && (size_t)G.ks * GEMV_NT * X8_NWI * 16 < x8_bytes(P.w.K)) return false;
   if (bt_of(P.B) >= 3 && !bt4_ok(q, G.ks, in)) return false;
@@ -225,7 +236,9 @@ void launch_in(const GemvParams& P, const Geo& G, hipStream_t s) {
   const int em = emit_mode(P), in = in_mode(P);
   if (in == IN_X8) launch_em<QT, NSB, J, KS, IN_X8, 0>(P, em, G.grid, s);
   else if (in == IN_X8_RMS) launch_em<QT, NSB, J, KS, IN_X8_RMS, 0>(P, em, G.grid, s);
-  else if constexpr (NSB == 1 && KS == 1 && J == 1) {  // the O projection: merge slabs or plain fp32
+  else if constexpr (NSB == 1 && KS == 2 && J == 1) {  // O at 4096 < K <= 8192: plain fp32 rows
+    launch_em<QT, 1, 1, 2, IN_MERGE, 1>(P, em, G.grid, s);
+  } else if constexpr (NSB == 1 && KS == 1 && J == 1) {  // the O projection: merge slabs or plain fp32
     switch (P.merge_S) {
       case 2: launch_em<QT, 1, 1, 1, IN_MERGE, 2>(P, em, G.grid, s); break;
       case 4: launch_em<QT, 1, 1, 1, IN_MERGE, 4>(P, em, G.grid, s); break;
@@ -236,8 +249,15 @@ void launch_in(const GemvParams& P, const Geo& G, hipStream_t s) {
 }
 
 template <int QT>
+void launch_glu_nsb2(const GemvParams& P, const Geo& G, hipStream_t s) {
+  if (bt_of(P.B) == 1) launch_k<QT, 2, 2, 1, IN_X8_RMS, 0, EM_GLU, 1>(P, G.grid, s);
+  else launch_k<QT, 2, 2, 1, IN_X8_RMS, 0, EM_GLU, 2>(P, G.grid, s);
+}
+
+template <int QT>
 void launch_q(const GemvParams& P, const Geo& G, hipStream_t s) {
-  if (G.ks == 1 && G.nsb == 1 && G.J == 1) launch_in<QT, 1, 1, 1>(P, G, s);
+  if (G.ks == 1 && G.nsb == 2 && G.J == 2) launch_glu_nsb2<QT>(P, G, s);
+  else if (G.ks == 1 && G.nsb == 1 && G.J == 1) launch_in<QT, 1, 1, 1>(P, G, s);
   else if (G.ks == 1 && G.nsb == 1) launch_in<QT, 1, 2, 1>(P, G, s);
   else if (G.ks == 1 && G.nsb == 2) launch_in<QT, 2, 1, 1>(P, G, s);
   else if (G.ks == 2) launch_in<QT, 1, 1, 2>(P, G, s);
@@ -246,8 +266,8 @@ void launch_q(const GemvParams& P, const Geo& G, hipStream_t s) {
 }
 
 bool launchable(const GemvParams& P, const Geo& G) {
-  // the merge / plain-fp32 input exists for the single-tile, unsplit geometry only
-  return in_mode(P) != IN_MERGE || (G.ks == 1 && G.nsb == 1 && G.J == 1);
+  // the merge / plain-fp32 input exists for single-tile blocks, unsplit or split in 2 (K <= 8192)
+  return in_mode(P) != IN_MERGE || (G.ks <= 2 && G.nsb == 1 && G.J == 1);
 }
 
 template <int QA, int QB, int IN, int BT>

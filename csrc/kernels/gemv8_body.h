@@ -161,7 +161,9 @@ __device__ __forceinline__ void gemv8_body(const GemvParams& P, const int bx) {
   epi_prefetch<EMIT, J, BT, PRE>(P, tile0, rbase, s, pre);
   u32x4 xw[BT][X8_NWI];
   f32x4 stv[BT][X8_NSTW];
-  constexpr int MG = IN == IN_MERGE ? NSB * KS : 1;  // groups per thread of the merge prologue
+  // groups per thread of the merge prologue: the block's NT = GEMV_NT * KS threads cover KS * 4096
+  // elements per group slot (O at K = 5120, Llama-2-13B, takes KS = 2)
+  constexpr int MG = IN == IN_MERGE ? NSB : 1;
   constexpr int MSS = MS > 0 ? MS : 1;
   constexpr int AR = BT > 1 ? BT : MSS;  // merge slabs (batch 1) or batch rows of plain fp32 input
   f32x4 av[AR][MG][4];

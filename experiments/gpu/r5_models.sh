@@ -5,11 +5,13 @@ set -o pipefail
 O=gpurun_out/r5_models
 mkdir -p $O
 export TMPDIR=/tmp
-for m in "mistral-7b Q4_0" "mixtral-8x7b Q4_K_M" "llama2-13b Q4_K_M" "gemma-7b Q4_0" "phi2 Q4_0" "gemma-2b Q4_0"; do
+T0=$SECONDS
+for m in "mistral-7b Q4_0" "llama2-13b Q4_K_M" "gemma-7b Q4_0" "phi2 Q4_0" "gemma-2b Q4_0" "mixtral-8x7b Q4_K_M"; do
   set -- $m
+  [ $((SECONDS - T0)) -lt 700 ] || { echo "skip $1: call time budget"; continue; }
   ( while sleep 60; do date > $O/heartbeat.txt; done ) &
   hb=$!
-  timeout -k 10 900 python -u bench.py --model $1 --ftype $2 --steps 64 --warmup 8 --prompt 512 --via-server 0 --batch-extra 4 --ttft-long 2048 --long-ctx "" > $O/bench_$1.log 2>&1; rc=$?
+  timeout -k 10 420 python -u bench.py --model $1 --ftype $2 --steps 64 --warmup 8 --prompt 512 --via-server 0 --batch-extra 4 --ttft-long 2048 --long-ctx "" > $O/bench_$1.log 2>&1; rc=$?
   kill $hb
   [ $rc -eq 0 ] || { tail -20 $O/bench_$1.log; exit 1; }
   echo "$1 $2: $(tail -1 $O/bench_$1.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); e=d["extra"]; print(d["value"], (e.get("continuous_batching") or {}).get("tokens_per_s"), e.get("ttft_ms"), e.get("ttft_2048_ms"))')"

@@ -355,3 +355,81 @@ def test_batched_rows_down_ks4(qd):
     nbE = C().x8_bytes(E)
     for b in range(B):
         assert rel(decode_image(out[b * nbE:(b + 1) * nbE], E), (resid[b] * nw2).cpu()) < 1e-2, (qd, b)
+
+
+@pytest.mark.parametrize("qt", [GGMLType.Q4_K, GGMLType.Q6_K, GGMLType.Q4_0])
+@pytest.mark.parametrize("B,K", [(1, 5120), (3, 5120), (4, 5120), (1, 8192), (2, 8192)])
+def test_plain_o_projection_k_split(qt, B, K):
+    """O projection on plain fp32 attention rows at 4096 < K <= 8192 (Llama-2-13B: H * D = 5120): the
+    quantising prologue over a block split in 2 wave groups. Before, such an O left the whole model off
+    the int8 chain (Llama-2-13B decoded on the fp32 GEMVs at 308 tok/s)."""
+    E = 5120
+    mo = QM(qt, E, K, seed=K + B)
+    a = torch.randn(B, K, device="cuda")
+    resid0 = torch.randn(B, E, device="cuda")
+    resid = resid0.clone()
+    nw = torch.rand(E, device="cuda") + 0.5
+    nbE, ld = C().x8_bytes(E), C().x8_stat_ld(E)
+    out = torch.zeros(B * nbE, dtype=torch.uint8, device="cuda")
+    sto = torch.zeros(B * ld + 4, device="cuda")
+    call(mo, B, a, resid, EPI_ADD, {"emit8": out.data_ptr(), "emit8_nw": nw.data_ptr(), "emit8_stat": sto.data_ptr()})
+    torch.cuda.synchronize()
+    assert rel(resid - resid0, a @ mo.w.T) < 1.5e-2
+    for b in range(B):
+        assert rel(decode_image(out[b * nbE:(b + 1) * nbE], E), (resid[b] * nw).cpu()) < 1e-2, b
+
+
+def test_engine_x8_chain_covers_13b_shapes(tmp_path):
+    """A 2-layer model with Llama-2-13B's widths (E = 5120, 40 heads, F = 13824) decodes on the int8
+    chain and matches the fp32 torch twin."""
+    from ollama_operator_amd.engine.runner import Runner
+    from ollama_operator_amd.gguf.constants import FileType
+    from ollama_operator_amd.models.config import preset
+    from ollama_operator_amd.models.random_init import write_random_gguf
+    import dataclasses
+    cfg = dataclasses.replace(preset("llama2-13b", ctx_len=256), n_layer=2, n_vocab=512)
+    p = str(tmp_path / "m.gguf")
+    write_random_gguf(p, cfg, FileType.MOSTLY_Q4_K_M, seed=3, quantize_from_float=True)
+    g = Runner(p, device="cuda:0", max_batch=64, max_seqs=1, ctx=256)
+    assert g.exe.exe.x8_on == 1
+    g.use_graphs = False  # launch counters count enqueues
+    c = Runner(p, device="cpu", max_batch=64, max_seqs=1, ctx=256, cpu_backend="torch")
+    prompt = [1] + [(11 * i + 3) % 500 for i in range(1, 20)]
+    sids = {id(r): r.new_sequence() for r in (g, c)}
+    for r in (g, c):
+        r.prefill(sids[id(r)], prompt)
+    V = g.cfg.n_vocab
+    for t in (5, 6):
+        C().reset_launch_counts()
+        g.set_tokens([t])
+        g.decode_step(sids[id(g)])
+        torch.cuda.synchronize()
+        n = C().launch_counts()
+        # every projection but layer 0's QKV (embedding rows, fp32 prologue) on the chain; the 512-row LM
+        # head may take either path
+        assert n["gemv8_row1"] + n["gemv8_dual"] >= 4 * 2 - 1 and n["gemv_flight"] <= 2, sorted(n.items())
+        g.kv.seqs[sids[id(g)]].tokens.append(t)
+        c.prefill(sids[id(c)], [t])
+        assert rel(g.logits[0, :V].float().cpu(), c.logits[0, :V]) < 3e-2
+
+
+@pytest.mark.parametrize("B", [1, 2])
+@pytest.mark.parametrize("qt", [GGMLType.Q4_K, GGMLType.Q4_0])
+def test_glu_producer_two_superblocks_per_lane(B, qt):
+    """gate_up at K = 5120 (Llama-2-13B): 1728 row tiles take two super-blocks per lane and two tiles
+    per block (NSB = 2, J = 2); h rows and down's images per row."""
+    E, F = 5120, 13824
+    x = torch.randn(B, E, device="cuda") * 2
+    nw = torch.rand(E, device="cuda") + 0.5
+    img, st = images(x, nw)
+    xn = x * torch.rsqrt(x.pow(2).mean(1, keepdim=True) + 1e-5) * nw
+    mg = QM(qt, 2 * F, E, seed=36 + B)
+    h = torch.zeros(B, F, device="cuda")
+    nbF = C().x8_bytes(F)
+    himg = torch.zeros(B * nbF, dtype=torch.uint8, device="cuda")
+    call(mg, B, None, h, EPI_GLU, {"x8": img.data_ptr(), "x8_stat": st.data_ptr(), "emit8": himg.data_ptr()})
+    torch.cuda.synchronize()
+    gu = xn @ mg.w.T
+    assert rel(h, torch.nn.functional.silu(gu[:, 0::2]) * gu[:, 1::2]) < 2e-2
+    for b in range(B):
+        assert rel(decode_image(himg[b * nbF:(b + 1) * nbF], F), h[b].cpu()) < 1e-2, b
