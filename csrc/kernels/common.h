@@ -122,6 +122,17 @@ __device__ __forceinline__ float block_max(float v, float* red) {
 // row (K padded), codes piece-major: piece t of super-block sb at byte (t * SB + sb) * piece_bytes.
 __device__ __forceinline__ int n_sb(int K) { return (K + 255) >> 8; }
 
+// super-blocks per group of an in-block K split over KS wave groups (<= 16 each). When a row's piece
+// run is a whole number of 128-B lines (SB % 8 == 0) the groups start on 16-super-block boundaries, so
+// each group's run starts on a line too (K = 10240 split 14 / 14 / 12: 3.3 TB/s memory path only,
+// 4.5 at 16 / 16 / 16, profiles/r5_decode align probe). Otherwise every row starts off a line anyway
+// and the split is balanced: Llama-2-13B's down (SB = 54) ran 16 / 16 / 16 / 6 aligned.
+__device__ __forceinline__ int ks_chunk(int SB, int KS) {
+  if (KS <= 1) return SB;
+  const int c = (SB + KS - 1) / KS;
+  return (SB & 7) ? c : (c + 15) & ~15;
+}
+
 // Dequantize piece p (= 8 * sb + t, natural order) of row `row` into two groups of 16 floats
 // (lo, hi) and their offsets (in weights) within the row. Used by the embedding gather and the fp16
 // dequant kernels (the GEMV decodes pieces itself, see gemv.hip).

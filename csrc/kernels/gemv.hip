@@ -200,7 +200,7 @@ __device__ __forceinline__ void flight_body(const GemvParams& P, const int bx, c
   // K-split groups start on 16-super-block boundaries: a group's piece runs then begin where the row's
   // piece run begins (SB = 43 split 15 / 15 / 13 put every run 240 B off: the down GEMVs streamed at
   // 3.3 TB/s memory-path-only vs 4.5 at 16 / 16 / 16, profiles/r5_decode align probe)
-  const int CH = KS > 1 ? ((SB + KS - 1) / KS + 15) & ~15 : SB;
+  const int CH = ks_chunk(SB, KS);
   const int sb0 = kg * CH, se = min(SB, sb0 + CH);
   const int n_tiles = (N + ROWS_B - 1) / ROWS_B;
   const int rbase = (wave - kg * GEMV_NW - jg * GEMV_NW) * (4 * R) + g * R;

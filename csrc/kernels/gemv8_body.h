@@ -146,10 +146,8 @@ __device__ __forceinline__ void gemv8_body(const GemvParams& P, const int bx) {
   float* part = stage + 32 * BT;                      // [KS - 1][BT][GEMV_NT] partial sums of the K split
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = lane >> 4, s = lane & 15;
   const int kg = KS > 1 ? wave / GEMV_NW : 0, gtid = tid - kg * GEMV_NT;
-  // K-split groups start on 16-super-block boundaries: a group's piece runs then begin where the row's
-  // piece run begins (SB = 43 split 15 / 15 / 13 put every run 240 B off: the down GEMVs streamed at
-  // 3.3 TB/s memory-path-only vs 4.5 at 16 / 16 / 16, profiles/r5_decode align probe)
-  const int CH = KS > 1 ? ((SB + KS - 1) / KS + 15) & ~15 : SB;
+  // K-split groups (ks_chunk): aligned to 16 super-blocks when the row stride keeps piece runs on lines
+  const int CH = ks_chunk(SB, KS);
   const int sb0 = kg * CH, se = min(SB, sb0 + CH);
   const int n_tiles = (N + 15) / 16;
   const int rbase = (wave - kg * GEMV_NW) * 4 + g;

@@ -330,10 +330,12 @@ def test_engine_batched_x8_chain_matches_single(tiny_models, B, monkeypatch):
 
 
 @pytest.mark.parametrize("qd", [GGMLType.Q4_0, GGMLType.Q4_K, GGMLType.Q6_K])
-def test_batched_rows_down_ks4(qd):
+@pytest.mark.parametrize("F", [14336, 13824])
+def test_batched_rows_down_ks4(qd, F):
     """2 batch rows on the residual producer at K = 14336 (Mistral-7B / Llama-3-8B down: 56 super-blocks,
-    the in-block K split over 4 wave groups, 1024-thread blocks)"""
-    B, E, F = 2, 4096, 14336
+    the in-block K split over 4 wave groups, 1024-thread blocks) and K = 13824 (Llama-2-13B: 54, the
+    balanced 14 / 14 / 14 / 12 split)"""
+    B, E = 2, 4096
     h = torch.randn(B, F, device="cuda")
     nbF = C().x8_bytes(F)
     himg = torch.zeros(B * nbF, dtype=torch.uint8, device="cuda")
