@@ -535,14 +535,28 @@ bool gemm_eligible(const GemvParams& P) {
 
 // Large-M library path (blas.cpp): dequantise W once into fp16 (in prep_x16's K order), one hipBLASLt
 // GEMM into the fp32 slab yws, then the fused epilogue as for split-K (finalize, one slab)
-static int g_lib_min_m = -1;  // -1: OMX_GEMM_LIB_MIN_M (default 0 = never; the hand-written dq GEMM runs), read once
+// -1: OMX_GEMM_LIB_MIN_M, read once. Default 2048: a 2048-row prefill chunk takes hipBLASLt (QKV, O,
+// down: 749 / 667 / 730-763 TFLOP/s against the dq kernel's 638 / 544 / 572-623, profiles/r5_gemm);
+// 2048-token TTFT 46.1 -> 42.4-43.2 ms (7B), 89.8 -> 72.8-73.3 (13B), profiles/r5_gemm lib_default/
+static int g_lib_min_m = -1;
+// OMX_GEMM_LIB_GLU (default 1): 0 keeps the gate_up GEMMs on the dq kernel (it wins the 7B shape per
+// call, 747 vs 690 TFLOP/s, but the 7B TTFT was a tie, 43.3 vs 43.2, and 13B lost 77.3 vs 73.3)
+static int g_lib_glu = -1;
 
 int gemm_lib_min_m() {
   if (g_lib_min_m < 0) {
     const char* e = getenv("OMX_GEMM_LIB_MIN_M");
-    g_lib_min_m = e ? atoi(e) : 0;
+    g_lib_min_m = e ? atoi(e) : 2048;
   }
   return g_lib_min_m;
+}
+
+static bool lib_glu() {
+  if (g_lib_glu < 0) {
+    const char* e = getenv("OMX_GEMM_LIB_GLU");
+    g_lib_glu = e ? atoi(e) : 1;
+  }
+  return g_lib_glu != 0;
 }
 
 void set_gemm_lib_min_m(int m) { g_lib_min_m = m; }
@@ -568,10 +582,12 @@ static bool gemm_lib(const GemvParams& P, const f16* x16, hipStream_t s) {
 
 void gemm(const GemvParams& P, hipStream_t s) {
   f16* x16 = (f16*)P.xws;
-  // hipBLASLt only when asked for (OMX_GEMM_LIB_MIN_M / set_gemm_lib_min_m: the test oracle and A/B
-  // baseline); from 128 rows the stream-order kernel (gemm_dq.hip), below that the 128 x 128 tile here
+  // hipBLASLt from gemm_lib_min_m() rows (the GLU matrices unless OMX_GEMM_LIB_GLU=0; always when the
+  // threshold is forced below 128: the test oracle); from 128 rows the stream-order kernel
+  // (gemm_dq.hip), below that the 128 x 128 tile here
   const int lm = gemm_lib_min_m();
-  const bool lib = lm > 0 && P.B >= lm;
+  const bool glu = P.epi == EPI_GLU || P.epi == EPI_GEGLU;
+  const bool lib = lm > 0 && P.B >= lm && (!glu || lib_glu() || lm < 128);
   if (lib) {
     hipLaunchKernelGGL(prep_x16_kernel, dim3(P.B), dim3(256), 0, s, P, x16);
     if (gemm_lib(P, x16, s)) {

@@ -261,11 +261,12 @@ class Runner:
         self._ext_next = 0
         # split-K partial slabs of small-M prefill GEMMs (the kernel picks splits that fit)
         self.gws = torch.zeros(GEMM_SPLIT_WS_FLOATS if str(dev).startswith("cuda") else 1, **f32)
-        # hipBLASLt prefill (gemm.hip gemm_lib), only when asked for (OMX_GEMM_LIB_MIN_M > 0: the A/B
-        # baseline of the hand-written stream-order GEMM, gemm_dq.hip): fp16 dequantised-weight scratch
-        # sized for the largest dense layer matrix and its fp32 output slab at max_batch rows
+        # hipBLASLt prefill (gemm.hip gemm_lib) for chunks of >= gemm_lib_min_m() rows (default 2048;
+        # OMX_GEMM_LIB_MIN_M, 0 = never): fp16 dequantised-weight scratch sized for the largest dense
+        # layer matrix and its fp32 output slab at max_batch rows
         self.w16 = self.yws = None
-        if self.is_gpu and native().gemm_lib_min_m() > 0 and max_batch >= 16:
+        lm = native().gemm_lib_min_m() if self.is_gpu else 0
+        if self.is_gpu and lm > 0 and max_batch >= max(16, lm):
             # expert stacks count per expert (DevQMat.N = rows of one expert): moe_gemm_lib
             mats = [v for L in self.w.layers for k, v in L.items() if isinstance(v, DevQMat) and k != "router"]
             if mats:
@@ -632,7 +633,7 @@ class Runner:
         # short prompts through the prefill path (GEMM + prep/finalize kernels resolved once); one per
         # hipBLASLt M bucket too -- a bucket's first GEMM also loads its kernel's code object (~0.1 s),
         # which must not land in a request's TTFT
-        lens = [min(self.max_batch, 32)]
+        lens = [min(self.max_batch, 32), min(self.max_batch, 128)]  # the tile and the dq GEMM paths
         if self.w16 is not None and native().gemm_lib_min_m() > 0:
             m = native().gemm_lib_min_m()
             while m <= min(self.max_batch, self.ctx - 1):  # every hipBLASLt M bucket (blas.cpp bucket_of)

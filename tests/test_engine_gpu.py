@@ -83,7 +83,7 @@ def test_prefill_dq_path_vs_torch(tiny_models, name):
     """Prompts >= 128 tokens take the stream-order dequant GEMM (gemm_dq.hip) for every dense matrix:
     logits must match the torch twin, before and after a decode step on the KV it wrote."""
     C = native()
-    assert C.dq_gemm_enabled() and C.gemm_lib_min_m() == 0
+    assert C.dq_gemm_enabled() and (C.gemm_lib_min_m() == 0 or C.gemm_lib_min_m() > 230)
     path = tiny_models[name]
     g = Runner(path, device="cuda", max_batch=256, max_seqs=2, ctx=256)
     c = Runner(path, device="cpu", max_batch=256, max_seqs=2, ctx=256)
