@@ -507,6 +507,7 @@ def main():
     served = None
     # resident weight bytes: the GGUF tensors (layout v2) plus the batched-decode layout M copies
     layout_m_gb = getattr(runner, "mfma_bytes", 0) / 1e9
+    prefill_f16_gb = getattr(runner, "f16_bytes", 0) / 1e9
     if server is not None:
         weights_gb = runner.w.nbytes / 1e9
         n_vocab = runner.cfg.n_vocab
@@ -543,7 +544,8 @@ def main():
             "extra": {"ttft_ms": round(ttft * 1e3, 2), f"ttft_{a.ttft_long}_ms": ttft_long, "prefill_chunk": a.chunk,
                       "load_s": round(load_s, 2),
                       "weights_gb": round(weights_gb, 3), "layout_m_gb": round(layout_m_gb, 3),
-                      "resident_weights_gb": round(weights_gb + layout_m_gb, 3),
+                      "prefill_f16_gb": round(prefill_f16_gb, 3),
+                      "resident_weights_gb": round(weights_gb + layout_m_gb + prefill_f16_gb, 3),
                       "long_context": long_res or None, "continuous_batching": batched, "server": served},
         }), flush=True)
     if world > 1:

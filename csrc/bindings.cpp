@@ -25,7 +25,8 @@ static QMat qmat(py::object o) {
   QMat m{};
   if (o.is_none()) return m;
   auto t = o.cast<py::tuple>();
-  if (t.size() < 7 || t.size() > 9) throw std::runtime_error("qmat tuple must be (s0, s1, s2, s3, N, K, qtype[, s4[, mt]])");
+  if (t.size() < 7 || t.size() > 10)
+    throw std::runtime_error("qmat tuple must be (s0, s1, s2, s3, N, K, qtype[, s4[, mt[, f16]]])");
   m.s0 = Pp<const uint8_t>(t[0].cast<uintptr_t>());
   m.s1 = Pp<const uint8_t>(t[1].cast<uintptr_t>());
   m.s2 = Pp<const uint8_t>(t[2].cast<uintptr_t>());
@@ -34,7 +35,8 @@ static QMat qmat(py::object o) {
   m.K = t[5].cast<int>();
   m.qtype = t[6].cast<int>();
   m.s4 = t.size() >= 8 ? Pp<const uint8_t>(t[7].cast<uintptr_t>()) : nullptr;
-  m.mt = t.size() == 9 ? Pp<const uint8_t>(t[8].cast<uintptr_t>()) : nullptr;
+  m.mt = t.size() >= 9 ? Pp<const uint8_t>(t[8].cast<uintptr_t>()) : nullptr;
+  m.f16 = t.size() == 10 ? Pp<const void>(t[9].cast<uintptr_t>()) : nullptr;
   if (m.s4 && m.qtype != QT_Q6_K) throw std::runtime_error("widened codes are for Q6_K only");
   if (m.qtype != QT_Q4_0 && m.qtype != QT_Q8_0 && m.qtype != QT_Q4_K && m.qtype != QT_Q5_K && m.qtype != QT_Q6_K &&
       m.qtype != QT_F16)

@@ -566,12 +566,15 @@ static bool gemm_lib(const GemvParams& P, const f16* x16, hipStream_t s) {
   const long long M = P.B, N = P.w.N, K = P.w.K;
   // M >= lm (256). Taking the wide QKV / gate_up matrices from 128 rows (where the library GEMM wins
   // per call, 66 -> 60 / 109 -> 90 us) left the 128-token TTFT unchanged (11.3 vs 12.3 ms), so no
-  if (lm <= 0 || M < lm || !P.w16ws || !P.yws || N * K > P.w16_elems || M * N > P.yws_elems) return false;
+  // a resident fp16 copy (QMat.f16, runner OMX_PREFILL_F16) skips the per-call dequantisation
+  const bool res = P.w.f16 != nullptr;
+  if (lm <= 0 || M < lm || !P.yws || M * N > P.yws_elems) return false;
+  if (!res && (!P.w16ws || N * K > P.w16_elems)) return false;
   const long long xcap = P.xws_elems ? P.xws_elems / K : M, ycap = P.yws_elems / N;
   const int m_cap = (int)(xcap < ycap ? xcap : ycap);
   if (!blas_plan_ok((int)M, (int)N, (int)K, P.gws ? (size_t)P.gws_elems * 4 : 0, m_cap)) return false;
-  dequant_f16(P.w, P.w16ws, s, 1);
-  if (!blas_gemm_tn(P.w16ws, x16, P.yws, (int)M, (int)N, (int)K, P.gws, P.gws ? (size_t)P.gws_elems * 4 : 0, s,
+  if (!res) dequant_f16(P.w, P.w16ws, s, 1);
+  if (!blas_gemm_tn(res ? P.w.f16 : P.w16ws, x16, P.yws, (int)M, (int)N, (int)K, P.gws, P.gws ? (size_t)P.gws_elems * 4 : 0, s,
                     m_cap))
     throw std::runtime_error("gemm_lib: hipBLASLt matmul failed after its plan was accepted");
   GemvParams F = P;

@@ -178,6 +178,15 @@ class Runner:
         self.mfma_bytes = 0
         if self.is_gpu and max_seqs > 1 and os.environ.get("OMX_MFMA_BATCH", "1") != "0":
             self.mfma_bytes = self.w.build_mfma_layouts()
+        # long prefill chunks (>= gemm_lib_min_m rows) on hipBLASLt: resident fp16 weight copies skip the
+        # per-call dequantisation (7B: 13.5 GB of the 288 GB HBM), when they take at most half the free
+        # memory; OMX_PREFILL_F16=0 keeps the per-call path
+        self.f16_bytes = 0
+        if self.is_gpu and os.environ.get("OMX_PREFILL_F16", "1") != "0":
+            lm = native().gemm_lib_min_m()
+            if lm > 0 and max_batch >= lm:
+                free = torch.cuda.mem_get_info(self.device)[0]
+                self.f16_bytes = self.w.build_f16_copies(free // 2)
         cfg = self.cfg = self.w.cfg
         loc = self.w.local
         self.max_batch = max_batch

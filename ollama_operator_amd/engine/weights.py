@@ -43,14 +43,28 @@ class DevQMat:
     wide: torch.Tensor | None = None
     # GPU, continuous batching: layout M copy for the matrix-core batched decode GEMV (gemv_mfma.hip)
     mt: torch.Tensor | None = None
+    # GPU, long prefill chunks: resident fp16 copy for the library GEMM (gemm.hip gemm_lib)
+    f16: torch.Tensor | None = None
 
     @property
     def tup(self) -> tuple:
         p = [s.data_ptr() for s in self.streams] + [0] * (4 - len(self.streams))
         t = (p[0], p[1], p[2], p[3], self.N, self.K, int(self.qtype))
+        wide = self.wide.data_ptr() if self.wide is not None else 0
+        if self.f16 is not None:
+            return t + (wide, self.mt.data_ptr() if self.mt is not None else 0, self.f16.data_ptr())
         if self.mt is not None:
-            return t + (self.wide.data_ptr() if self.wide is not None else 0, self.mt.data_ptr())
-        return t + (self.wide.data_ptr(),) if self.wide is not None else t
+            return t + (wide, self.mt.data_ptr())
+        return t + (wide,) if self.wide is not None else t
+
+    def build_f16(self) -> int:
+        """Resident fp16 copy in the prefill GEMM's K order (dequant_f16 perm = 1); returns its bytes."""
+        from ..ops import native, stream_handle
+        if self.f16 is None:
+            self.f16 = torch.empty(self.N * self.K, dtype=torch.float16, device=self.streams[0].device)
+            native().dequant_f16(self.tup[:7] + ((self.wide.data_ptr(),) if self.wide is not None else ()),
+                                 self.f16.data_ptr(), stream_handle(), 1)
+        return self.f16.numel() * 2
 
     def build_mfma_layout(self) -> int:
         """Layout M copy (gemv_mfma.hip `repack_m`, built on the device from the v2 streams) for the
@@ -319,6 +333,17 @@ class DeviceWeights:
                 if isinstance(v, DevQMat) and k not in ("gu_exps", "down_exps"):
                     n += v.build_mfma_layout()
         return n
+
+    def build_f16_copies(self, budget: int) -> int:
+        """Resident fp16 copies of every dense layer projection for the library prefill GEMM, if they
+        fit in `budget` bytes (else none). MoE expert stacks and the LM head keep the per-call path.
+        Returns the bytes added."""
+        mats = [v for L in self.layers for k, v in L.items()
+                if isinstance(v, DevQMat) and k not in ("gu_exps", "down_exps", "router")]
+        need = sum(v.N * v.K * 2 for v in mats if v.f16 is None)
+        if need > budget:
+            return 0
+        return sum(v.build_f16() for v in mats)
 
     @property
     def nbytes(self) -> int:

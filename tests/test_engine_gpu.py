@@ -103,10 +103,12 @@ def test_prefill_dq_path_vs_torch(tiny_models, name):
 
 
 @pytest.mark.parametrize("name", ["tiny-llama", "tiny-mixtral", "tiny-gemma", "tiny-phi2"])
-def test_prefill_library_path_vs_torch(tiny_models, name):
+def test_prefill_library_path_vs_torch(tiny_models, name, monkeypatch):
     """The hipBLASLt prefill path (gemm.hip gemm_lib; for Mixtral per-expert GEMMs over the sorted
     rows with the GLU / routing-weighted scatter epilogues, moe_gemm_lib) forced from 16 rows: logits
-    must match the torch twin, and the dequantised-weight scratch must have been used."""
+    must match the torch twin, and the dequantised-weight scratch must have been used (per-call
+    dequantisation: no resident fp16 copies)."""
+    monkeypatch.setenv("OMX_PREFILL_F16", "0")
     C = native()
     old = C.gemm_lib_min_m()
     C.set_gemm_lib_min_m(16)
@@ -307,3 +309,31 @@ def test_admit_many_gpu_matches_sequential(tiny_models, name):
     torch.cuda.synchronize()
     for i, lg in enumerate(ref):
         assert rel(g.logits[i, :V].float().cpu(), lg) < 2e-2, i
+
+
+@pytest.mark.parametrize("name", ["tiny-llama", "tiny-gemma", "tiny-llama-q40"])
+def test_prefill_library_resident_f16(tiny_models, name):
+    """Resident fp16 weight copies (OMX_PREFILL_F16, default on): the library prefill GEMM reads them
+    and never touches the per-call dequantisation scratch; logits match the torch twin."""
+    C = native()
+    old = C.gemm_lib_min_m()
+    C.set_gemm_lib_min_m(16)
+    try:
+        path = tiny_models[name]
+        g = Runner(path, device="cuda", max_batch=128, max_seqs=2, ctx=160)
+        c = Runner(path, device="cpu", max_batch=64, max_seqs=2, ctx=160)
+        assert g.f16_bytes > 0
+        g.w16.fill_(float("nan"))
+        rng = np.random.default_rng(3)
+        toks = [1] + [int(x) for x in rng.integers(3, 500, 69)]
+        sg, sc = g.new_sequence(), c.new_sequence()
+        C.reset_launch_counts()
+        g.prefill(sg, toks)
+        torch.cuda.synchronize()
+        assert C.launch_counts()["gemm_lib"] >= 2 * g.cfg.n_layer
+        assert torch.isnan(g.w16).all()  # the scratch stayed unused
+        c.prefill(sc, toks)
+        V = g.cfg.n_vocab
+        assert rel(g.logits[0, :V].cpu(), c.logits[0, :V]) < 3e-2
+    finally:
+        C.set_gemm_lib_min_m(old)
