@@ -304,6 +304,7 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("set_gemm_lib_min_m", &set_gemm_lib_min_m, "prefill rows from which the hipBLASLt path runs (0 = off)");
   m.def("gemm_lib_min_m", &gemm_lib_min_m);
+  m.def("gemm_lib_min_m_res", &gemm_lib_min_m_res);
   m.def("set_dq_gemm", &set_dq_gemm, "1: prefill GEMMs from 128 rows on the stream-order dequant kernel (gemm_dq.hip)");
   m.def("set_dq_tuning", &set_dq_tuning, "microbenchmarks: force the dq GEMM tile config (0..3, -1 auto) and split-K factor (0 auto)");
   m.def("dq_gemm_enabled", &dq_gemm_enabled);

@@ -551,6 +551,25 @@ int gemm_lib_min_m() {
   return g_lib_min_m;
 }
 
+// with a resident fp16 copy (no per-call dequantisation) the library path starts at 512 rows
+// (OMX_GEMM_LIB_MIN_M_F16): 7B TTFT 17.2 -> 15.0 ms at 512 tokens, 26.3 -> 20.0 at 1024
+// (profiles/r5_gemm/lib_default/bench_lib*_p*.log)
+static int g_lib_min_m_res = -1;
+
+int gemm_lib_min_m_res() {
+  if (g_lib_min_m_res < 0) {
+    const char* e = getenv("OMX_GEMM_LIB_MIN_M_F16");
+    g_lib_min_m_res = e ? atoi(e) : 512;
+  }
+  return g_lib_min_m_res;
+}
+
+// rows from which this matrix's prefill GEMM takes hipBLASLt (0 = never)
+static int lib_min_for(const QMat& w) {
+  const int lm = gemm_lib_min_m();
+  return lm > 0 && w.f16 ? std::min(lm, gemm_lib_min_m_res()) : lm;
+}
+
 static bool lib_glu() {
   if (g_lib_glu < 0) {
     const char* e = getenv("OMX_GEMM_LIB_GLU");
@@ -562,7 +581,7 @@ static bool lib_glu() {
 void set_gemm_lib_min_m(int m) { g_lib_min_m = m; }
 
 static bool gemm_lib(const GemvParams& P, const f16* x16, hipStream_t s) {
-  const int lm = gemm_lib_min_m();
+  const int lm = lib_min_for(P.w);
   const long long M = P.B, N = P.w.N, K = P.w.K;
   // M >= lm (256). Taking the wide QKV / gate_up matrices from 128 rows (where the library GEMM wins
   // per call, 66 -> 60 / 109 -> 90 us) left the 128-token TTFT unchanged (11.3 vs 12.3 ms), so no
@@ -588,7 +607,7 @@ void gemm(const GemvParams& P, hipStream_t s) {
   // hipBLASLt from gemm_lib_min_m() rows (the GLU matrices unless OMX_GEMM_LIB_GLU=0; always when the
   // threshold is forced below 128: the test oracle); from 128 rows the stream-order kernel
   // (gemm_dq.hip), below that the 128 x 128 tile here
-  const int lm = gemm_lib_min_m();
+  const int lm = lib_min_for(P.w);
   const bool glu = P.epi == EPI_GLU || P.epi == EPI_GEGLU;
   const bool lib = lm > 0 && P.B >= lm && (!glu || lib_glu() || lm < 128);
   if (lib) {

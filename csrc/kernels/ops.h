@@ -147,6 +147,8 @@ constexpr int GEMM_MIN_B = 16;
 // prefill rows from which the library GEMM path is taken (0 = never); OMX_GEMM_LIB_MIN_M overrides
 void set_gemm_lib_min_m(int m);
 int gemm_lib_min_m();
+// the same for matrices with a resident fp16 copy (QMat.f16): min(gemm_lib_min_m(), this)
+int gemm_lib_min_m_res();
 // D[M][N] (fp32, row-major) = X[M][K] . W[N][K]^T, X and W fp16 row-major, on hipBLASLt; false when
 // no algorithm fits (the caller falls back)
 // m_cap: rows of x16 / d the buffers hold (>= M); when the M-bucket's algorithm does not accept M

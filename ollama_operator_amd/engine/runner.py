@@ -182,11 +182,13 @@ class Runner:
         # per-call dequantisation (7B: 13.5 GB of the 288 GB HBM), when they take at most half the free
         # memory; OMX_PREFILL_F16=0 keeps the per-call path
         self.f16_bytes = 0
-        if self.is_gpu and os.environ.get("OMX_PREFILL_F16", "1") != "0":
-            lm = native().gemm_lib_min_m()
-            if lm > 0 and max_batch >= lm:
-                free = torch.cuda.mem_get_info(self.device)[0]
-                self.f16_bytes = self.w.build_f16_copies(free // 2)
+        lm = native().gemm_lib_min_m() if self.is_gpu else 0
+        lm_res = min(lm, native().gemm_lib_min_m_res()) if lm > 0 else 0
+        if self.is_gpu and os.environ.get("OMX_PREFILL_F16", "1") != "0" and lm_res > 0 and max_batch >= lm_res:
+            free = torch.cuda.mem_get_info(self.device)[0]
+            self.f16_bytes = self.w.build_f16_copies(free // 2)
+        # rows from which prefill chunks take hipBLASLt (gemm.hip lib_min_for; 0 = never)
+        self.lib_min = lm_res if self.f16_bytes else lm
         cfg = self.cfg = self.w.cfg
         loc = self.w.local
         self.max_batch = max_batch
@@ -274,8 +276,7 @@ class Runner:
         # OMX_GEMM_LIB_MIN_M, 0 = never): fp16 dequantised-weight scratch sized for the largest dense
         # layer matrix and its fp32 output slab at max_batch rows
         self.w16 = self.yws = None
-        lm = native().gemm_lib_min_m() if self.is_gpu else 0
-        if self.is_gpu and lm > 0 and max_batch >= max(16, lm):
+        if self.is_gpu and self.lib_min > 0 and max_batch >= max(16, self.lib_min):
             # expert stacks count per expert (DevQMat.N = rows of one expert): moe_gemm_lib
             mats = [v for L in self.w.layers for k, v in L.items() if isinstance(v, DevQMat) and k != "router"]
             if mats:
@@ -632,7 +633,7 @@ class Runner:
             return
         if self.w16 is not None:  # hipBLASLt plans for the long-prefill path (gemm.hip gemm_lib)
             C = native()
-            lm = C.gemm_lib_min_m()
+            lm = self.lib_min
             if lm > 0 and self.max_batch >= lm:
                 shapes = {(v.N, v.K) for L in self.w.layers for k, v in L.items()
                           if isinstance(v, DevQMat) and k != "router"}
@@ -643,8 +644,8 @@ class Runner:
         # hipBLASLt M bucket too -- a bucket's first GEMM also loads its kernel's code object (~0.1 s),
         # which must not land in a request's TTFT
         lens = [min(self.max_batch, 32), min(self.max_batch, 128)]  # the tile and the dq GEMM paths
-        if self.w16 is not None and native().gemm_lib_min_m() > 0:
-            m = native().gemm_lib_min_m()
+        if self.w16 is not None and self.lib_min > 0:
+            m = self.lib_min
             while m <= min(self.max_batch, self.ctx - 1):  # every hipBLASLt M bucket (blas.cpp bucket_of)
                 lens.append(m)
                 m = m * 2 if m < 256 else m + 256
@@ -659,7 +660,7 @@ class Runner:
         # batched admission once with a row count off the power-of-two buckets (admit_many rows,
         # hipBLASLt's algorithm check for an exact M): the first call of that check costs ~0.3 s,
         # which the first burst of concurrent requests would otherwise pay
-        lm = native().gemm_lib_min_m()
+        lm = self.lib_min
         n_each = max(67, lm // 2 + 3) if self.w16 is not None and lm > 0 else 67
         if len(self.kv.rows_free) >= 2 and self.max_batch >= 2 * n_each and self.ctx > n_each:
             sids = [self.new_sequence(), self.new_sequence()]
