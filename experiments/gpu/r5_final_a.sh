@@ -1,7 +1,7 @@
 #!/bin/bash
 # round 5 rehearsal, part A: the full GPU test suite and smoke() on the final tree
 set -o pipefail
-O=gpurun_out/r5_final
+O=gpurun_out/${FINAL_DIR:-r5_final}
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1; rc=$?

@@ -2,7 +2,7 @@
 # round 5 rehearsal, part B: the driver's bench lines on the final tree -- default (256 steps, every extra)
 # and 20 steps
 set -o pipefail
-O=gpurun_out/r5_final
+O=gpurun_out/${FINAL_DIR:-r5_final}
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 900 python -u bench.py > $O/bench_default.log 2>&1 || { tail -20 $O/bench_default.log; exit 1; }

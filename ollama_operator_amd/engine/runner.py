@@ -677,6 +677,13 @@ class Runner:
                 self._graph(1)
             self._decode_S = 0
         torch.cuda.synchronize()
+        # the objects alive after load (torch, the model, graphs) move to the permanent generation: a
+        # full collection no longer walks them, so one cannot land as a multi-ms pause inside a decode
+        # stream (the 256-step engine bench varied 666-698 tok/s while the served stream of the same
+        # run held 700-713)
+        if os.environ.get("OMX_GC_FREEZE", "1") != "0":
+            gc.collect()
+            gc.freeze()
 
     def decode_step(self, sid: int, pos: int | None = None) -> None:
         """One token for sequence `sid` whose input token (not yet in `tokens`) is already in
