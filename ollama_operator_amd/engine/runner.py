@@ -318,6 +318,7 @@ class Runner:
         # decode_ctx2048 593 -> 602 tok/s, profiles/r5_decode) or the on-device split rule with the
         # in-launch ticket merge (0; always past 4096 keys)
         self.defer_long = os.environ.get("OMX_DEFER_LONG", "1") != "0"
+        self.defer_max_s = int(os.environ.get("OMX_DEFER_MAX_S", "8"))  # 2, 4 or 8 deferred splits at most
         self._defer_ok = (self.is_gpu and os.environ.get("OMX_DEFER_MERGE", "1") != "0" and
                           native().gemv_merge_supported(1, Eq, loc["D"], 8) and self.n_splits(1) >= 8)
         self._decode_S = 0
@@ -394,7 +395,7 @@ class Runner:
         if not self._defer_ok:
             return 0
         S = 1
-        while S < 8 and length > S * self.defer_kps:
+        while S < self.defer_max_s and length > S * self.defer_kps:
             S *= 2
         return S if length <= S * self.defer_kps or (self.defer_long and length <= 8 * 512) else 0
 
