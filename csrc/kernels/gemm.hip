@@ -551,15 +551,16 @@ int gemm_lib_min_m() {
   return g_lib_min_m;
 }
 
-// with a resident fp16 copy (no per-call dequantisation) the library path starts at 512 rows
-// (OMX_GEMM_LIB_MIN_M_F16): 7B TTFT 17.2 -> 15.0 ms at 512 tokens, 26.3 -> 20.0 at 1024
-// (profiles/r5_gemm/lib_default/bench_lib*_p*.log)
+// with a resident fp16 copy (no per-call dequantisation) the library path starts at 128 rows
+// (OMX_GEMM_LIB_MIN_M_F16): 7B TTFT 17.2 -> 15.0 ms at 512 tokens, 26.3 -> 20.0 at 1024, and from 128
+// instead of 512 rows 10.1 -> 9.3 ms at 128 tokens, 11.8-12.3 -> 11.0-11.1 at 256
+// (profiles/r5_gemm/lib_default/threshold/)
 static int g_lib_min_m_res = -1;
 
 int gemm_lib_min_m_res() {
   if (g_lib_min_m_res < 0) {
     const char* e = getenv("OMX_GEMM_LIB_MIN_M_F16");
-    g_lib_min_m_res = e ? atoi(e) : 512;
+    g_lib_min_m_res = e ? atoi(e) : 128;
   }
   return g_lib_min_m_res;
 }

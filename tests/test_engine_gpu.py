@@ -79,9 +79,11 @@ def test_prefill_gemm_path_vs_torch(tiny_models, name):
 
 @pytest.mark.parametrize("name", ["tiny-llama", "tiny-mixtral", "tiny-phi2", "tiny-llama-q8", "tiny-llama-q40",
                                   "tiny-llama-q5km", "tiny-gemma", "tiny-orca"])
-def test_prefill_dq_path_vs_torch(tiny_models, name):
-    """Prompts >= 128 tokens take the stream-order dequant GEMM (gemm_dq.hip) for every dense matrix:
+def test_prefill_dq_path_vs_torch(tiny_models, name, monkeypatch):
+    """Prompts >= 128 tokens take the stream-order dequant GEMM (gemm_dq.hip) for every dense matrix when
+    no resident fp16 copies exist (OMX_PREFILL_F16=0; with them the library path takes >= 128 rows):
     logits must match the torch twin, before and after a decode step on the KV it wrote."""
+    monkeypatch.setenv("OMX_PREFILL_F16", "0")
     C = native()
     assert C.dq_gemm_enabled() and (C.gemm_lib_min_m() == 0 or C.gemm_lib_min_m() > 230)
     path = tiny_models[name]
