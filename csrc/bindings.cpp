@@ -230,6 +230,8 @@ PYBIND11_MODULE(_C, m) {
     P.emit_prev_n = ii("emit_prev_n");
     P.emit_scale = Pp<float>(ip("emit_scale"));
     P.xscale = Pp<const float>(ip("xscale"));
+    P.rexp_out = Pp<float>(ip("rexp_out"));
+    P.rexp_in = Pp<const float>(ip("rexp_in"));
     P.y16 = Pp<void>(ip("y16"));
     P.ld16y = ii("ld16y");
     if ((P.x16 || P.emit16 || P.y16) && !gemv_mb_supported(P))

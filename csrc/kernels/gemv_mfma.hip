@@ -505,6 +505,7 @@ __device__ __forceinline__ void mb_body(const GemvParams& P, const int bx, const
   const bool av = j < B;         // A-operand lane: batch row j
   const bool rs = G16 && P.xstat != nullptr && !(DBG & 2);
   const bool es = P.emit16 != nullptr && P.emit_prev != nullptr;  // emission range scale (never with rs)
+  const bool er = P.emit16 != nullptr && P.rexp_in != nullptr && !es;  // the same, exponents precomputed
   const float* sx = rs ? P.xstat : P.emit_prev;
   const int sxn = rs ? P.xstat_n : P.emit_prev_n;
 
@@ -570,6 +571,7 @@ __device__ __forceinline__ void mb_body(const GemvParams& P, const int bx, const
 #pragma unroll
         for (int i = 0; i < MB_NW; ++i) t += stat[i * 16 + tid];
         srstd[tid] = rsqrtf(t / K + P.eps);
+        if (P.rexp_out && bx == 0) P.rexp_out[tid] = (float)emit_range_exp(t / K);
       }
       __syncthreads();
     }
@@ -628,6 +630,7 @@ __device__ __forceinline__ void mb_body(const GemvParams& P, const int bx, const
       if (lane == 0 && b < B) {
         if (rs) {
           srstd[b] = rsqrtf(s / K + P.eps) * (P.xscale ? P.xscale[b] : 1.f);
+          if (P.rexp_out && bx == 0) P.rexp_out[b] = (float)emit_range_exp(s / K);
         } else {
           const int e = emit_range_exp(s / N);
           srstd[b] = __builtin_ldexpf(1.f, -e);
@@ -636,7 +639,12 @@ __device__ __forceinline__ void mb_body(const GemvParams& P, const int bx, const
       }
     }
   }
-  if (!es && P.emit16 && P.emit_scale && bx == 0 && tid < B) P.emit_scale[tid] = 1.f;
+  if (er && tid < B) {
+    const int e = (int)P.rexp_in[tid];
+    srstd[tid] = __builtin_ldexpf(1.f, -e);
+    if (bx == 0 && P.emit_scale) P.emit_scale[tid] = __builtin_ldexpf(1.f, e);
+  }
+  if (!es && !er && P.emit16 && P.emit_scale && bx == 0 && tid < B) P.emit_scale[tid] = 1.f;
   // staged rows and srstd visible to every wave
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 
@@ -664,7 +672,7 @@ __device__ __forceinline__ void mb_body(const GemvParams& P, const int bx, const
         if (P.bias) x += eo[1];
         const float nv = eo[0] + x;
         P.y[(long long)b * P.ldy + vn] = nv;
-        const float c = es ? srstd[b] : 1.f;  // range scale 2^-e of the emitted row (exact)
+        const float c = es || er ? srstd[b] : 1.f;  // range scale 2^-e of the emitted row (exact)
         ((f16*)P.emit16)[(long long)b * P.ld_emit + vn] = (f16)(nv * eo[3] * c);
         sq = nv * nv;
       }

@@ -93,6 +93,10 @@ struct GemvParams {
   int emit_prev_n;
   float* emit_scale;
   const float* xscale;
+  // cheaper form used by the engine: the consumer that reduces the old row's partials for its RMSNorm
+  // anyway (QKV, gate_up) writes e_b to rexp_out[b]; the producer reads rexp_in[b] instead of emit_prev
+  float* rexp_out;
+  const float* rexp_in;
   void* y16;                   // EPI_GLU / EPI_GEGLU: fp16 output [B][ld16y] instead of y
   int ld16y;
   // batch-1 int8 activation chain (gemv8.hip): the producer of a GEMV's input writes it already

@@ -34,8 +34,8 @@ bool Executor::chain(const StepInputs& in) const {
          cfg.n_expert == 0 && ws.xa16 && ws.h16 && ws.a16 && ws.st[0] && ws.st[1];
 }
 
-// a partial slab st[0] / st[1] is [16][n] sum-of-squares partials followed by 16 row scales 2^e (the
-// emission range guard, gemv_mfma.hip emit_range_exp); the runner sizes it 16 * n + 16 floats
+// a partial slab st[0] / st[1] is [16][n] sum-of-squares partials, 16 row scales 2^e (the emission range
+// guard, gemv_mfma.hip emit_range_exp) and 16 range exponents for the next producer; 16 * n + 32 floats
 static void chain_in(GemvParams& P, const void* x16, int ld16, const float* xstat, int n_stat) {
   P.x16 = x16;
   P.ld16 = ld16;
@@ -174,6 +174,7 @@ void Executor::attn_block(int i, const StepInputs& in, hipStream_t s) {
   const bool ch = chain(in);
   const bool q8 = x8(in);
   if (ch && i > 0) chain_in(P, ws.xa16, ws.ld_e, ws.st[1], (E + 15) / 16);  // emitted by layer i-1's down
+  if (ch) P.rexp_out = ws.st[1] + 16 * ((E + 15) / 16) + 16;  // O's range exponents (layer 0: from resid)
   if (q8 && i > 0) x8_in(P, ws.x8e, ws.x8st);                                 // emitted by layer i-1's down
   if (q8 && i > 0 && B == 1 && ws.attn_fuse == 2 && ws.x8q && !phi) {
     // QKV + attention in one launch (qkv_attn.hip): the attention lands as O's int8 image
@@ -350,8 +351,9 @@ void Executor::attn_block(int i, const StepInputs& in, hipStream_t s) {
   O.ldy = E;
   if (ch) {
     chain_in(O, ws.a16, ws.ld_q, nullptr, 0);
-    // the residual before O: its partials are in st[1] (layer i - 1's down emission, or the embedding's)
-    chain_emit(O, ws.xa16, ws.ld_e, L.ffn_norm, ws.st[0], ws.st[1]);  // gate_up's RMSNorm input
+    // range exponents of the residual before O: written by this layer's QKV (st[1] + 16 n + 16)
+    chain_emit(O, ws.xa16, ws.ld_e, L.ffn_norm, ws.st[0], nullptr);  // gate_up's RMSNorm input
+    O.rexp_in = ws.st[1] + 16 * ((E + 15) / 16) + 16;
   }
   if (q8 && cfg.tp == 1) x8_emit(O, ws.x8e, L.ffn_norm, ws.x8st);  // gate_up's RMSNorm input, int8
   gemv(O, s);
@@ -469,6 +471,7 @@ void Executor::ffn_block(int i, const StepInputs& in, hipStream_t s) {
   G.ldy = F;
   if (ch) {
     chain_in(G, ws.xa16, ws.ld_e, ws.st[0], (E + 15) / 16);
+    G.rexp_out = ws.st[0] + 16 * ((E + 15) / 16) + 16;  // down's range exponents
     G.y16 = ws.h16;
     G.ld16y = ws.ld_f;
   }
@@ -483,7 +486,8 @@ void Executor::ffn_block(int i, const StepInputs& in, hipStream_t s) {
   if (ch) {  // the next RMSNorm'd GEMV: layer i+1's QKV, or the LM head
     chain_in(Dn, ws.h16, ws.ld_f, nullptr, 0);
     chain_emit(Dn, ws.xa16, ws.ld_e, i + 1 < (int)layers.size() ? layers[i + 1].attn_norm : out_norm, ws.st[1],
-               ws.st[0]);
+               nullptr);
+    Dn.rexp_in = ws.st[0] + 16 * ((E + 15) / 16) + 16;  // written by this layer's gate_up
   }
   if (q8 && cfg.tp > 1) {
     x8_in(Dn, ws.x8f, nullptr);  // partial sums to the slab: the all-reduce emits the next image

@@ -236,8 +236,8 @@ class Runner:
             r256 = lambda n: (n + 255) // 256 * 256  # noqa: E731
             h16 = dict(device=dev, dtype=torch.float16)
             self.mb_bufs = dict(xa16=torch.zeros(17, r256(E), **h16), h16=torch.zeros(17, r256(Fl), **h16),
-                                a16=torch.zeros(17, r256(Eq), **h16), st0=torch.zeros((E + 15) // 16 * 16 + 16, **f32),
-                                st1=torch.zeros((E + 15) // 16 * 16 + 16, **f32))
+                                a16=torch.zeros(17, r256(Eq), **h16), st0=torch.zeros((E + 15) // 16 * 16 + 32, **f32),
+                                st1=torch.zeros((E + 15) // 16 * 16 + 32, **f32))
         # batch-1 int8 activation chain (csrc/kernels/gemv8.hip): zeroed images (pad slots stay zero)
         self.x8_bufs = None
         self.attn_fuse = False
