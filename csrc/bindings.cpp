@@ -313,7 +313,7 @@ PYBIND11_MODULE(_C, m) {
   // launch counters (ops.h LC_*): tests assert which kernel family a call enqueued
   m.def("launch_counts", []() {
     static const char* names[LC_N] = {"dq_gemm", "gemm_tile", "gemm_lib", "gemv8_row1", "gemv8_rows", "gemv8_dual",
-                                      "gemv_mb", "gemv_flight", "attn_decode", "attn_prefill", "qkv_attn", "attn_o", "mall_prefetch"};
+                                      "gemv_mb", "gemv_flight", "attn_decode", "attn_prefill"};
     py::dict d;
     for (int i = 0; i < LC_N; ++i) d[names[i]] = launch_count(i);
     return d;
@@ -359,32 +359,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("mfma_layout_bytes", &mfma_layout_bytes);
   m.def("x8_bytes", [](int K) { return x8_bytes(K); });
   m.def("x8_stat_ld", [](int K) { return x8_stat_ld(K); });
-  m.def("gemv8_ffn", [](py::object wg, py::object wd, uintptr_t img_in, uintptr_t stat, uintptr_t img_f, uintptr_t h,
-                        uintptr_t resid, uintptr_t nw, uintptr_t img_out, uintptr_t stat_out, uintptr_t sync, int epi,
-                        float eps, uintptr_t stream) {
-    GemvParams G{}, D{};
-    G.w = qmat(wg);
-    G.B = 1;
-    G.n_sel = 1;
-    G.eps = eps;
-    G.epi = epi;
-    G.y = Pp<float>(h);
-    G.ldy = G.w.N / 2;
-    G.x8 = Pp<const void>(img_in);
-    G.x8_stat = Pp<const float>(stat);
-    G.emit8 = Pp<void>(img_f);
-    D.w = qmat(wd);
-    D.B = 1;
-    D.n_sel = 1;
-    D.epi = EPI_ADD;
-    D.y = Pp<float>(resid);
-    D.ldy = D.w.N;
-    D.x8 = Pp<const void>(img_f);
-    D.emit8 = Pp<void>(img_out);
-    D.emit8_nw = Pp<const float>(nw);
-    D.emit8_stat = Pp<float>(stat_out);
-    return gemv8_ffn(G, D, Pp<void>(sync), S(stream));
-  });
   m.def("x8_slots", [](int K) { return x8_slots(K); });
   m.def("repack_m", [](py::object w, uintptr_t out, uintptr_t stream) {
     QMat q = qmat(w);
@@ -437,6 +411,7 @@ PYBIND11_MODULE(_C, m) {
     P.out_logprob = Pp<float>(d.contains("out_logprob") ? d["out_logprob"].cast<uintptr_t>() : 0);
     P.ws = Pp<float>(d.contains("ws") ? d["ws"].cast<uintptr_t>() : 0);
     P.counters = Pp<int>(d.contains("counters") ? d["counters"].cast<uintptr_t>() : 0);
+    P.err = Pp<int>(d.contains("err") ? d["err"].cast<uintptr_t>() : 0);
     sample(P, S(stream));
   });
 
@@ -539,11 +514,6 @@ PYBIND11_MODULE(_C, m) {
         w.x8e = Pp<void>(ptr("x8e"));
         w.x8f = Pp<void>(ptr("x8f"));
         w.x8st = Pp<float>(ptr("x8st"));
-        w.x8sync = Pp<void>(ptr("x8sync"));
-        w.x8q = Pp<void>(ptr("x8q"));
-        w.x8_fuse = d.contains("x8_fuse") ? d["x8_fuse"].cast<int>() : 1;
-        w.attn_o = d.contains("attn_o") ? d["attn_o"].cast<int>() : 0;
-        w.attn_o_kps = d.contains("attn_o_kps") ? d["attn_o_kps"].cast<int>() : 0;
         w.x8_ok = (d.contains("x8_ok") ? d["x8_ok"].cast<int>() : 0) && e.x8_capable() ? 1 : 0;
         {  // continuous-batching rows on the chain: as many as asked for and every emitter covers
           const int want = d.contains("x8_bmax") ? d["x8_bmax"].cast<int>() : 1;
@@ -554,16 +524,11 @@ PYBIND11_MODULE(_C, m) {
       })
       .def_property_readonly("x8_on", [](const Executor& e) { return e.ws.x8_ok; })
       .def_property_readonly("x8_bmax", [](const Executor& e) { return e.ws.x8_ok ? e.ws.x8_bmax : 0; })
-      .def_property_readonly("n_attn8", [](const Executor& e) { return e.n_attn8; })
-      .def_property_readonly("n_ffn8", [](const Executor& e) { return e.n_ffn8; })
-      .def_property_readonly("n_qkv_attn", [](const Executor& e) { return e.n_qkv_attn; })
-      .def_property_readonly("n_attn_o", [](const Executor& e) { return e.n_attn_o; })
       .def("set_segments", [](Executor& e, std::vector<std::pair<int, int>> segs) { e.segments = std::move(segs); })
-      .def("set_splits", [](Executor& e, int n, int defer, int fuse) {
+      .def("set_splits", [](Executor& e, int n, int defer) {
         e.ws.n_splits = n;
         e.ws.defer = defer;
-        e.ws.attn_fuse = fuse;
-      }, py::arg("n"), py::arg("defer") = 0, py::arg("fuse") = 0)
+      }, py::arg("n"), py::arg("defer") = 0)
       .def("run", [](Executor& e, const std::string& what, int layer, py::dict d, uintptr_t stream) {
         static const std::pair<const char*, int> names[] = {{"forward", ST_FORWARD}, {"embed", ST_EMBED},
             {"attn", ST_ATTN}, {"ffn", ST_FFN}, {"head", ST_HEAD}, {"forward_tp", ST_FORWARD_TP}};
@@ -657,9 +622,6 @@ PYBIND11_MODULE(_C, m) {
     ARParams P = ar_params(d);
     if (slab < 0 || slab >= AR_SLABS || n % 4 || n > P.slab_floats) throw std::runtime_error("ar_allreduce_add: bad slab / n");
     ar_allreduce_add(P, slab, Pp<float>(y), n, S(stream));
-  });
-  m.def("mall_prefetch", [](uintptr_t p, size_t bytes, int blocks, uintptr_t sink, uintptr_t stream) {
-    mall_prefetch(Pp<const void>(p), bytes, blocks, Pp<unsigned>(sink), S(stream));
   });
   m.def("ar_allreduce_add_emit", [](py::dict d, int slab, uintptr_t y, int E, int B, uintptr_t img, uintptr_t nw,
                                      uintptr_t stat, uintptr_t stream) {

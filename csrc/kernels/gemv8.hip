@@ -28,81 +28,14 @@ namespace omx {
 
 template <int QT, int NSB, int J, int KS, int IN, int MS, int EMIT, int BT>
 __global__ __launch_bounds__(GEMV_NT * KS) void qgemv8_kernel(GemvParams P) {
-  gemv8_body<QT, NSB, J, KS, IN, MS, EMIT, false, BT>(P, blockIdx.x);
+  gemv8_body<QT, NSB, J, KS, IN, MS, EMIT, BT>(P, blockIdx.x);
 }
 
 // q,k rows + v rows of different quant types (Q4_K_M QKV) over the same image: one launch
 template <int QA, int QB, int IN, int BT>
 __global__ __launch_bounds__(GEMV_NT) void qgemv8_dual_kernel(GemvParams PA, GemvParams PB, int gxa) {
-  if ((int)blockIdx.x < gxa) gemv8_body<QA, 1, 1, 1, IN, 0, EM_NONE, false, BT>(PA, blockIdx.x);
-  else gemv8_body<QB, 1, 1, 1, IN, 0, EM_NONE, false, BT>(PB, (int)blockIdx.x - gxa);
-}
-
-// ------------------------------------------------------------------------------------------------
-// gate_up -> down in ONE launch (batch-1 FFN). Phase A: every block computes its gate_up tile pair and
-// emits its slice of down's int8 image with write-through (sc1) stores, then arrives on a counter.
-// Phase B: the last N_down / 16 blocks of the grid also own one down tile each: they request that
-// tile's weights right after their phase-A work -- BEFORE the hand-off -- so the down weight stream
-// overlaps the gate_up tail, the launch boundary and the hand-off wait, then wait for every arrival
-// and read the image with sc1 loads. Hand-off form: MI355X_MICROARCH.md "Valid forms" table row 1
-// (every storing wave vmcnt(0) -> workgroup barrier -> one lane's agent-scope atomic add; the poller
-// loads after its poll matched, the other waves after the barrier it joins; every byte stored and
-// loaded sc1). Deadlock freedom: waiting blocks never exceed the grid's residency minus the other
-// blocks' slots (host check), and a wait gives up after 2 ms (error word; the runner raises).
-constexpr int FFN_IMG_DW = 20;  // image dwords per thread (K <= 13568 at 256 threads)
-
-// phase B: one 16-row down tile, input image handed off in this launch, EPI_ADD + emission
-template <int QT, int NSB>
-__device__ __forceinline__ void gemv8_after(const GemvParams& P, const int tile, const Handoff& H) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const QMat& w = P.w;
-  const int K = w.K, N = w.N, SB = n_sb(K), XS = SB * XPAD, XSP = x8_slots_dev(K);
-  i32x4* lq = (i32x4*)smem;
-  f32x2* lf = (f32x2*)(smem + (size_t)XSP * 16);
-  float* stage = (float*)(lf + XSP);
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = lane >> 4, s = lane & 15;
-  const int rbase = wave * 4 + g;
-  WTile<QT, NSB, 1> T;
-  load_wtile<QT, NSB, 1>(w, 0, tile * 16 + rbase, N, SB, 0, s, T, SB);  // ahead of the hand-off
-  __builtin_amdgcn_sched_barrier(0);
-  handoff_wait(H);
-  const int nd = XSP * 6;  // image dwords
-  const unsigned* src = (const unsigned*)P.x8;
-  unsigned xd[FFN_IMG_DW];
-#pragma unroll
-  for (int i = 0; i < FFN_IMG_DW; ++i)
-    xd[i] = __hip_atomic_load(src + min(tid + GEMV_NT * i, nd - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-  for (int i = 0; i < FFN_IMG_DW; ++i)
-    if (tid + GEMV_NT * i < nd) ((unsigned*)smem)[tid + GEMV_NT * i] = xd[i];
-  __syncthreads();
-  float acc[1][1] = {{0.f}};
-  compute_wtile<QT, NSB, 1, 1>(T, SB, 0, s, lq, lf, XS, acc, SB);
-  const float v = row16_sum(acc[0][0]);
-  const int n = tile * 16 + rbase;
-  if (s == 0) {
-    float nv = 0.f;
-    if (n < N) {
-      float* dst = P.y + n;
-      nv = *dst + v + (P.bias ? P.bias[n] : 0.f);
-      *dst = nv;
-    }
-    stage[rbase] = n < N ? nv * P.emit8_nw[n] : 0.f;
-    stage[16 + rbase] = nv * nv;
-  }
-  __syncthreads();
-  if (tid == 0) emit_group(P.emit8, N, tile, stage, stage + 16, P.emit8_stat);
-}
-
-template <int QA, int QB, int NSBB>
-__global__ __launch_bounds__(GEMV_NT, 2) void ffn8_kernel(GemvParams PA, GemvParams PB, Handoff H) {
-  const int bx = blockIdx.x;
-  gemv8_body<QA, 1, 2, 1, IN_X8_RMS, 0, EM_GLU, true>(PA, bx);  // gate_up tile pair -> down's image
-  handoff_arrive(H);
-  const int tb = bx - ((int)gridDim.x - H.n_cons);  // this block's down tile (the grid's last blocks)
-  if (tb < 0) return;
-  __syncthreads();  // the LDS image of phase A is rewritten below
-  gemv8_after<QB, NSBB>(PB, tb, H);
+  if ((int)blockIdx.x < gxa) gemv8_body<QA, 1, 1, 1, IN, 0, EM_NONE, BT>(PA, blockIdx.x);
+  else gemv8_body<QB, 1, 1, 1, IN, 0, EM_NONE, BT>(PB, (int)blockIdx.x - gxa);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -304,71 +237,7 @@ bool dual_b(const GemvParams& A, const GemvParams& B, int gxa, int gxb, hipStrea
   }
 }
 
-template <int QA, int QB, int NSBB>
-bool launch_ffn(const GemvParams& G, const GemvParams& D, Handoff H, hipStream_t s) {
-  const size_t lds = lds8(max(G.w.K, D.w.K), 1);
-  const int nA = ((G.w.N + 15) / 16 + 1) / 2, nB = (D.w.N + 15) / 16;
-  const int grid = max(nA, nB);
-  static int cap_cache[8][2] = {};  // (blocks per CU, CUs) per device, for this instantiation
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 8) return false;
-  int* cc = cap_cache[dev];
-  if (cc[0] == 0) {
-    int nb = 0, ncu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, ffn8_kernel<QA, QB, NSBB>, GEMV_NT, lds) != hipSuccess ||
-        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      return false;
-    cc[0] = nb > 0 ? nb : -1;
-    cc[1] = ncu;
-  }
-  // the nB waiting blocks must leave at least as many slots to the rest of the grid (progress)
-  if (cc[0] < 0 || (long long)cc[0] * cc[1] < 2LL * nB) return false;
-  H.n_prod = grid;
-  H.n_cons = nB;
-  hipLaunchKernelGGL((ffn8_kernel<QA, QB, NSBB>), dim3(grid), dim3(GEMV_NT), lds, s, G, D, H);
-  return true;
-}
-
-template <int QA, int QB>
-bool ffn_nsb(const GemvParams& G, const GemvParams& D, const Handoff& H, hipStream_t s) {
-  switch (((D.w.K + 255) / 256 + 15) / 16) {
-    case 1: return launch_ffn<QA, QB, 1>(G, D, H, s);
-    case 2: return launch_ffn<QA, QB, 2>(G, D, H, s);
-    case 3: return launch_ffn<QA, QB, 3>(G, D, H, s);
-    default: return false;
-  }
-}
-
-template <int QA>
-bool ffn_b(const GemvParams& G, const GemvParams& D, const Handoff& H, hipStream_t s) {
-  switch (D.w.qtype) {
-    case QT_Q4_K: return ffn_nsb<QA, QT_Q4_K>(G, D, H, s);
-    case QT_Q6_K: return ffn_nsb<QA, QT_Q6_K>(G, D, H, s);
-    case QT_Q4_0: return ffn_nsb<QA, QT_Q4_0>(G, D, H, s);
-    case QT_Q8_0: return ffn_nsb<QA, QT_Q8_0>(G, D, H, s);
-    default: return false;
-  }
-}
-
 }  // namespace
-
-bool gemv8_ffn(const GemvParams& G, const GemvParams& D, void* sync, hipStream_t s) {
-  Geo GG, GD;
-  if (!sync || G.B != 1 || !covered(G, GG) || !covered(D, GD)) return false;
-  if (emit_mode(G) != EM_GLU || in_mode(G) != IN_X8_RMS || GG.nsb != 1 || GG.ks != 1 || GG.J != 2) return false;
-  if (emit_mode(D) != EM_ADD || in_mode(D) != IN_X8 || D.x8 != G.emit8 || D.w.K != G.w.N / 2) return false;
-  if ((size_t)FFN_IMG_DW * GEMV_NT * 4 < x8_bytes(D.w.K)) return false;
-  Handoff H{};
-  H.count = (unsigned*)sync;
-  H.done = (unsigned*)sync + 1;
-  H.err = (int*)sync + 2;
-  switch (G.w.qtype) {
-    case QT_Q4_K: return ffn_b<QT_Q4_K>(G, D, H, s);
-    case QT_Q4_0: return ffn_b<QT_Q4_0>(G, D, H, s);
-    case QT_Q8_0: return ffn_b<QT_Q8_0>(G, D, H, s);
-    default: return false;
-  }
-}
 
 bool gemv8_supported(const GemvParams& P) {
   Geo G;

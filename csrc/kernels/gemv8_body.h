@@ -1,5 +1,4 @@
-// The batch-1 / few-row int8-chain GEMV body (gemv8.hip) and its prefetched epilogues, shared by
-// the standalone launches (gemv8.hip) and the fused QKV + attention launch (qkv_attn.hip).
+// The batch-1 / few-row int8-chain GEMV body (gemv8.hip) and its prefetched epilogues.
 #pragma once
 #include "gemv8_core.h"
 
@@ -78,9 +77,7 @@ __device__ __forceinline__ void epi_prepare(const GemvParams& P, EpiPre<J, BT>& 
 
 // EM_NONE rows: the 16 lanes of a row group reduce; lane s == b writes batch row b (EPI_QKV: RoPE +
 // paged K/V scatter; EPI_STORE: + bias; anything else: the shared epi_apply)
-// WT: write-through (sc1) stores -- another workgroup of the same launch reads q / k / v (the fused
-// QKV + attention launch, attn8.hip qkv_attn_kernel)
-template <int J, int BT, bool WT = false>
+template <int J, int BT>
 __device__ __forceinline__ void epi_rows(const GemvParams& P, float (&acc)[1][BT], int n, int s, int j,
                                          const EpiPre<J, BT>& E) {
   float v[BT], pv[BT];
@@ -107,20 +104,12 @@ __device__ __forceinline__ void epi_rows(const GemvParams& P, float (&acc)[1][BT
         out = (d & 1) ? (px * E.sn[j] + x * E.cs[j]) : (x * E.cs[j] - px * E.sn[j]);
       }
       if (which == 0) {
-        if constexpr (WT) st_wt(P.y + (long long)b * P.ldy + vn, out);
-        else P.y[(long long)b * P.ldy + vn] = out;
+        P.y[(long long)b * P.ldy + vn] = out;
       } else {
         const long long blk = E.slot / P.bs, off = E.slot % P.bs;
         const long long idx = ((blk * P.n_kv + hh) * P.bs + off) * (P.Dc > 0 ? P.Dc : D) + d;
-        if constexpr (WT) {
-          const unsigned short bits = __builtin_bit_cast(unsigned short, (f16)out);
-          // two explicit stores: a pointer select here is lowered to an indexed scratch array
-          if (which == 1) __hip_atomic_store((unsigned short*)P.kc + idx, bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          else __hip_atomic_store((unsigned short*)P.vc + idx, bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-          if (which == 1) kv_store(P.kc, idx, out, P.kv8);
-          else kv_store(P.vc, idx, out, P.kv8);
-        }
+        if (which == 1) kv_store(P.kc, idx, out, P.kv8);
+        else kv_store(P.vc, idx, out, P.kv8);
       }
     } else {
       epi_apply(P, b, vn, v[b], pv[b], 0);
@@ -133,7 +122,7 @@ __device__ __forceinline__ void epi_rows(const GemvParams& P, float (&acc)[1][BT
 // MS: merge slabs of IN_MERGE (1 = plain fp32 input, no merge).
 // BT: batch rows (continuous batching): every weight tile is read once and dotted with BT activation
 // images (row b of the LDS image at b * XSP slots); rows >= P.B are computed but never stored.
-template <int QT, int NSB, int J, int KS, int IN, int MS, int EMIT, bool WT = false, int BT = 1>
+template <int QT, int NSB, int J, int KS, int IN, int MS, int EMIT, int BT = 1>
 __device__ __forceinline__ void gemv8_body(const GemvParams& P, const int bx) {
   static_assert(BT == 1 || MS <= 1, "batched rows take the plain fp32 input (no deferred merge)");
   constexpr int NT = GEMV_NT * KS;
@@ -343,7 +332,7 @@ __device__ __forceinline__ void gemv8_body(const GemvParams& P, const int bx) {
 #pragma unroll
     for (int b = 0; b < BT; ++b) acc[0][b] *= rstd[b];
     if constexpr (EMIT == EM_NONE) {
-      if (kg == 0) epi_rows<J, BT, WT>(P, acc, t * 16 + rbase, s, j, pre);
+      if (kg == 0) epi_rows<J, BT>(P, acc, t * 16 + rbase, s, j, pre);
     } else {
       const int n = t * 16 + rbase;
       float v[BT], pv[BT];
@@ -386,11 +375,7 @@ __device__ __forceinline__ void gemv8_body(const GemvParams& P, const int bx) {
         }
         if ((t & 1) || t + 1 >= n_tiles) {
           __syncthreads();
-          if constexpr (WT) {  // write-through hand-off inside the launch (ffn8): the one-lane form
-            if (tid < nb)
-              emit_group<WT>((char*)P.emit8 + (size_t)tid * x8_slots_dev(N / 2) * 24, N / 2, t >> 1, stage + 32 * tid,
-                             nullptr, nullptr);
-          } else if (tid < 16 * nb) {
+          if (tid < 16 * nb) {
             const int b = tid >> 4, i = tid & 15;
             emit_group16((char*)P.emit8 + (size_t)b * x8_slots_dev(N / 2) * 24, N / 2, t >> 1, stage[32 * b + i], 0.f,
                          nullptr, i);

@@ -1,5 +1,5 @@
-// Shared device pieces of the batch-1 int8 activation chain (gemv8.hip, attn8.hip): the image layout,
-// the one-lane group quantiser and the in-launch hand-off primitives.
+// Shared device pieces of the batch-1 int8 activation chain (gemv8.hip, allreduce.hip): the image layout
+// and the group quantisers.
 #pragma once
 #include "gemv_core.h"
 
@@ -18,9 +18,7 @@ __device__ __forceinline__ int x8_stat_ld_dev(int K) { return ((K >> 4) + 3) & ~
 constexpr int X8_NWI = 3;   // 16-byte image words per thread (K <= 16384 at 256 threads x KS)
 constexpr int X8_NSTW = 2;  // f32x4 RMS partials per lane (K <= 8192)
 
-// quantise the 16 staged values of group G into the consumer image (one lane). WT: write-through (sc1)
-// dword stores -- the image is handed to another workgroup of the SAME launch (ffn8_kernel)
-template <bool WT = false>
+// quantise the 16 staged values of group G into the consumer image (one lane)
 __device__ __forceinline__ void emit_group(void* img, int Kc, int G, const float* v, const float* sq,
                                            float* stat) {
   float amax = 0.f;
@@ -42,17 +40,8 @@ __device__ __forceinline__ void emit_group(void* img, int Kc, int G, const float
   }
   const int XSP = x8_slots_dev(Kc);
   const int slot = (G >> 4) * XPAD + (G & 15);
-  if constexpr (WT) {
-    unsigned* q = (unsigned*)img + 4 * slot;
-    unsigned* f = (unsigned*)((char*)img + (size_t)XSP * 16) + 2 * slot;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) __hip_atomic_store(q + j, (unsigned)pk[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(f, __float_as_uint(d), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(f + 1, __float_as_uint(d * (float)qsum), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  } else {
-    ((i32x4*)img)[slot] = pk;
-    ((f32x2*)((char*)img + (size_t)XSP * 16))[slot] = (f32x2){d, d * (float)qsum};
-  }
+  ((i32x4*)img)[slot] = pk;
+  ((f32x2*)((char*)img + (size_t)XSP * 16))[slot] = (f32x2){d, d * (float)qsum};
   if (stat) {
     float ss = 0.f;
 #pragma unroll
@@ -84,49 +73,6 @@ __device__ __forceinline__ void emit_group16(void* img, int Kc, int G, float v, 
     for (int m = 8; m >= 1; m >>= 1) ss += __shfl_xor(ss, m, 16);
     if (i == 0) stat[G] = ss;
   }
-}
-
-// In-launch hand-off (MI355X_MICROARCH.md "Valid forms" table row 1): every storing wave waits for
-// its (sc1, write-through) stores, the workgroup barriers, one lane adds to an agent-scope counter; the
-// consumer polls it with sc1 loads, its other waves load after a barrier, every handed-off byte is
-// loaded sc1.
-struct Handoff {
-  unsigned* count;  // phase-A arrivals
-  unsigned* done;   // phase-B passes; the last one re-arms both (the next launch starts from zero)
-  int* err;         // 1: a wait timed out (results of that step are invalid)
-  int n_prod, n_cons;
-};
-
-__device__ __forceinline__ void handoff_arrive(const Handoff& H) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its sc1 stores are done
-  __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_fetch_add(H.count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__device__ __forceinline__ void handoff_wait(const Handoff& H) {
-  if (threadIdx.x == 0) {
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
-    while (__hip_atomic_load(H.count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)H.n_prod) {
-      if (__builtin_amdgcn_s_memrealtime() - t0 > 200000ull) {  // 2 ms: never in a healthy step
-        __hip_atomic_store(H.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-    if (__hip_atomic_fetch_add(H.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)H.n_cons - 1) {
-      __hip_atomic_store(H.count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(H.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  __syncthreads();
-}
-
-// sc1 (write-through) scalar stores of the epilogue values another workgroup of the launch reads
-__device__ __forceinline__ void st_wt(float* p, float v) {
-  __hip_atomic_store((unsigned*)p, __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ float ld_wt(const float* p) {
-  return __uint_as_float(__hip_atomic_load((const unsigned*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
 
 }  // namespace omx

@@ -120,26 +120,7 @@ inline int x8_stat_ld(int K) { return ((K >> 4) + 3) & ~3; }  // RMS-partial flo
 bool gemv8(const GemvParams& P, hipStream_t s);
 bool gemv8_2(const GemvParams& A, const GemvParams& B, hipStream_t s);  // q,k + v rows, one launch
 bool gemv8_supported(const GemvParams& P);
-// gate_up (G: EPI_GLU, emits D's image) -> down (D: EPI_ADD) in one launch with an in-kernel hand-off;
-// sync: 16 zeroed ints of device memory (counters + error word); false = not covered (two launches)
-bool gemv8_ffn(const GemvParams& G, const GemvParams& D, void* sync, hipStream_t s);
 struct AttnParams;
-// QKV (A: q,k rows or all rows, x8 RMS image in, EPI_QKV; B: v rows or B.w.s0 null) + paged attention in
-// one launch (qkv_attn.hip); the attention output lands as the O projection's int8 image `img`
-// (x8_bytes(H * D), pad slots zero); sync: the x8sync words. false = not covered
-bool qkv_attn(const GemvParams& A, const GemvParams& B, const AttnParams& At, void* img, void* sync, hipStream_t s);
-// paged attention (At: NQ == 1, n_splits = split slots per KV group, kps = keys per split, ws / counters
-// the split workspace and tickets) + O projection (O: EPI_ADD with int8 emission) in one launch
-// (attn_o.hip); the attention lands in O's int8 image `img` (x8_bytes(H * D), pad slots zero) inside
-// the launch. false = not covered (shape, or the grid would not be co-resident)
-bool attn_o(const GemvParams& O, const AttnParams& At, void* img, void* sync, hipStream_t s);
-// reads [p, p + bytes) on `blocks` workgroups so the lines land in the MALL (prefetch.hip); sink: >= 256
-// words, written only on a practically impossible fold value
-void mall_prefetch(const void* p, size_t bytes, int blocks, unsigned* sink, hipStream_t s);
-// QKV (A: q,k rows or all rows; B: v rows or B.w.s0 null) + paged attention + O projection (O.x8 = the
-// attention image, EPI_ADD + emission) in one launch (attn8.hip); false = not covered
-bool attn8(const GemvParams& A, const GemvParams& B, const GemvParams& O, const AttnParams& At, void* sync,
-           hipStream_t s);
 
 // y = epi(W x): the quantised GEMV for small B (decode), the MFMA dequant GEMM for B >= GEMM_MIN_B
 // when an fp16 activation workspace is given (prefill); same epilogues either way.
@@ -254,6 +235,9 @@ struct SampleParams {
   // per-row tickets [B] (zero-initialised; re-armed by the kernel)
   float* ws = nullptr;
   int* counters = nullptr;
+  // optional error word: set to 1 when a row's choice was out of range (non-finite logits); the id
+  // itself is clamped to 0 so the next step's embedding read stays in bounds, the host fails the request
+  int* err = nullptr;
 };
 constexpr int SAMPLE_WS_FLOATS_PER_ROW(int V) { return ((V + 1023) / 1024) * 2 * 64; }
 void sample(const SampleParams& P, hipStream_t s);
@@ -310,9 +294,6 @@ enum {
   LC_GEMV_FLIGHT,    // gemv.hip / gemv_batch.hip fp32-prologue GEMVs
   LC_ATTN_DECODE,    // attention.hip split flash-decode kernel
   LC_ATTN_PREFILL,   // attention.hip MFMA flash prefill
-  LC_QKV_ATTN,       // qkv_attn.hip fused QKV + attention (batch-1 decode, short context)
-  LC_ATTN_O,         // attn_o.hip fused attention + O projection (batch-1 decode)
-  LC_MALL_PREFETCH,  // prefetch.hip side-stream weight reader
   LC_N
 };
 void count_launch(int which);

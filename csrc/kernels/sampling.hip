@@ -285,7 +285,10 @@ __device__ void legacy_select(const SampleParams& P, int b, float* lg, int V, in
 __device__ __forceinline__ void finish_sample(const SampleParams& P, int b, int chosen, float chosen_lp) {
   // a non-finite logit row (an overflowed activation upstream) must not turn into an out-of-range id:
   // the id is the next step's embedding row, read on device without a host check
-  if ((unsigned)chosen >= (unsigned)P.V) chosen = 0;
+  if ((unsigned)chosen >= (unsigned)P.V) {
+    chosen = 0;
+    if (P.err) *P.err = 1;  // the host fails the request (Runner.sampler_error)
+  }
   const int seen = P.hist_count[b];
   P.out[b] = chosen;
   if (P.out_logprob) P.out_logprob[b] = chosen_lp;

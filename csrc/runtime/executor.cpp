@@ -176,83 +176,6 @@ void Executor::attn_block(int i, const StepInputs& in, hipStream_t s) {
   if (ch && i > 0) chain_in(P, ws.xa16, ws.ld_e, ws.st[1], (E + 15) / 16);  // emitted by layer i-1's down
   if (ch) P.rexp_out = ws.st[1] + 16 * ((E + 15) / 16) + 16;  // O's range exponents (layer 0: from resid)
   if (q8 && i > 0) x8_in(P, ws.x8e, ws.x8st);                                 // emitted by layer i-1's down
-  if (q8 && i > 0 && B == 1 && ws.attn_fuse == 2 && ws.x8q && !phi) {
-    // QKV + attention in one launch (qkv_attn.hip): the attention lands as O's int8 image
-    GemvParams V{};
-    if (!L.qkv_fused) {
-      V = P;
-      V.w = L.wv;
-      V.row_offset = Eq + Ekv;
-    }
-    AttnParams A{};
-    A.block_table = in.block_table;
-    A.max_blocks = in.max_blocks;
-    A.q_seq = in.q_seq;
-    A.q_len = in.q_len;
-    A.NQ = B;
-    A.H = cfg.H;
-    A.n_kv = cfg.Hkv;
-    A.D = cfg.Dc > 0 ? cfg.Dc : cfg.D;
-    A.kv8 = cfg.kv8;
-    A.Dv = cfg.D;
-    A.bs = in.bs;
-    A.scale = 1.0f / std::sqrt((float)cfg.D);
-    A.window = cfg.window;
-    if (A.D == A.Dv && qkv_attn(P, V, A, ws.x8q, ws.x8sync, s)) {
-      ++n_qkv_attn;
-      GemvParams O = base_params(L.wo, B, ws.abuf, Eq, ws);
-      O.bias = L.bo;
-      O.ldy = E;
-      x8_in(O, ws.x8q, nullptr);
-      if (cfg.tp > 1) {  // partial sums to this rank's all-reduce slab (it emits gate_up's image)
-        O.epi = EPI_STORE;
-        O.y = tp_dst(0, B);
-      } else {
-        O.epi = EPI_ADD;
-        O.y = ws.resid;
-        x8_emit(O, ws.x8e, L.ffn_norm, ws.x8st);  // gate_up's RMSNorm input, int8
-      }
-      gemv(O, s);
-      return;
-    }
-  }
-  if (q8 && i > 0 && B == 1 && ws.attn_fuse == 1 && ws.x8q && !phi) {  // QKV + attention + O in one launch (attn8.hip)
-    GemvParams V{};
-    if (!L.qkv_fused) {
-      V = P;
-      V.w = L.wv;
-      V.row_offset = Eq + Ekv;
-    }
-    GemvParams O = base_params(L.wo, B, ws.abuf, Eq, ws);
-    O.bias = L.bo;
-    O.epi = EPI_ADD;
-    O.y = ws.resid;
-    O.ldy = E;
-    x8_in(O, ws.x8q, nullptr);
-    x8_emit(O, ws.x8e, L.ffn_norm, ws.x8st);
-    AttnParams A{};
-    A.q = ws.qbuf;
-    A.ldq = Eq;
-    A.kc = L.kc;
-    A.vc = L.vc;
-    A.block_table = in.block_table;
-    A.max_blocks = in.max_blocks;
-    A.q_seq = in.q_seq;
-    A.q_len = in.q_len;
-    A.NQ = B;
-    A.H = cfg.H;
-    A.n_kv = cfg.Hkv;
-    A.D = cfg.Dc > 0 ? cfg.Dc : cfg.D;
-    A.kv8 = cfg.kv8;
-    A.Dv = cfg.D;
-    A.bs = in.bs;
-    A.scale = 1.0f / std::sqrt((float)cfg.D);
-    A.window = cfg.window;
-    if (attn8(P, V, O, A, ws.x8sync, s)) {
-      ++n_attn8;
-      return;
-    }
-  }
   if (!L.qkv_fused) {  // q,k and v rows of different quant types: one dual launch at B == 1
     GemvParams V = P;
     V.w = L.wv;
@@ -304,22 +227,6 @@ void Executor::attn_block(int i, const StepInputs& in, hipStream_t s) {
     throw std::runtime_error("deferred attention merge: unsupported (K, D, splits)");
   A.defer = defer;
   if (ch) A.out16 = ws.a16;
-  if (q8 && B == 1 && ws.attn_o && !phi && cfg.tp == 1 && ws.x8q && !in.prefill && ws.attn_ws && ws.attn_cnt) {
-    // attention + O projection in one launch (attn_o.hip): O's weights stream while the attention
-    // runs; the split merge happens inside the attention blocks, O reads a ready int8 image
-    AttnParams Ao = A;
-    Ao.kps = ws.attn_o_kps > 0 ? ws.attn_o_kps : 128;
-    GemvParams O = base_params(L.wo, B, ws.abuf, Eq, ws);
-    O.bias = L.bo;
-    O.epi = EPI_ADD;
-    O.y = ws.resid;
-    O.ldy = E;
-    x8_emit(O, ws.x8e, L.ffn_norm, ws.x8st);  // gate_up's RMSNorm input, int8
-    if (attn_o(O, Ao, ws.x8q, ws.x8sync, s)) {
-      ++n_attn_o;
-      return;
-    }
-  }
   if (in.prefill && !segments.empty()) {  // several sequences' prompts: flash attention per segment
     for (const auto& sg : segments) {
       AttnParams As = A;
@@ -494,10 +401,6 @@ void Executor::ffn_block(int i, const StepInputs& in, hipStream_t s) {
   } else if (q8) {
     x8_in(Dn, ws.x8f, nullptr);
     x8_emit(Dn, ws.x8e, i + 1 < (int)layers.size() ? layers[i + 1].attn_norm : out_norm, ws.x8st);
-    if (ws.x8_fuse && B == 1 && gemv8_ffn(G, Dn, ws.x8sync, s)) {  // one launch, in-kernel hand-off
-      ++n_ffn8;
-      return;
-    }
   }
   gemv(G, s);
   gemv(Dn, s);

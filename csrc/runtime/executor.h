@@ -90,15 +90,8 @@ struct Workspace {
   void* x8e = nullptr;
   void* x8f = nullptr;
   float* x8st = nullptr;
-  void* x8sync = nullptr;    // 128 zeroed ints: in-launch hand-off counters + error words (gemv8_ffn, attn8)
-  void* x8q = nullptr;       // int8 image of the attention output (the O projection's input, attn8)
-  int attn_o = 0;            // batch-1 decode on the int8 chain: attention + O in one launch (attn_o.hip)
-  int attn_o_kps = 0;        //   its target keys per split (0 = 128)
-  int attn_fuse = 0;         // this step (B == 1, short context): 1 = QKV + attention + O in one launch
-                             // (attn8, opt-in), 2 = QKV + attention in one launch (qkv_attn), O after
   int x8_ok = 0;
   int x8_bmax = 1;           // batch rows the chain takes (continuous batching: up to X8_MAX_B)
-  int x8_fuse = 1;           // gate_up -> down in one launch (gemv8_ffn) when covered
 };
 constexpr int MB_CHAIN_MAX = 16;
 
@@ -142,7 +135,6 @@ class Executor {
   bool chain_capable() const;                            // every projection takes the fp16 matrix-core chain
   bool x8_capable(int B = 1) const;                               // every emitter of the int8 chain takes gemv8
   StepInputs bound{};                                    // pre-bound step inputs (set_inputs)
-  long long n_attn8 = 0, n_ffn8 = 0, n_qkv_attn = 0, n_attn_o = 0;                     // fused launches enqueued (tests: the path ran)
   // batched admission (Runner.admit_many): the rows of a prefill step are several sequences' contiguous
   // prompt segments {first row, rows}; attention runs the MFMA flash kernel once per segment. Empty: one
   // sequence (or a decode step). Host-side: admission steps are never graph-captured.

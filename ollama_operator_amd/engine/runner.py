@@ -99,11 +99,7 @@ class NativeExec:
         b = getattr(r, "x8_bufs", None)
         if not b:
             return {}
-        return dict(x8e=b["x8e"].data_ptr(), x8f=b["x8f"].data_ptr(), x8st=b["x8st"].data_ptr(), x8q=b["x8q"].data_ptr(),
-                    x8sync=b["x8sync"].data_ptr(), x8_ok=1, x8_fuse=int(os.environ.get("OMX_X8_FUSE", "0") != "0"),
-                    # batch-1 decode: attention + O projection in one launch (attn_o.hip)
-                    attn_o=int(os.environ.get("OMX_ATTN_O", "0") != "0"),  # opt-in: slower, profiles/r5_decode
-                    attn_o_kps=int(os.environ.get("OMX_ATTN_O_KPS", "128")),
+        return dict(x8e=b["x8e"].data_ptr(), x8f=b["x8f"].data_ptr(), x8st=b["x8st"].data_ptr(), x8_ok=1,
                     # batch rows on the chain: B = 2 measured 1.73 vs 2.08 ms per step on the int8 rows, B = 3
                     # 2.15 vs 2.19 ms; at 4 rows layout M's MFMA GEMVs win (profiles/r4_batch), so 3 by default
                     x8_bmax=int(os.environ.get("OMX_X8_BATCH", "3")))
@@ -114,19 +110,7 @@ class NativeExec:
     def run(self, stage: str, layer: int, B: int, n_logits: int = 0, use_idx: bool = False,
             prefill: bool = False):
         S, defer = self.r.split_plan(B)
-        # batch-1 decode over <= 512 keys: QKV + attention + O in one launch (attn8.hip), when the
-        # executor covers the shapes (it falls back to the split attention kernel otherwise)
-        # the fused launches stage at most A8_MAXBT = 64 block-table entries: fuse only while S *
-        # defer_kps keys fit. 1: QKV + attention + O (attn8.hip, opt-in OMX_ATTN_FUSE=1); 2: QKV +
-        # attention (qkv_attn.hip, opt-in up to OMX_QKV_ATTN_MAXS splits' worth of keys)
-        S_ = self.r._decode_S
-        fits = S_ * self.r.defer_kps <= 64 * self.r.block_size
-        fuse = 0
-        if B == 1 and fits and S_ in (1, 2, 4) and self.r.attn_fuse:
-            fuse = 1
-        elif B == 1 and fits and 1 <= S_ <= self.r.qkv_attn_maxs:
-            fuse = 2
-        self.exe.set_splits(S, defer, fuse)
+        self.exe.set_splits(S, defer)
         self.exe.step(self.stages[stage], layer, B, n_logits, use_idx, prefill, stream_handle() if self.on_gpu else 0)
 
 
@@ -240,26 +224,12 @@ class Runner:
                                 st1=torch.zeros((E + 15) // 16 * 16 + 32, **f32))
         # batch-1 int8 activation chain (csrc/kernels/gemv8.hip): zeroed images (pad slots stay zero)
         self.x8_bufs = None
-        self.attn_fuse = False
         if self.is_gpu and os.environ.get("OMX_X8", "1") != "0":
             C = native()
             u8 = dict(device=dev, dtype=torch.uint8)
             nb = 4  # batch rows of the chain (gemv8.hip X8_MAX_B): row b's image at b * x8_bytes
             self.x8_bufs = dict(x8e=torch.zeros(nb * C.x8_bytes(E), **u8), x8f=torch.zeros(nb * C.x8_bytes(Fl), **u8),
-                                x8st=torch.zeros(nb * C.x8_stat_ld(E) + 4, **f32),
-                                x8q=torch.zeros(C.x8_bytes(Eq), **u8),
-                                x8sync=torch.zeros(128, device=dev, dtype=torch.int32))
-        self.attn_fuse = os.environ.get("OMX_ATTN_FUSE", "0") != "0"
-        # batch-1 decode over <= OMX_QKV_ATTN_MAXS x defer_kps keys: QKV + attention in one launch
-        # (qkv_attn.hip). Off by default: 17.8-18.1 us per layer against 8.0 + 5.7 for the two launches
-        # (profiles/r5_decode): the last arriver's single-block attention trails the QKV tail
-        self.qkv_attn_maxs = int(os.environ.get("OMX_QKV_ATTN_MAXS", "0")) if self.x8_bufs is not None else 0
-        # the in-launch hand-offs of the opt-in fused paths (attn8 / ffn8) report a timeout or an
-        # over-long block table through an error word: checked after every fused decode step
-        self._fused_check = self.x8_bufs is not None and (
-            self.attn_fuse or os.environ.get("OMX_X8_FUSE", "0") != "0")
-        # (qkv_attn can raise the same error word only past the staged block table, which the host's
-        # `fits` bound in NativeExec.run never lets a fused step reach)
+                                x8st=torch.zeros(nb * C.x8_stat_ld(E) + 4, **f32))
         # MoE prefill grouping (csrc/kernels/moe.hip moe_sort -> grouped MFMA GEMM)
         n_pairs = max_batch * ksel
         self.moe_rows = torch.zeros(n_pairs, **i32)
@@ -309,6 +279,8 @@ class Runner:
         # and hand-off tickets (zeroed once; the kernel re-arms them)
         self.s_ws = torch.zeros(max_batch, -(-cfg.n_vocab // 1024) * 128, **f32)
         self.s_tickets = torch.zeros(max_batch, **i32)
+        # sampler error word: a row whose logits were non-finite (its id is clamped to 0 on device)
+        self.s_err = torch.zeros(1, **i32)
         self.kv = PagedKV(n_blocks, block_size, max_seqs, self.max_blocks)
         # deferred flash-decode merge (B == 1): attention leaves S <= 8 partial slabs, the O GEMV
         # merges them in its activation prologue (no in-launch ticket + re-read)
@@ -366,7 +338,14 @@ class Runner:
     def close(self) -> None:
         """Release the TP collective workspace (all ranks call this together). The executor forgets
         the slabs and the captured graphs (which point at them) go first, so no later step can write
-        into freed memory; a closed runner refuses further steps."""
+        into freed memory; a closed runner refuses further steps.
+
+        Then everything else goes with it: the graphs, the Runner <-> NativeExec reference cycle and the
+        device tensors. warmup() froze the objects alive after load (gc.freeze), and a frozen cycle is
+        never collected, so without this every unload (keep-alive expiry, eviction, reload) would keep
+        the model's weights, KV cache and graphs resident on the GPU."""
+        if self._closed:
+            return
         if self.ar is not None:
             if isinstance(self.exe, NativeExec):
                 self.exe.exe.clear_ar()
@@ -374,6 +353,23 @@ class Runner:
             self.ar.close()
             self.ar = None
         self._closed = True
+        self.graphs.clear()
+        ex, self.exe = self.exe, None
+        if isinstance(ex, NativeExec):
+            ex.r = None
+            ex.exe = None
+        for k, v in list(vars(self).items()):  # device buffers and weights: dropped now, not at collection
+            if isinstance(v, (torch.Tensor, list, dict, DeviceWeights)) and k not in ("graphs",):
+                setattr(self, k, None)
+        if self.is_gpu:
+            torch.cuda.synchronize(self.device)
+        refreeze = gc.get_freeze_count() > 0
+        gc.unfreeze()
+        gc.collect()
+        if refreeze:  # the other loaded models stay out of the collector's way
+            gc.freeze()
+        if self.is_gpu:
+            torch.cuda.empty_cache()
 
     # ------------------------------------------------------------------ sizing helpers
     def n_splits(self, B: int) -> int:
@@ -580,7 +576,7 @@ class Runner:
                                  frequency_penalty=p(self.s_fpen), history=p(self.s_hist),
                                  hist_count=p(self.s_hcount), hist_cap=HIST_CAP, repeat_last_n=p(self.s_lastn),
                                  seed=p(self.s_seed), step=p(self.s_step), out=p(self.s_out),
-                                 ws=p(self.s_ws), counters=p(self.s_tickets)), stream_handle())
+                                 ws=p(self.s_ws), counters=p(self.s_tickets), err=p(self.s_err)), stream_handle())
         else:
             for b in range(B):
                 o, hist, seed, step = self._host_sampler[b]
@@ -722,33 +718,23 @@ class Runner:
                     self._decode_body(B)
             if self.is_gpu:
                 self._adv_next = (sids[0], poss[0] + 1) if B == 1 else (tuple(sids), tuple(p + 1 for p in poss))
-            if self._fused_check and B == 1:
-                err = self.x8_error()
-                if err:
-                    self.x8_bufs["x8sync"].zero_()
-                    raise RuntimeError("fused decode step (OMX_ATTN_FUSE / OMX_X8_FUSE): an in-launch hand-off "
-                                       "timed out or the sequence exceeded the staged block table; the step's "
-                                       "logits are invalid")
         finally:
             self._decode_S = 0
 
-    def _check_handoffs(self) -> None:
-        """Once per generation (one small read): an in-launch hand-off of the decode graph (attn_o.hip
-        and the opt-in fused paths) that timed out leaves its error word set -- those steps' tokens are
-        invalid, so fail loudly (the server turns it into an error response; the pod restarts)."""
-        if self.x8_bufs is None or self._closed:
-            return
-        err = self.x8_error()
-        if err:
-            self.x8_bufs["x8sync"].zero_()
-            raise RuntimeError("decode step: an in-launch hand-off (attention + O / fused layer halves) timed out; "
-                               "the generated tokens are invalid")
+    def sampler_error(self) -> bool:
+        """True (and the word re-armed) when a sample since the last check met non-finite logits: the
+        tokens of that request are not valid output. One small device read (a sync)."""
+        if self._closed or not self.is_gpu:
+            return False
+        if int(self.s_err.item()):
+            self.s_err.zero_()
+            return True
+        return False
 
-    def x8_error(self) -> int:
-        """Nonzero when an in-launch hand-off of the int8 chain timed out (gemv8.hip ffn8_kernel): the
-        step's results are invalid. Reads device memory (a sync)."""
-        b = self.x8_bufs
-        return int(b["x8sync"][2].item() or b["x8sync"][16 + 66].item() or b["x8sync"][98].item()) if b else 0
+    def check_sampler(self) -> None:
+        if self.sampler_error():
+            raise RuntimeError("sampling met non-finite logits (numerical fault upstream); the generated tokens "
+                               "are invalid")
 
     def set_tokens(self, tokens: list[int]) -> None:
         """Host -> d_tokens[:len(tokens)] (batch recomposition: rows' next inputs)."""
@@ -923,7 +909,7 @@ class Runner:
                 ctrl.signal(False)  # generation over (also when the consumer closed us early)
             if ctrl is not None and self.ar is not None:
                 self.ar.check()  # a peer that missed a barrier timed the step out: fail loudly
-            self._check_handoffs()
+            self.check_sampler()
             if times is not None:
                 times.gen_tokens = n
                 times.gen_s = time.perf_counter() - t1

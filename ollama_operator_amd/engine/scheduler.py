@@ -391,7 +391,14 @@ class BatchScheduler:
         req.out.put(tok)
 
     def _retire(self, req: _Req) -> None:
-        req.out.put(_DONE)
+        # a sample since the last check met non-finite logits (the sampler clamped the id): that request's
+        # stream is not valid output -- fail it loudly rather than end it as a normal completion
+        err = getattr(self.r, "sampler_error", None)
+        if err is not None and err():
+            req.out.put(RuntimeError("sampling met non-finite logits (numerical fault upstream); the generated "
+                                     "tokens are invalid"))
+        else:
+            req.out.put(_DONE)
         if req.sid is not None:
             self.idle.append(req.sid)
             while len(self.idle) > self.max_idle:  # bounded prefix cache

@@ -99,64 +99,6 @@ def main():
                 ops["emit8_stat"] = ost.data_ptr()
         s = torch.cuda.Stream()
         n_launch = 64
-        if os.environ.get("OMX_BENCH_PF") and not hot:
-            # MALL prefetch probe (prefetch.hip): while launch i runs on the main stream, a side stream reads
-            # copy i + 1 (its lines land in the 256 MiB Infinity Cache), so launch i + 1 finds its weights
-            # on-die. Both streams captured into ONE graph (fork / join by events: the prefetch of copy
-            # i + 1 depends on launch i - 1 only, so it can run beside launch i).
-            side = torch.cuda.Stream()
-            sink = torch.zeros(256, dtype=torch.int32, device="cuda")
-            tot = keep[0].numel()
-
-            def timed(g):
-                for _ in range(3):
-                    g.replay()
-                torch.cuda.synchronize()
-                ts = []
-                for _ in range(10):
-                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                    e0.record()
-                    g.replay()
-                    e1.record()
-                    torch.cuda.synchronize()
-                    ts.append(e0.elapsed_time(e1) * 1e3 / n_launch)
-                return float(np.median(ts))
-            for pf in [0] + [int(x) for x in os.environ.get("OMX_BENCH_PF_BLOCKS", "32,64,128,256").split(",")]:
-                with torch.cuda.stream(s):
-                    sh, sd = s.cuda_stream, side.cuda_stream
-                    for i in range(3):
-                        C.gemv(tups[i % len(tups)], 1, 0, K, 0, 0, 0, 1e-5, epi, y.data_ptr(), Ny, 0, 0, ops, sh)
-                        C.mall_prefetch(keep[i].data_ptr(), tot, 64, sink.data_ptr(), sh)
-                    torch.cuda.synchronize()
-                    g = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(g, stream=s):
-                        prev = torch.cuda.Event()
-                        prev.record(s)
-                        for i in range(n_launch):
-                            if pf:
-                                side.wait_event(prev)
-                                C.mall_prefetch(keep[(i + 1) % len(keep)].data_ptr(), tot, pf, sink.data_ptr(), sd)
-                            C.gemv(tups[i % len(tups)], 1, 0, K, 0, 0, 0, 1e-5, epi, y.data_ptr(), Ny, 0, 0, ops, sh)
-                            prev = torch.cuda.Event()
-                            prev.record(s)
-                        if pf:
-                            s.wait_stream(side)
-                t = timed(g)
-                del g
-                tag = f"+ MALL prefetch on {pf:3d} blocks" if pf else "(no prefetch)              "
-                line = f"{name:9s} cold graph {tag} {t:7.2f} us/launch  {nbytes / t / 1e3:7.1f} GB/s"
-                if pf:  # the prefetch reader alone over the rotated copies
-                    with torch.cuda.stream(s):
-                        g = torch.cuda.CUDAGraph()
-                        with torch.cuda.graph(g, stream=s):
-                            for i in range(n_launch):
-                                C.mall_prefetch(keep[i % len(keep)].data_ptr(), tot, pf, sink.data_ptr(), s.cuda_stream)
-                    ta = timed(g)
-                    del g
-                    line += f"   | reader alone {ta:7.2f} us/copy {nbytes / ta / 1e3:7.1f} GB/s"
-                print(line, flush=True)
-            del tups, keep
-            continue
         with torch.cuda.stream(s):
             sh = s.cuda_stream
             for i in range(3):  # warm (instantiation, lds attributes)

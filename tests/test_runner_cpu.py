@@ -110,3 +110,30 @@ def test_kv_cache_type_env(tiny_models, monkeypatch):
     monkeypatch.setenv("OMX_KV_CACHE_TYPE", "fp8")
     r = Runner(tiny_models["tiny-llama"], device="cpu", max_batch=8, max_seqs=1, ctx=64)
     assert not r.kv8 and r.kc[0].dtype == torch.float16
+
+
+@pytest.mark.parametrize("backend", ["torch", "native"])
+def test_close_releases_runner_after_gc_freeze(tiny_models, backend):
+    """warmup() freezes the objects alive after load (gc.freeze), and Runner <->
+    NativeExec point at each other; close() must break that cycle so the unloaded model's buffers go
+    (the server's unload path: ModelManager._unload -> Runner.close)."""
+    import gc
+    import weakref
+    from ollama_operator_amd.ops.cpu import cpu_module
+    if backend == "native" and cpu_module() is None:
+        pytest.skip("native CPU backend not built")
+    r = Runner(tiny_models["tiny-llama"], device="cpu", max_batch=4, max_seqs=2, ctx=64, cpu_backend=backend)
+    sid = r.new_sequence()
+    r.prefill(sid, [1, 2, 3])
+    ref, kc = weakref.ref(r), weakref.ref(r.kc[0])
+    gc.collect()
+    gc.freeze()
+    try:
+        r.close()
+        assert r.exe is None and r.kc is None
+        del r
+        gc.collect()
+        assert ref() is None, "runner still alive after close()"
+        assert kc() is None, "KV cache still alive after close()"
+    finally:
+        gc.unfreeze()
