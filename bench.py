@@ -425,7 +425,7 @@ def main():
     long_ctx = [int(x) for x in a.long_ctx.split(",") if x.strip()] if gpu else []
     LC_WARM, LC_STEPS = 8, 64
     ctx = max(a.prompt + a.warmup + a.steps + 64, a.ttft_long + 8 if a.ttft_long else 0,
-              max(long_ctx, default=0) + LC_WARM + LC_STEPS + 16)
+              max(long_ctx, default=0) + LC_WARM + LC_STEPS + 64)
     t_load = time.perf_counter()
     runner = Runner(path, device=f"cuda:{local}" if gpu else "cpu", max_batch=a.chunk,
                     max_seqs=max(2, a.batch_extra), ctx=ctx)
@@ -438,7 +438,11 @@ def main():
     prompt = [1] + torch.randint(3, runner.cfg.n_vocab, (a.prompt - 1,), generator=g).tolist()
     opts = SamplingOptions(seed=42 + rank)  # Ollama defaults
     sid = runner.new_sequence()
-    gen = runner.generate(sid, prompt, opts, max_tokens=a.warmup + a.steps + 2)
+    # decode steps per graph replay (Runner.decode_group): the timed window must hold whole groups
+    G = getattr(runner, "decode_group", 1)
+    if a.steps % G:
+        runner.decode_group = G = 1
+    gen = runner.generate(sid, prompt, opts, max_tokens=a.warmup + a.steps + 4 * G + 4)
     t_p = time.perf_counter()
     next(gen)  # prefill + first token
     ttft = time.perf_counter() - t_p
@@ -453,12 +457,19 @@ def main():
         if gpu:
             torch.cuda.synchronize()
 
+    # Exactly a.steps decode steps in the timed window: the sync before t0 retires every step already
+    # enqueued (the generator keeps steps in flight ahead of the tokens it hands out), the loop hands out
+    # tokens until a.steps more have been enqueued, and the sync after t1 retires them. Counting handed-out
+    # tokens instead would credit the window with steps the GPU finished before t0.
     sync()
+    s0 = runner.steps_issued
     t0 = time.perf_counter()
-    for _ in range(a.steps):
+    while runner.steps_issued - s0 < a.steps:
         next(gen)
     sync()
     dt = time.perf_counter() - t0
+    if runner.steps_issued - s0 != a.steps:
+        raise RuntimeError(f"timed window ran {runner.steps_issued - s0} decode steps, not {a.steps}")
     t = torch.tensor([dt], device="cuda" if gpu else "cpu")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -484,17 +495,19 @@ def main():
             best = dt_l if best is None else min(best, dt_l)
         ttft_long = round(best * 1e3, 2)
     long_res = {}
-    for L in sorted({min(x, runner.ctx - LC_WARM - LC_STEPS - 4) for x in long_ctx}):
-        # decode after an L-token prompt: every step attends over >= L cached keys (split flash-decode)
+    for L in sorted({min(x, runner.ctx - LC_WARM - LC_STEPS - 8 * G - 8) for x in long_ctx}):
+        # decode after an L-token prompt: every step attends over >= L cached keys (split flash-decode);
+        # exactly LC_STEPS decode steps timed, as the headline loop
         p = [1] + torch.randint(3, runner.cfg.n_vocab, (L - 1,), generator=g).tolist()
         sid = runner.new_sequence()
-        gl = runner.generate(sid, p, opts, max_tokens=LC_WARM + LC_STEPS + 2)
+        gl = runner.generate(sid, p, opts, max_tokens=LC_WARM + LC_STEPS + 4 * G + 4)
         next(gl)
         for _ in range(LC_WARM):
             next(gl)
         sync()
+        s_l = runner.steps_issued
         t_l = time.perf_counter()
-        for _ in range(LC_STEPS):
+        while runner.steps_issued - s_l < LC_STEPS:
             next(gl)
         sync()
         dt_l = time.perf_counter() - t_l

@@ -25,8 +25,8 @@ static QMat qmat(py::object o) {
   QMat m{};
   if (o.is_none()) return m;
   auto t = o.cast<py::tuple>();
-  if (t.size() < 7 || t.size() > 10)
-    throw std::runtime_error("qmat tuple must be (s0, s1, s2, s3, N, K, qtype[, s4[, mt[, f16]]])");
+  if (t.size() < 7 || t.size() > 9)
+    throw std::runtime_error("qmat tuple must be (s0, s1, s2, s3, N, K, qtype[, s4[, mt]])");
   m.s0 = Pp<const uint8_t>(t[0].cast<uintptr_t>());
   m.s1 = Pp<const uint8_t>(t[1].cast<uintptr_t>());
   m.s2 = Pp<const uint8_t>(t[2].cast<uintptr_t>());
@@ -36,7 +36,6 @@ static QMat qmat(py::object o) {
   m.qtype = t[6].cast<int>();
   m.s4 = t.size() >= 8 ? Pp<const uint8_t>(t[7].cast<uintptr_t>()) : nullptr;
   m.mt = t.size() >= 9 ? Pp<const uint8_t>(t[8].cast<uintptr_t>()) : nullptr;
-  m.f16 = t.size() == 10 ? Pp<const void>(t[9].cast<uintptr_t>()) : nullptr;
   if (m.s4 && m.qtype != QT_Q6_K) throw std::runtime_error("widened codes are for Q6_K only");
   if (m.qtype != QT_Q4_0 && m.qtype != QT_Q8_0 && m.qtype != QT_Q4_K && m.qtype != QT_Q5_K && m.qtype != QT_Q6_K &&
       m.qtype != QT_F16)
@@ -146,7 +145,7 @@ PYBIND11_MODULE(_C, m) {
       })
       .def("repack", [](const GGUFMap& g, const std::string& name, py::array_t<int64_t> rows,
                         py::array_t<int64_t> dst_rows, int64_t K_src, int64_t kb0, int64_t kb1,
-                        std::vector<uintptr_t> dst, int n_threads) {
+                        std::vector<uintptr_t> dst, int n_threads, int64_t K_out) {
         const auto& e = g.get(name);
         uint8_t* d[4] = {nullptr, nullptr, nullptr, nullptr};
         for (size_t i = 0; i < dst.size() && i < 4; ++i) d[i] = Pp<uint8_t>(dst[i]);
@@ -156,18 +155,20 @@ PYBIND11_MODULE(_C, m) {
           if (r(i) < 0 || r(i) >= n_src_rows) throw std::runtime_error("repack: row out of range");
         if (dst_rows.shape(0) != rows.shape(0)) throw std::runtime_error("repack: rows/dst_rows length");
         py::gil_scoped_release nogil;
-        repack_rows(g.data(e), e.type, K_src, rows.data(), dst_rows.data(), rows.shape(0), kb0, kb1, d, n_threads);
-      });
+        repack_rows(g.data(e), e.type, K_src, rows.data(), dst_rows.data(), rows.shape(0), kb0, kb1, d, n_threads, K_out);
+      }, py::arg("name"), py::arg("rows"), py::arg("dst_rows"), py::arg("K_src"), py::arg("kb0"), py::arg("kb1"),
+         py::arg("dst"), py::arg("n_threads"), py::arg("K_out") = 0);
   m.def("repack_ptr", [](uintptr_t src, int qtype, int64_t K_src, py::array_t<int64_t> rows,
                          py::array_t<int64_t> dst_rows, int64_t kb0, int64_t kb1, std::vector<uintptr_t> dst,
-                         int n_threads) {
+                         int n_threads, int64_t K_out) {
     uint8_t* d[4] = {nullptr, nullptr, nullptr, nullptr};
     for (size_t i = 0; i < dst.size() && i < 4; ++i) d[i] = Pp<uint8_t>(dst[i]);
     if (dst_rows.shape(0) != rows.shape(0)) throw std::runtime_error("repack: rows/dst_rows length");
     py::gil_scoped_release nogil;
     repack_rows(Pp<const uint8_t>(src), qtype, K_src, rows.data(), dst_rows.data(), rows.shape(0), kb0, kb1, d,
-                n_threads);
-  });
+                n_threads, K_out);
+  }, py::arg("src"), py::arg("qtype"), py::arg("K_src"), py::arg("rows"), py::arg("dst_rows"), py::arg("kb0"),
+     py::arg("kb1"), py::arg("dst"), py::arg("n_threads"), py::arg("K_out") = 0);
 
   // ------------------------------------------------------------------ single ops (tests, prefill)
   m.def("gemv", [](py::object w, int B, uintptr_t x, int ldx, int norm, uintptr_t norm_w, uintptr_t norm_b,
@@ -306,10 +307,10 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("set_gemm_lib_min_m", &set_gemm_lib_min_m, "prefill rows from which the hipBLASLt path runs (0 = off)");
   m.def("gemm_lib_min_m", &gemm_lib_min_m);
-  m.def("gemm_lib_min_m_res", &gemm_lib_min_m_res);
   m.def("set_dq_gemm", &set_dq_gemm, "1: prefill GEMMs from 128 rows on the stream-order dequant kernel (gemm_dq.hip)");
   m.def("set_dq_tuning", &set_dq_tuning, "microbenchmarks: force the dq GEMM tile config (0..3, -1 auto) and split-K factor (0 auto)");
   m.def("dq_gemm_enabled", &dq_gemm_enabled);
+  m.def("set_dq_ring", &set_dq_ring, "1: prefill dq GEMMs on the register-ring kernel, 0: the glds kernel");
   // launch counters (ops.h LC_*): tests assert which kernel family a call enqueued
   m.def("launch_counts", []() {
     static const char* names[LC_N] = {"dq_gemm", "gemm_tile", "gemm_lib", "gemv8_row1", "gemv8_rows", "gemv8_dual",
@@ -427,6 +428,7 @@ PYBIND11_MODULE(_C, m) {
         k.D = c["D"].cast<int>();
         k.n_rot = c["n_rot"].cast<int>();
         k.F = c["F"].cast<int>();
+        k.F_valid = c.contains("F_valid") ? c["F_valid"].cast<int>() : 0;
         k.n_layer = c["n_layer"].cast<int>();
         k.V = c["V"].cast<int>();
         k.eps = c["eps"].cast<float>();

@@ -207,15 +207,16 @@ static void q6k_split_qh(const uint8_t* qh, uint8_t* dst, int64_t piece_stride) 
 }
 
 void repack_rows(const uint8_t* src, int qtype, int64_t K_src, const int64_t* rows, const int64_t* dst_rows,
-                 int64_t n_rows, int64_t kb0, int64_t kb1, uint8_t* const dst[4], int n_threads) {
+                 int64_t n_rows, int64_t kb0, int64_t kb1, uint8_t* const dst[4], int n_threads, int64_t K_out) {
   int blk, nb;
   block_geom(qtype, blk, nb);
   const int64_t nblk_src = K_src / blk;
   if (kb0 < 0 || kb1 > nblk_src || kb0 >= kb1) throw std::runtime_error("repack: bad K block range");
   const int64_t K = (kb1 - kb0) * blk;
-  const int64_t SB = (K + 255) / 256;
+  if (K_out < K) K_out = K;
+  const int64_t SB = (K_out + 255) / 256;  // the destination's super-blocks per row (stride of every stream)
   int64_t sb[4];
-  stream_bytes(qtype, K, sb);
+  stream_bytes(qtype, K_out, sb);
   const int64_t row_bytes = nblk_src * nb;
   auto work = [&](int64_t r0, int64_t r1) {
     for (int64_t r = r0; r < r1; ++r) {

@@ -46,7 +46,10 @@ class GGUFMap {
 // Repack source rows `rows[0..n_rows)` of a block-quantized matrix with K_src weights per row,
 // keeping K blocks [kb0, kb1), into the device stream layout (qmat.h) at dst[0..3]; source row
 // rows[i] lands in destination row dst_rows[i] (or i when dst_rows is null).
+// K_out > K: the destination rows hold K_out weights (whole super-blocks); the blocks past K stay as the
+// caller zeroed them (zero codes and scales: zero weights). The GPU loader pads ffn_down's K this way so
+// every piece run of the decode GEMV starts on a 256-B boundary (Llama-2-7B: 43 -> 48 super-blocks).
 void repack_rows(const uint8_t* src, int qtype, int64_t K_src, const int64_t* rows, const int64_t* dst_rows,
-                 int64_t n_rows, int64_t kb0, int64_t kb1, uint8_t* const dst[4], int n_threads);
+                 int64_t n_rows, int64_t kb0, int64_t kb1, uint8_t* const dst[4], int n_threads, int64_t K_out = 0);
 
 }  // namespace omx

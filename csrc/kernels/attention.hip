@@ -10,8 +10,8 @@
 //    are 4 key groups, the block's 32 groups x U = 4 slots (2 when G = 8) stream 128 keys per step.
 //  * Software pipeline: the next step's K/V loads are in flight while the current step computes
 //    (explicit register ping-pong), so a long range costs one HBM round trip, not one per step.
-//  * The split's slice of the block table is staged in LDS up front: K/V addresses never wait on a
-//    dependent global load inside the loop.
+//  * The page entries of a step are loaded into registers one step ahead of its K/V loads (the first
+//    step's right at entry, ahead of q): no LDS staging or barrier sits in front of the first K/V load.
 //  * q.k reductions are 16-lane DPP sums (no LDS permutes); the online softmax is batched per step
 //    (one max/rescale per 4 keys).
 //  * Flash-decode split count is decided ON DEVICE from the length: S_eff = min(n_splits,
@@ -38,7 +38,6 @@ void set_attn_tuning(int kps, int hpb) {
   if (kps >= 16) g_attn_kps = kps;
   if (hpb >= 0) g_attn_hpb = hpb;
 }
-constexpr int ATT_BTW = 1024;           // block-table entries staged in LDS per window
 
 template <int CTRL>
 __device__ __forceinline__ float dppf(float v) {
@@ -179,7 +178,6 @@ __global__ __launch_bounds__(ATT_NT) void attn_decode_kernel(AttnParams P) {
   constexpr int ATT_U = U, ATT_STEP = NG * U;
   constexpr bool RAW = KV8 && DPL % 4 == 0;
   __shared__ float sm[ATT_NW][G][D + 2];
-  __shared__ int sbt[ATT_BTW];
   const int qi = blockIdx.x, split = blockIdx.z;
   const int kvh = blockIdx.y / (P.H / P.n_kv / G);  // KV head of this block's G query heads
   const int h0 = blockIdx.y * G;                    // first query head of the block
@@ -199,20 +197,6 @@ __global__ __launch_bounds__(ATT_NT) void attn_decode_kernel(AttnParams P) {
 
   const int Dv = P.Dv > 0 ? P.Dv : D;  // valid dims: q / output head stride; dims >= Dv are padding
   float q[G][DPL];
-#pragma unroll
-  for (int g = 0; g < G; ++g) {
-    const float* qp = P.q + (long long)qi * P.ldq + (h0 + g) * Dv;
-    if (Dv == D) {  // unpadded head: plain loads (a per-element select makes hipcc wait per load)
-#pragma unroll
-      for (int j = 0; j < DPL; ++j) q[g][j] = qp[li * DPL + j] * P.scale;
-    } else {
-#pragma unroll
-      for (int j = 0; j < DPL; ++j) {
-        const int d = li * DPL + j;  // clamped load, then zero: padded K dims never contribute
-        q[g][j] = qp[min(d, Dv - 1)] * (d < Dv ? P.scale : 0.f);
-      }
-    }
-  }
   float m[G], l[G], acc[G][DPL];
 #pragma unroll
   for (int g = 0; g < G; ++g) {
@@ -222,26 +206,48 @@ __global__ __launch_bounds__(ATT_NT) void attn_decode_kernel(AttnParams P) {
     for (int j = 0; j < DPL; ++j) acc[g][j] = 0.f;
   }
   const int* bt = P.block_table + (long long)seq * P.max_blocks;
-  const f16* kc = (const f16*)P.kc;
-  const f16* vc = (const f16*)P.vc;
   const int bs = P.bs;
+  // page arithmetic: shifts for the power-of-two page sizes the runner uses (a runtime division per
+  // key slot sat in the dependent address chain), division otherwise (uniform branch)
+  const bool p2 = (bs & (bs - 1)) == 0;
+  const int bsh = __ffs(bs) - 1;
 
-  // block-table windows (one window covers ATT_BTW * bs keys; a single one in practice)
-  for (int w0 = t0; w0 < t1; w0 += ATT_BTW * bs) {
-    const int w1 = min(t1, w0 + ATT_BTW * bs);
-    const int b0 = w0 / bs, nb = (w1 - 1) / bs - b0 + 1;
-    __syncthreads();  // previous window's readers are done with sbt
-    OMX_KASSERT(nb <= ATT_BTW && b0 + nb <= P.max_blocks);
-    for (int i = threadIdx.x; i < nb; i += ATT_NT) sbt[i] = bt[b0 + i];
-    __syncthreads();
+  auto load_q = [&]() {
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const float* qp = P.q + (long long)qi * P.ldq + (h0 + g) * Dv;
+      if (Dv == D) {  // unpadded head: plain loads (a per-element select makes hipcc wait per load)
+#pragma unroll
+        for (int j = 0; j < DPL; ++j) q[g][j] = qp[li * DPL + j] * P.scale;
+      } else {
+#pragma unroll
+        for (int j = 0; j < DPL; ++j) {
+          const int d = li * DPL + j;  // clamped load, then zero: padded K dims never contribute
+          q[g][j] = qp[min(d, Dv - 1)] * (d < Dv ? P.scale : 0.f);
+        }
+      }
+    }
+  };
 
-    auto issue = [&](int ts, KVStep<DPL, U, RAW>& st) {
+  if (t0 < t1) {
+    // The page of every key slot of a step is loaded straight into registers one step ahead (no LDS
+    // staging and no barrier before the first K/V load), and q is requested behind the first K/V issue:
+    // the probe (experiments/attn_probe, profiles/r6_attn) timed the old staged prologue at 1.0 us of
+    // the 5.7 us of a 150-key launch
+    // lane li < U of a key group loads the page of the group's slot li; issue() takes slot u's page from
+    // lane (group base + u) -- one register per step instead of U (the fp8 / D = 112 / G >= 4 kernels
+    // would spill U pages twice over)
+    auto ldbt = [&](int s0) {
+      const int t = min(s0 + (li & (ATT_U - 1)) * NG + grp, t1 - 1);
+      return bt[p2 ? t >> bsh : t / bs];
+    };
+    auto issue = [&](int s0, int pl, KVStep<DPL, U, RAW>& st) {
 #pragma unroll
       for (int u = 0; u < ATT_U; ++u) {
-        const int t = min(ts + u * NG + grp, w1 - 1);  // clamped; masked at use
-        const long long blk = sbt[t / bs - b0];
-        OMX_KASSERT(t >= 0 && t / bs - b0 < nb && blk >= 0);
-        const long long base = ((blk * P.n_kv + kvh) * bs + (t % bs)) * D + li * DPL;
+        const int t = min(s0 + u * NG + grp, t1 - 1);  // clamped; masked at use
+        const long long blk = __shfl(pl, (lane & ~(LPK - 1)) + u, 64);
+        OMX_KASSERT(t >= 0 && blk >= 0 && (p2 ? t >> bsh : t / bs) < P.max_blocks);
+        const long long base = ((blk * P.n_kv + kvh) * bs + (p2 ? t & (bs - 1) : t % bs)) * D + li * DPL;
         if constexpr (RAW) {
           load_krow8_raw<DPL>((const uint8_t*)P.kc + base, st.k[u]);
           load_krow8_raw<DPL>((const uint8_t*)P.vc + base, st.v[u]);
@@ -249,16 +255,16 @@ __global__ __launch_bounds__(ATT_NT) void attn_decode_kernel(AttnParams P) {
           load_krow8<DPL>((const uint8_t*)P.kc + base, st.k[u]);
           load_krow8<DPL>((const uint8_t*)P.vc + base, st.v[u]);
         } else {
-          load_krow<DPL>(kc + base, st.k[u]);
-          load_krow<DPL>(vc + base, st.v[u]);
+          load_krow<DPL>((const f16*)P.kc + base, st.k[u]);
+          load_krow<DPL>((const f16*)P.vc + base, st.v[u]);
         }
       }
     };
-    auto consume = [&](int ts, const KVStep<DPL, U, RAW>& st) {
+    auto consume = [&](int s0, const KVStep<DPL, U, RAW>& st) {
       float sc[ATT_U][G];
 #pragma unroll
       for (int u = 0; u < ATT_U; ++u) {
-        const bool ok = ts + u * NG + grp < w1;  // uniform within the key's lane group
+        const bool ok = s0 + u * NG + grp < t1;  // uniform within the key's lane group
         float kf[DPL];
         row_f32(st.k[u], kf);
 #pragma unroll
@@ -306,17 +312,26 @@ __global__ __launch_bounds__(ATT_NT) void attn_decode_kernel(AttnParams P) {
     };
 
     KVStep<DPL, U, RAW> A, B;
-    int ts = w0;
-    issue(ts, A);
-    while (true) {
-      if (ts + ATT_STEP < w1) issue(ts + ATT_STEP, B);
-      consume(ts, A);
-      ts += ATT_STEP;
-      if (ts >= w1) break;
-      if (ts + ATT_STEP < w1) issue(ts + ATT_STEP, A);
-      consume(ts, B);
-      ts += ATT_STEP;
-      if (ts >= w1) break;
+    int pA = ldbt(t0), pB = 0;
+    issue(t0, pA, A);
+    if (t0 + ATT_STEP < t1) pB = ldbt(t0 + ATT_STEP);
+    load_q();
+    int s0 = t0;
+    while (true) {  // step s0 in A / B; the next step's K/V and the page entries of the one after in flight
+      if (s0 + ATT_STEP < t1) {
+        issue(s0 + ATT_STEP, pB, B);
+        if (s0 + 2 * ATT_STEP < t1) pA = ldbt(s0 + 2 * ATT_STEP);
+      }
+      consume(s0, A);
+      s0 += ATT_STEP;
+      if (s0 >= t1) break;
+      if (s0 + ATT_STEP < t1) {
+        issue(s0 + ATT_STEP, pA, A);
+        if (s0 + 2 * ATT_STEP < t1) pB = ldbt(s0 + 2 * ATT_STEP);
+      }
+      consume(s0, B);
+      s0 += ATT_STEP;
+      if (s0 >= t1) break;
     }
   }
 
@@ -636,6 +651,9 @@ static int heads_per_block(const AttnParams& P) {
   const int G = P.H / P.n_kv;
   int hpb = g_attn_hpb > 0 ? g_attn_hpb : (P.NQ * P.n_kv < 64 ? 1 : G);
   if (P.D > 128 && hpb > 2) hpb = 2;  // head dim 256: the per-wave merge tile [8][G][D + 2] fits LDS for G <= 2
+  // head dims 80 / 96 / 112 (an fp8 row of 5-7 bytes per lane is widened at load): at 4+ heads per block
+  // the kernel spills, so those dims take at most 2 (K/V re-reads of a wider group hit L2)
+  if (P.D % 64 && hpb > 2) hpb = 2;
   while (hpb > 1 && (G % hpb || (hpb != 1 && hpb != 2 && hpb != 4 && hpb != 8))) --hpb;
   return hpb < 1 ? 1 : hpb;
 }
@@ -648,8 +666,8 @@ static void launch_dk(const AttnParams& P, hipStream_t s) {
   switch (G) {
     case 1: hipLaunchKernelGGL((attn_decode_kernel<D, 1, KV8, LPK8>), grid, dim3(ATT_NT), 0, s, P); break;
     case 2: hipLaunchKernelGGL((attn_decode_kernel<D, 2, KV8, LPK8>), grid, dim3(ATT_NT), 0, s, P); break;
-    case 4: if constexpr (D <= 128) hipLaunchKernelGGL((attn_decode_kernel<D, 4, KV8>), grid, dim3(ATT_NT), 0, s, P); break;
-    case 8: if constexpr (D <= 128) hipLaunchKernelGGL((attn_decode_kernel<D, 8, KV8>), grid, dim3(ATT_NT), 0, s, P); break;
+    case 4: if constexpr (D <= 128 && D % 64 == 0) hipLaunchKernelGGL((attn_decode_kernel<D, 4, KV8>), grid, dim3(ATT_NT), 0, s, P); break;
+    case 8: if constexpr (D <= 128 && D % 64 == 0) hipLaunchKernelGGL((attn_decode_kernel<D, 8, KV8>), grid, dim3(ATT_NT), 0, s, P); break;
     default: break;
   }
 }

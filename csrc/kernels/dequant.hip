@@ -1,6 +1,7 @@
 // Row gather + dequantisation from the repacked quant streams (SURVEY.md §2.2 N15 embedding
 // gather) and whole-matrix dequantisation to fp16 (resident fp16 copies for MFMA prefill GEMMs).
 #include "common.h"
+#include "gemv8_core.h"
 #include "ops.h"
 
 namespace omx {
@@ -10,23 +11,41 @@ namespace omx {
 // models/clip.py) enter the sequence as such rows.
 // stat (optional, the batched fp16 decode chain): per-16-element sum-of-squares partials [n][K / 16] of
 // the gathered rows, the "residual before the add" of layer 0's O emission (gemv_mfma.hip range scale)
+// one 16-element group of a gathered row into layer 0's int8 input image (img8 != null)
+__device__ __forceinline__ void embed_emit(void* img8, const float* nw, float* ist, int K, int G, const float* v) {
+  float xv[16], sq[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    xv[j] = v[j] * nw[16 * G + j];
+    sq[j] = v[j] * v[j];
+  }
+  emit_group(img8, K, G, xv, sq, ist);
+}
+
 __global__ __launch_bounds__(256) void embed_rows_kernel(QMat w, const int* rows, float* out, int ldo, float scale,
-                                                         const float* ext, float* stat) {
+                                                         const float* ext, float* stat, void* img8, const float* img_nw,
+                                                         float* img_stat) {
   const int b = blockIdx.x;
   const long long row = rows[b];
   const int P = w.K / 32;
   float* o = out + (long long)b * ldo;
   float* st = stat ? stat + (long long)b * (w.K / 16) : nullptr;
+  void* im = img8 ? (char*)img8 + (size_t)b * x8_slots_dev(w.K) * 24 : nullptr;
+  float* ist = img8 ? img_stat + (size_t)b * x8_stat_ld_dev(w.K) : nullptr;
   if (row < 0) {
     const float* src = ext + (-row - 1) * (long long)w.K;
     OMX_KASSERT(ext != nullptr);
     for (int i = threadIdx.x; i < w.K; i += blockDim.x) o[i] = ext ? src[i] : 0.f;
-    if (st) {
-      for (int g = threadIdx.x; g < w.K / 16; g += blockDim.x) {
-        float s = 0.f;
-        for (int i = 0; i < 16; ++i) s += ext ? src[16 * g + i] * src[16 * g + i] : 0.f;
-        st[g] = s;
+    for (int g = threadIdx.x; g < w.K / 16; g += blockDim.x) {
+      float v[16];
+      float s = 0.f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        v[i] = ext ? src[16 * g + i] : 0.f;
+        s += v[i] * v[i];
       }
+      if (st) st[g] = s;
+      if (im) embed_emit(im, img_nw, ist, w.K, g, v);
     }
     return;
   }
@@ -51,13 +70,19 @@ __global__ __launch_bounds__(256) void embed_rows_kernel(QMat w, const int* rows
       st[olo >> 4] = slo;
       st[ohi >> 4] = shi;
     }
+    if (im) {  // a piece's halves are whole 16-groups: each emitted by the thread that holds it
+      embed_emit(im, img_nw, ist, w.K, olo >> 4, lo);
+      embed_emit(im, img_nw, ist, w.K, ohi >> 4, hi);
+    }
   }
 }
 
 void embed_rows(const QMat& w, const int* rows, int n, float* out, int ldo, hipStream_t s, float scale,
-                const float* ext, float* stat) {
+                const float* ext, float* stat, void* img8, const float* img_nw, float* img_stat) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(embed_rows_kernel, dim3(n), dim3(256), 0, s, w, rows, out, ldo, scale, ext, stat);
+  if (img8 && (!img_nw || !img_stat || w.K % 16)) img8 = nullptr;
+  hipLaunchKernelGGL(embed_rows_kernel, dim3(n), dim3(256), 0, s, w, rows, out, ldo, scale, ext, stat, img8, img_nw,
+                     img_stat);
 }
 
 // rows on blockIdx.y (grid-stride), pieces of a row on x (no 64-bit index division per piece); PERM:

@@ -535,41 +535,25 @@ bool gemm_eligible(const GemvParams& P) {
 
 // Large-M library path (blas.cpp): dequantise W once into fp16 (in prep_x16's K order), one hipBLASLt
 // GEMM into the fp32 slab yws, then the fused epilogue as for split-K (finalize, one slab)
-// -1: OMX_GEMM_LIB_MIN_M, read once. Default 2048: a 2048-row prefill chunk takes hipBLASLt (QKV, O,
-// down: 749 / 667 / 730-763 TFLOP/s against the dq kernel's 638 / 544 / 572-623, profiles/r5_gemm);
-// 2048-token TTFT 46.1 -> 42.4-43.2 ms (7B), 89.8 -> 72.8-73.3 (13B), profiles/r5_gemm lib_default/
+// -1: OMX_GEMM_LIB_MIN_M, read once. Default 0: prefill GEMMs never take the library. Round 6 made the
+// hand-written dequant GEMM (gemm_dq.hip, register-ring edition) the only default path: the resident fp16
+// weight copies that made hipBLASLt worth it (12.95 GB for 7B, 3.2x the model) are gone, and the per-call
+// library path (dequantise W into fp16 scratch, GEMM, finalize) loses or ties at 2048 rows
+// (profiles/r6_gemm). OMX_GEMM_LIB_MIN_M=<rows> keeps it reachable for A/B runs and the test oracle.
 static int g_lib_min_m = -1;
-// OMX_GEMM_LIB_GLU (default 1): 0 keeps the gate_up GEMMs on the dq kernel (it wins the 7B shape per
-// call, 747 vs 690 TFLOP/s, but the 7B TTFT was a tie, 43.3 vs 43.2, and 13B lost 77.3 vs 73.3)
+// OMX_GEMM_LIB_GLU (default 1): 0 keeps the gate_up GEMMs on the dq kernel when the library path is on
 static int g_lib_glu = -1;
 
 int gemm_lib_min_m() {
   if (g_lib_min_m < 0) {
     const char* e = getenv("OMX_GEMM_LIB_MIN_M");
-    g_lib_min_m = e ? atoi(e) : 2048;
+    g_lib_min_m = e ? atoi(e) : 0;
   }
   return g_lib_min_m;
 }
 
-// with a resident fp16 copy (no per-call dequantisation) the library path starts at 128 rows
-// (OMX_GEMM_LIB_MIN_M_F16): 7B TTFT 17.2 -> 15.0 ms at 512 tokens, 26.3 -> 20.0 at 1024, and from 128
-// instead of 512 rows 10.1 -> 9.3 ms at 128 tokens, 11.8-12.3 -> 11.0-11.1 at 256
-// (profiles/r5_gemm/lib_default/threshold/)
-static int g_lib_min_m_res = -1;
-
-int gemm_lib_min_m_res() {
-  if (g_lib_min_m_res < 0) {
-    const char* e = getenv("OMX_GEMM_LIB_MIN_M_F16");
-    g_lib_min_m_res = e ? atoi(e) : 128;
-  }
-  return g_lib_min_m_res;
-}
-
 // rows from which this matrix's prefill GEMM takes hipBLASLt (0 = never)
-static int lib_min_for(const QMat& w) {
-  const int lm = gemm_lib_min_m();
-  return lm > 0 && w.f16 ? std::min(lm, gemm_lib_min_m_res()) : lm;
-}
+static int lib_min_for(const QMat&) { return gemm_lib_min_m(); }
 
 static bool lib_glu() {
   if (g_lib_glu < 0) {
@@ -584,17 +568,13 @@ void set_gemm_lib_min_m(int m) { g_lib_min_m = m; }
 static bool gemm_lib(const GemvParams& P, const f16* x16, hipStream_t s) {
   const int lm = lib_min_for(P.w);
   const long long M = P.B, N = P.w.N, K = P.w.K;
-  // M >= lm (256). Taking the wide QKV / gate_up matrices from 128 rows (where the library GEMM wins
-  // per call, 66 -> 60 / 109 -> 90 us) left the 128-token TTFT unchanged (11.3 vs 12.3 ms), so no
-  // a resident fp16 copy (QMat.f16, runner OMX_PREFILL_F16) skips the per-call dequantisation
-  const bool res = P.w.f16 != nullptr;
   if (lm <= 0 || M < lm || !P.yws || M * N > P.yws_elems) return false;
-  if (!res && (!P.w16ws || N * K > P.w16_elems)) return false;
+  if (!P.w16ws || N * K > P.w16_elems) return false;
   const long long xcap = P.xws_elems ? P.xws_elems / K : M, ycap = P.yws_elems / N;
   const int m_cap = (int)(xcap < ycap ? xcap : ycap);
   if (!blas_plan_ok((int)M, (int)N, (int)K, P.gws ? (size_t)P.gws_elems * 4 : 0, m_cap)) return false;
-  if (!res) dequant_f16(P.w, P.w16ws, s, 1);
-  if (!blas_gemm_tn(res ? P.w.f16 : P.w16ws, x16, P.yws, (int)M, (int)N, (int)K, P.gws, P.gws ? (size_t)P.gws_elems * 4 : 0, s,
+  dequant_f16(P.w, P.w16ws, s, 1);
+  if (!blas_gemm_tn(P.w16ws, x16, P.yws, (int)M, (int)N, (int)K, P.gws, P.gws ? (size_t)P.gws_elems * 4 : 0, s,
                     m_cap))
     throw std::runtime_error("gemm_lib: hipBLASLt matmul failed after its plan was accepted");
   GemvParams F = P;

@@ -11,6 +11,7 @@ int g_dq_enable = -1;  // -1: OMX_GEMM_DQ (default on), read once
 int g_dq_cfg = -2;     // OMX_DQ_CFG: force tile config 0..3 (microbenchmarks); -2 = not read yet
 int g_dq_sk = 0;       // > 0: force the split-K factor (microbenchmarks, set_dq_tuning)
 int g_dq_dbg = 0;      // OMX_DQ_DBG=1: no operand reloads after the first K step (timing probe only)
+int g_dq_ring = 1;     // OMX_DQ_RING (default 1): the register-ring kernel (gemm_dq_impl.h), 0 = the glds one
 
 void run_dq_q4k(const GemvParams& P, f16* xp, int Kp, hipStream_t s);  // gemm_dq_q4k.hip
 void run_dq_q5k(const GemvParams& P, f16* xp, int Kp, hipStream_t s);  // gemm_dq_q5k.hip
@@ -29,11 +30,18 @@ bool dq_gemm_enabled() {
     g_dq_cfg = c ? atoi(c) : -1;
     const char* d = getenv("OMX_DQ_DBG");
     g_dq_dbg = d ? atoi(d) : 0;
+    const char* r = getenv("OMX_DQ_RING");
+    g_dq_ring = r ? atoi(r) : g_dq_ring;
   }
   return g_dq_enable != 0;
 }
 
 void set_dq_gemm(int on) { g_dq_enable = on ? 1 : 0; }
+
+void set_dq_ring(int on) {
+  dq_gemm_enabled();  // env defaults read first, then overridden
+  g_dq_ring = on ? 1 : 0;
+}
 
 void set_dq_tuning(int cfg, int sk) {
   dq_gemm_enabled();  // env defaults read first, then overridden

@@ -485,6 +485,157 @@ __global__ __launch_bounds__(DQ_NT, 1) void dq_gemm_kernel(GemvParams P, const f
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Register-ring edition (round 6): both operands are staged through registers, two K steps deep, and
+// written into the LDS double buffer after the barrier (the guide's T14 form). The glds edition above
+// issues the X DMA one step ahead, and every `__syncthreads()` drains the vector-memory queue while a
+// glds is in flight: each K step then waits for loads issued only one compute phase earlier (~0.9 us
+// of MFMA work at 2 waves per SIMD against a 1-3 us loaded HBM round trip), which is what held the
+// 256 x 256 tile at ~2.2 us per K step (profiles/r4_gemm). With plain loads the barrier is a bare
+// s_barrier, the compiler's counted vmcnt waits only for the slot being written, and every load has
+// two compute phases to land. Same LDS image, fragments, MFMA shape and epilogues as the glds kernel.
+template <int QT, int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__(DQ_NT, 1) void dq_gemm_ring_kernel(GemvParams P, const f16* __restrict__ X, int Kp, int sk) {
+  static_assert(WM * WN == 8, "8 waves");
+  constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
+  constexpr int XS = BM * DQ_BK, WS = BN * DQ_BK;
+  constexpr int XL = BM / 64;  // 16-B X chunks per thread per K step (BM rows x 8 chunks / 512 threads)
+  static_assert(TM >= 1 && TN >= 1 && BN * 2 <= DQ_NT && XL >= 1, "tile shape");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  f16* Xs = (f16*)smem;     // [2][BM][64] swizzled
+  f16* Ws = Xs + 2 * XS;    // [2][BN][64] swizzled
+
+  const QMat& w = P.w;
+  const int M = P.B, N = w.N, SB = Kp >> 8, nks = SB * 4;
+  const unsigned sbinv = (0xFFFFFFFFu / (unsigned)SB) + 1u;
+  const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int z = wg % sk, tile = wg / sk;
+  const int nt = (N + BN - 1) / BN;
+  const int m0 = (tile / nt) * BM, n0 = (tile % nt) * BN;
+  const int ks0 = (int)((long long)z * nks / sk), ks1 = (int)((long long)(z + 1) * nks / sk);
+
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int wr = tid >> 1, wh = tid & 1;
+  const bool wact = BN * 2 >= DQ_NT || wr < BN;
+  const long long wrow = min(n0 + wr, N - 1);
+  // X chunk i of this thread: row xr + 64 i, 16-B column chunk xc (8 threads cover a 128-B row)
+  const int xr = tid >> 3, xc = tid & 7;
+  const f16* xsrc[XL];
+#pragma unroll
+  for (int i = 0; i < XL; ++i) xsrc[i] = X + (long long)min(m0 + xr + 64 * i, M - 1) * Kp + 8 * xc;
+
+  u32x4 xa[XL], xb[XL];
+  Piece<QT> wa, wb;
+  auto load_x = [&](int ks, u32x4 (&xv)[XL]) {
+#pragma unroll
+    for (int i = 0; i < XL; ++i) xv[i] = *(const u32x4*)(xsrc[i] + ks * DQ_BK);
+  };
+  auto load_w = [&](int ks, Piece<QT>& wp) {
+    if (wact) load_piece<QT>(w, wrow, SB, 2 * ks + wh, wp);
+  };
+  auto write = [&](int ks, const u32x4 (&xv)[XL], const Piece<QT>& wp, int buf) {
+    f16* xd = Xs + buf * XS;
+#pragma unroll
+    for (int i = 0; i < XL; ++i) *(u32x4*)(xd + swz(xr + 64 * i, xc)) = xv[i];
+    if (wact) {
+      const int pc = 2 * ks + wh;
+      unsigned o[16];
+      dq_piece<QT>(wp, SB == 1 ? pc : (int)__umulhi((unsigned)pc, sbinv), o);
+      f16* wd = Ws + buf * WS;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        *(u32x4*)(wd + swz(wr, 4 * wh + i)) = (u32x4){o[4 * i], o[4 * i + 1], o[4 * i + 2], o[4 * i + 3]};
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  const int wm = wave / WN, wn = wave % WN;
+  const int fr = lane & 31, fq = lane >> 5;
+  auto compute = [&](int buf) {
+    const f16* xbp = Xs + buf * XS;
+    const f16* wbp = Ws + buf * WS;
+#pragma unroll
+    for (int kk = 0; kk < DQ_BK / 16; ++kk) {
+      f16x8 a[TM], b[TN];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) b[j] = *(const f16x8*)(wbp + swz(wn * (BN / WN) + 32 * j + fr, 2 * kk + fq));
+#pragma unroll
+      for (int i = 0; i < TM; ++i) a[i] = *(const f16x8*)(xbp + swz(wm * (BM / WM) + 32 * i + fr, 2 * kk + fq));
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[i], b[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  };
+
+  // ring: before the even half of a trip, LDS buffer 0 holds step ks, registers b hold step ks + 1 and
+  // registers a hold step ks + 2; each half writes the next step from the registers that have waited
+  // longest, reloads them with the step two ahead, then computes (steps past the end are clamped: a
+  // redundant load, a write into a buffer nobody reads)
+  const int kl = ks1 - 1;
+  load_x(ks0, xa);
+  load_w(ks0, wa);
+  load_x(min(ks0 + 1, kl), xb);
+  load_w(min(ks0 + 1, kl), wb);
+  write(ks0, xa, wa, 0);
+  load_x(min(ks0 + 2, kl), xa);
+  load_w(min(ks0 + 2, kl), wa);
+  // two steps per trip and no branch inside it: a mid-trip exit split the trip into blocks, and at that
+  // join hipcc waited vmcnt(0) for the step that had just been issued
+  int ks = ks0;
+  for (; ks + 1 < ks1; ks += 2) {
+    __syncthreads();  // buffer 0 holds step ks; buffer 1's readers (step ks - 1) are done
+    write(ks + 1, xb, wb, 1);
+    load_x(min(ks + 3, kl), xb);
+    load_w(min(ks + 3, kl), wb);
+    compute(0);
+    __syncthreads();  // buffer 1 holds step ks + 1; buffer 0's readers are done
+    write(min(ks + 2, kl), xa, wa, 0);
+    load_x(min(ks + 4, kl), xa);
+    load_w(min(ks + 4, kl), wa);
+    compute(1);
+  }
+  if (ks < ks1) {  // odd step count: the last step sits in buffer 0
+    __syncthreads();
+    compute(0);
+  }
+
+  const int nb = n0 + wn * (BN / WN) + fr;
+  const int mb = m0 + wm * (BM / WM) + 4 * fq;
+  if (sk > 1) {
+    float* slab = P.gws + (long long)z * M * N;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int gm = mb + 32 * i + (r & 3) + 8 * (r >> 2), gn = nb + 32 * j;
+          if (gm < M && gn < N) __builtin_nontemporal_store(acc[i][j][r], slab + (long long)gm * N + gn);
+        }
+    return;
+  }
+  switch (P.epi) {
+    case EPI_STORE: dq_out<EPI_STORE, TM, TN>(P, acc, mb, nb, M, N); break;
+    case EPI_ADD: dq_out<EPI_ADD, TM, TN>(P, acc, mb, nb, M, N); break;
+    case EPI_GELU: dq_out<EPI_GELU, TM, TN>(P, acc, mb, nb, M, N); break;
+    case EPI_GLU: dq_out<EPI_GLU, TM, TN>(P, acc, mb, nb, M, N); break;
+    case EPI_GEGLU: dq_out<EPI_GEGLU, TM, TN>(P, acc, mb, nb, M, N); break;
+    case EPI_GELU_ERF: dq_out<EPI_GELU_ERF, TM, TN>(P, acc, mb, nb, M, N); break;
+    case EPI_QGELU: dq_out<EPI_QGELU, TM, TN>(P, acc, mb, nb, M, N); break;
+    default: dq_out<EPI_QKV, TM, TN>(P, acc, mb, nb, M, N); break;
+  }
+}
+
 template <int BM, int BN>
 constexpr size_t dq_lds() { return (size_t)(2 * BM + 2 * BN) * DQ_BK * sizeof(f16); }
 
@@ -493,6 +644,7 @@ constexpr size_t dq_lds() { return (size_t)(2 * BM + 2 * BN) * DQ_BK * sizeof(f1
 extern int g_dq_cfg;  // gemm_dq.hip: forced tile config (microbenchmarks), -1 auto
 extern int g_dq_dbg;  // gemm_dq.hip: OMX_DQ_DBG microbenchmark mode (no operand reloads), 0 in production
 extern int g_dq_sk;   // gemm_dq.hip: forced split-K factor (microbenchmarks), 0 auto
+extern int g_dq_ring;  // gemm_dq.hip: 1 = the register-ring kernel (OMX_DQ_RING), 0 = the glds kernel
 
 namespace {
 
@@ -500,6 +652,16 @@ template <int QT, int BM, int BN, int WM, int WN>
 void launch_dq(const GemvParams& P, const f16* xp, int Kp, int sk, hipStream_t s) {
   const int mt = (P.B + BM - 1) / BM, nt = (P.w.N + BN - 1) / BN;
   const size_t lds = dq_lds<BM, BN>();
+  // the Q6_K piece (codes + high bits + scales + d) in a two-deep ring at 256 x 256 exceeds 256 VGPRs
+  // (268 B/lane of scratch): that one tile stays on the glds kernel
+  constexpr bool ring_ok = !(QT == QT_Q6_K && BM == 256 && BN == 256);
+  if constexpr (ring_ok) {
+    if (g_dq_ring && !g_dq_dbg) {
+      hipLaunchKernelGGL((dq_gemm_ring_kernel<QT, BM, BN, WM, WN>), dim3(mt * nt * sk), dim3(DQ_NT), lds, s, P, xp, Kp,
+                         sk);
+      return;
+    }
+  }
   hipLaunchKernelGGL((dq_gemm_kernel<QT, BM, BN, WM, WN>), dim3(mt * nt * sk), dim3(DQ_NT), lds, s, P, xp, Kp, sk,
                      g_dq_dbg);
 }

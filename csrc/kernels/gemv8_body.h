@@ -137,7 +137,10 @@ __device__ __forceinline__ void gemv8_body(const GemvParams& P, const int bx) {
   const int kg = KS > 1 ? wave / GEMV_NW : 0, gtid = tid - kg * GEMV_NT;
   // K-split groups (ks_chunk): aligned to 16 super-blocks when the row stride keeps piece runs on lines
   const int CH = ks_chunk(SB, KS);
-  const int sb0 = kg * CH, se = min(SB, sb0 + CH);
+  // lanes stop at the last super-block holding weights: a padded K (weights.py ffn_pad) keeps its runs
+  // line-aligned without streaming the zero super-blocks
+  const int SBv = P.k_valid > 0 && P.k_valid < K ? n_sb(P.k_valid) : SB;
+  const int sb0 = kg * CH, se = min(SBv, sb0 + CH);
   const int n_tiles = (N + 15) / 16;
   const int rbase = (wave - kg * GEMV_NW) * 4 + g;
   const int tile0 = bx * J;
@@ -377,7 +380,8 @@ __device__ __forceinline__ void gemv8_body(const GemvParams& P, const int bx) {
           __syncthreads();
           if (tid < 16 * nb) {
             const int b = tid >> 4, i = tid & 15;
-            emit_group16((char*)P.emit8 + (size_t)b * x8_slots_dev(N / 2) * 24, N / 2, t >> 1, stage[32 * b + i], 0.f,
+            const int Kc = P.emit8_k > 0 ? P.emit8_k : N / 2;  // the consumer's (possibly padded) K
+            emit_group16((char*)P.emit8 + (size_t)b * x8_slots_dev(Kc) * 24, Kc, t >> 1, stage[32 * b + i], 0.f,
                          nullptr, i);
           }
           __syncthreads();

@@ -108,6 +108,10 @@ struct GemvParams {
   void* emit8;                 // producer: image of this GEMV's output (EPI_ADD: new residual * emit8_nw;
   const float* emit8_nw;       //   EPI_GLU / EPI_GEGLU: the GLU output)
   float* emit8_stat;           //   EPI_ADD: per-16-row sum-of-squares partials of the new residual
+  int k_valid;                 // K columns holding weights (0 = K): ffn_down's zero padding past it is not
+                               // streamed by the int8-chain GEMV (gemv8_body.h)
+  int emit8_k;                 //   EPI_GLU: K of the consumer's image (0 = N / 2; larger when ffn_down's K is
+                               //   padded: the image slots past N / 2 stay zero)
   int dbg8;                    // microbenchmarks only (scripts/bench_gemv8.py): 1 = gemv8 memory path alone
                                // (weights loaded and folded, no dot products); 0 in production
 };
@@ -132,8 +136,6 @@ constexpr int GEMM_MIN_B = 16;
 // prefill rows from which the library GEMM path is taken (0 = never); OMX_GEMM_LIB_MIN_M overrides
 void set_gemm_lib_min_m(int m);
 int gemm_lib_min_m();
-// the same for matrices with a resident fp16 copy (QMat.f16): min(gemm_lib_min_m(), this)
-int gemm_lib_min_m_res();
 // D[M][N] (fp32, row-major) = X[M][K] . W[N][K]^T, X and W fp16 row-major, on hipBLASLt; false when
 // no algorithm fits (the caller falls back)
 // m_cap: rows of x16 / d the buffers hold (>= M); when the M-bucket's algorithm does not accept M
@@ -160,6 +162,7 @@ void gemm(const GemvParams& P, hipStream_t s);
 bool dq_gemm(const GemvParams& P, hipStream_t s);
 bool dq_gemm_enabled();
 void set_dq_gemm(int on);
+void set_dq_ring(int on);  // 1: the register-ring dq kernel (gemm_dq_impl.h), 0: the glds kernel
 void set_dq_tuning(int cfg, int sk);  // microbenchmarks: force tile config (-1 auto) and split-K (0 auto)
 void gemm_finalize(const GemvParams& P, int sk, hipStream_t s);  // sums sk split-K slabs + epilogue
 
@@ -178,8 +181,12 @@ void set_gemv_tuning(int blocks_per_cu, int rows, int debug, int ks = -1, int xf
 
 // Dequantize rows of a repacked matrix (embedding gather / fp16 copies)
 // rows[i] < 0: row -(rows[i] + 1) of ext [*][w.K] (external embeddings, e.g. image patches)
+// img8 / img_nw / img_stat (optional, the int8 decode chain): the gathered rows also go out as layer 0's
+// QKV input image (x8_bytes(K) per row: int8(row * img_nw) per 16-group + RMS partials, x8_stat_ld(K)
+// floats per row), exactly what the residual-adding producers emit for the later layers
 void embed_rows(const QMat& w, const int* rows, int n, float* out, int ldo, hipStream_t s, float scale = 1.f,
-                const float* ext = nullptr, float* stat = nullptr);
+                const float* ext = nullptr, float* stat = nullptr, void* img8 = nullptr, const float* img_nw = nullptr,
+                float* img_stat = nullptr);
 // rows [row0, row0 + w.N) of w (an expert's slice of a stacked MoE matrix); perm: prep_x16 K order
 void dequant_f16(const QMat& w, void* out_f16, hipStream_t s, int perm = 0, long long row0 = 0);
 

@@ -28,5 +28,4 @@ struct QMat {
   int N, K, qtype;
   const uint8_t* s4;  // optional widened Q6_K codes (QT_Q6_K8), null otherwise
   const uint8_t* mt;  // optional layout M copy for the batched MFMA decode GEMV (gemv_mfma.hip), or null
-  const void* f16;    // optional resident fp16 copy [N][K] in prep_x16's K order (the library prefill GEMM)
 };

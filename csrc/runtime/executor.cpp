@@ -94,6 +94,11 @@ bool Executor::x8(const StepInputs& in) const {
          cfg.arch == 0 && cfg.n_expert == 0;
 }
 
+// layer 0's QKV input image written by the embedding gather (E % 16 == 0, a dense llama-family stack)
+bool Executor::x8_layer0(const StepInputs& in) const {
+  return x8(in) && !layers.empty() && cfg.E % 16 == 0 && layers[0].attn_norm && ws.x8e && ws.x8st;
+}
+
 static void x8_in(GemvParams& P, const void* img, const float* stat) {
   P.x8 = img;
   P.x8_stat = stat;
@@ -141,7 +146,11 @@ bool Executor::x8_capable(int B) const {
 
 void Executor::embed(const StepInputs& in, hipStream_t s) {
   // the batched fp16 chain: the embedded rows' partials go to st[1], read by layer 0's O emission
-  embed_rows(tok_embd, in.tokens, in.B, ws.resid, cfg.E, s, cfg.embed_scale, ws.ext, chain(in) ? ws.st[1] : nullptr);
+  // the int8 chain: the gather also writes layer 0's QKV input image (x8_layer0), as the producers do
+  // for every later layer, so layer 0 takes the same int8 GEMV instead of the fp32-prologue one
+  const bool q8 = x8_layer0(in);
+  embed_rows(tok_embd, in.tokens, in.B, ws.resid, cfg.E, s, cfg.embed_scale, ws.ext, chain(in) ? ws.st[1] : nullptr,
+             q8 ? ws.x8e : nullptr, q8 ? layers[0].attn_norm : nullptr, q8 ? ws.x8st : nullptr);
 }
 
 void Executor::attn_block(int i, const StepInputs& in, hipStream_t s) {
@@ -175,7 +184,7 @@ void Executor::attn_block(int i, const StepInputs& in, hipStream_t s) {
   const bool q8 = x8(in);
   if (ch && i > 0) chain_in(P, ws.xa16, ws.ld_e, ws.st[1], (E + 15) / 16);  // emitted by layer i-1's down
   if (ch) P.rexp_out = ws.st[1] + 16 * ((E + 15) / 16) + 16;  // O's range exponents (layer 0: from resid)
-  if (q8 && i > 0) x8_in(P, ws.x8e, ws.x8st);                                 // emitted by layer i-1's down
+  if (q8 && (i > 0 || x8_layer0(in))) x8_in(P, ws.x8e, ws.x8st);  // emitted by layer i-1's down / the embed
   if (!L.qkv_fused) {  // q,k and v rows of different quant types: one dual launch at B == 1
     GemvParams V = P;
     V.w = L.wv;
@@ -385,11 +394,13 @@ void Executor::ffn_block(int i, const StepInputs& in, hipStream_t s) {
   if (q8) {
     x8_in(G, ws.x8e, ws.x8st);
     G.emit8 = ws.x8f;  // down's input
+    G.emit8_k = F;     // down's K (ffn_down padded to whole 16-super-block groups: weights.py ffn_pad)
   }
   GemvParams Dn = base_params(L.wdown, B, ws.hbuf, F, ws);
   Dn.epi = dst_epi;
   Dn.y = dst;
   Dn.ldy = E;
+  Dn.k_valid = cfg.F_valid;
   if (ch) {  // the next RMSNorm'd GEMV: layer i+1's QKV, or the LM head
     chain_in(Dn, ws.h16, ws.ld_f, nullptr, 0);
     chain_emit(Dn, ws.xa16, ws.ld_e, i + 1 < (int)layers.size() ? layers[i + 1].attn_norm : out_norm, ws.st[1],

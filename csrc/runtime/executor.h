@@ -23,6 +23,7 @@ struct ExecConfig {
   int tp = 1;            // >1: O/down projections write partial sums to ypart (caller all-reduces)
   float embed_scale = 1.f;  // token embeddings x this (Gemma: sqrt(E))
   int glu_act = 0;          // 0 SiLU-GLU, 1 GELU-GLU (Gemma GeGLU)
+  int F_valid = 0;          // FFN width before ffn_down's K padding (weights.py ffn_pad; 0 = F)
 };
 
 struct LayerW {
@@ -143,6 +144,7 @@ class Executor {
  private:
   float* tp_dst(int slab, int B) const;  // where a row-parallel projection leaves its partial sums
   bool chain(const StepInputs& in) const;  // this step runs the fp16 matrix-core decode chain
+  bool x8_layer0(const StepInputs& in) const;  // the embed writes layer 0's int8 QKV image
   bool x8(const StepInputs& in) const;     // this step runs the batch-1 int8 activation chain
   int ar_active_ = 0;
 };

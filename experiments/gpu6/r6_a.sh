@@ -4,7 +4,8 @@ set -o pipefail
 O=gpurun_out/r6_a
 mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 180 ./experiments/attn_probe/attn_probe > $O/attn_probe.log 2>&1 || { tail -30 $O/attn_probe.log; exit 1; }
+hipcc -O3 --offload-arch=gfx950 -std=c++17 -I csrc/kernels experiments/attn_probe/probe.hip -o /tmp/attn_probe || exit 1
+timeout -k 10 180 /tmp/attn_probe > $O/attn_probe.log 2>&1 || { tail -30 $O/attn_probe.log; exit 1; }
 cat $O/attn_probe.log
 timeout -k 10 500 python -u -m pytest tests/test_gemv8_gpu.py tests/test_engine_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1; rc=$?
 tail -3 $O/pytest_gpu.log

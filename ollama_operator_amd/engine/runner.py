@@ -49,7 +49,7 @@ class NativeExec:
                          n_rot=cfg.n_rot, F=loc["F"], n_layer=cfg.n_layer, V=loc["V"], eps=float(cfg.norm_eps),
                          n_expert=cfg.n_expert, n_expert_used=cfg.n_expert_used, window=cfg.sliding_window,
                          tp=r.tp_size, embed_scale=float(cfg.embed_scale), glu_act=int(cfg.gelu_glu),
-                         kv8=int(getattr(r, "kv8", False))))
+                         kv8=int(getattr(r, "kv8", False)), F_valid=loc["F"] - getattr(w, "ffn_pad", 0)))
         p = lambda t: t.data_ptr() if t is not None else 0  # noqa: E731
         e.set_globals(w.tok_embd.tup, p(w.out_norm), p(w.out_norm_b), w.lm_head.tup, p(w.lm_bias), p(w.inv_freq))
         for i, L in enumerate(w.layers):
@@ -162,17 +162,10 @@ class Runner:
         self.mfma_bytes = 0
         if self.is_gpu and max_seqs > 1 and os.environ.get("OMX_MFMA_BATCH", "1") != "0":
             self.mfma_bytes = self.w.build_mfma_layouts()
-        # long prefill chunks (>= gemm_lib_min_m rows) on hipBLASLt: resident fp16 weight copies skip the
-        # per-call dequantisation (7B: 13.5 GB of the 288 GB HBM), when they take at most half the free
-        # memory; OMX_PREFILL_F16=0 keeps the per-call path
-        self.f16_bytes = 0
-        lm = native().gemm_lib_min_m() if self.is_gpu else 0
-        lm_res = min(lm, native().gemm_lib_min_m_res()) if lm > 0 else 0
-        if self.is_gpu and os.environ.get("OMX_PREFILL_F16", "1") != "0" and lm_res > 0 and max_batch >= lm_res:
-            free = torch.cuda.mem_get_info(self.device)[0]
-            self.f16_bytes = self.w.build_f16_copies(free // 2)
-        # rows from which prefill chunks take hipBLASLt (gemm.hip lib_min_for; 0 = never)
-        self.lib_min = lm_res if self.f16_bytes else lm
+        # rows from which prefill chunks take hipBLASLt (gemm.hip gemm_lib_min_m; default 0 = never: every
+        # prefill GEMM runs the hand-written dequant kernel over the resident quantised weights, and no fp16
+        # weight copy exists -- OMX_GEMM_LIB_MIN_M=<rows> is the A/B knob)
+        self.lib_min = native().gemm_lib_min_m() if self.is_gpu else 0
         cfg = self.cfg = self.w.cfg
         loc = self.w.local
         self.max_batch = max_batch
@@ -285,6 +278,12 @@ class Runner:
         # deferred flash-decode merge (B == 1): attention leaves S <= 8 partial slabs, the O GEMV
         # merges them in its activation prologue (no in-launch ticket + re-read)
         self.defer_kps = int(os.environ.get("OMX_DEFER_KPS", "128"))
+        # batch-1 generation: decode steps per graph replay (1 = one token per replay)
+        # (default 1: the A/B in profiles/r6_decode measured 4-step graphs 1.3 % slower per step -- the
+        # ~13 us boundary between two replays disappears inside a group, but the larger graph ran with
+        # more idle time between its kernels)
+        self.decode_group = max(1, int(os.environ.get("OMX_DECODE_GROUP", "1")))
+        self.steps_issued = 0  # decode steps enqueued so far (batched steps count once): bench timing
         # past 8 x defer_kps keys, up to 8 x 512: 8 deferred splits of ceil(len / 8) keys (OMX_DEFER_LONG=1,
         # default: attention 14.4 -> 11.6 us at 2k keys, the O prologue's 8-slab merge 4.9 -> 7.1 us, net
         # decode_ctx2048 593 -> 602 tok/s, profiles/r5_decode) or the on-device split rule with the
@@ -328,7 +327,7 @@ class Runner:
             self._tok_host = torch.zeros(max_batch, dtype=torch.int32).pin_memory()
             # sampled tokens of the B == 1 steps, written by the feedback kernel straight into host-mapped
             # pinned memory (slot = input position % ring): no D2H copy command per step
-            self._ring_n = 8
+            self._ring_n = 32  # > the steps in flight: two groups of decode_group steps (generate)
             h, d = native().host_alloc_mapped(4 * self._ring_n)
             self._host_ring_dev = d
             self._host_ring = np.ctypeslib.as_array((ctypes.c_int32 * self._ring_n).from_address(h))
@@ -596,8 +595,10 @@ class Runner:
         else:
             self.d_tokens[:B].copy_(self.s_out[:B])
 
-    def _graph(self, B: int):
-        key = (B, self._decode_S)
+    def _graph(self, B: int, steps: int = 1):
+        """The decode graph of `steps` consecutive steps for B rows (one replay = `steps` tokens per row:
+        the feedback kernel advances every row on device between them, so no host work sits in between)."""
+        key = (B, self._decode_S, steps)
         g = self.graphs.get(key)
         if g is None:
             s = torch.cuda.Stream()
@@ -615,7 +616,8 @@ class Runner:
             gc.disable()
             try:
                 with torch.cuda.graph(g, capture_error_mode="thread_local"):
-                    self._decode_body(B)
+                    for _ in range(steps):
+                        self._decode_body(B)
             finally:
                 if gc_was:
                     gc.enable()
@@ -672,6 +674,8 @@ class Runner:
             for S in buckets:  # one decode graph per split bucket reachable at this context size
                 self._decode_S = S
                 self._graph(1)
+                if self.decode_group > 1 and self.tp_ctrl is None:
+                    self._graph(1, self.decode_group)
             self._decode_S = 0
         torch.cuda.synchronize()
         # the objects alive after load (torch, the model, graphs) move to the permanent generation: a
@@ -681,6 +685,35 @@ class Runner:
         if os.environ.get("OMX_GC_FREEZE", "1") != "0":
             gc.collect()
             gc.freeze()
+
+    def decode_steps(self, sid: int, pos: int, k: int) -> None:
+        """k consecutive batch-1 decode steps of sequence `sid` from input position `pos`, as ONE graph
+        replay when graphs are on (generate's pipelined loop): the boundary between two replayed graphs
+        costs ~13 us of idle GPU (profiles/r5_decode step traces, the gap after decode_feedback), paid once
+        per k tokens instead of once per token. Every step of the group uses the split bucket of the
+        group's last length (any bucket is exact; only its speed depends on the length)."""
+        if k <= 1 or not (self.is_gpu and self.use_graphs):
+            for j in range(k):
+                self.decode_batch([sid], [pos + j])
+            return
+        if self._closed:
+            raise RuntimeError("runner is closed")
+        s = self.kv.seqs[sid]
+        reserved = False
+        if pos + k > len(s.blocks) * self.block_size:
+            self.kv.reserve(sid, min(self.ctx, pos + k + 4 * self.block_size))
+            self._sync_block_table(sid)
+            reserved = True
+        if not (not reserved and self._adv_next == (sid, pos)):
+            self._upload(np.array([[pos], [self.kv.slot(sid, pos)], [pos + 1], [s.row], [0]], np.int32), None)
+        self._decode_S = self.decode_splits(pos + k)
+        try:
+            with trace_range(f"decode x{k}"):
+                self._graph(1, k).replay()
+            self._adv_next = (sid, pos + k)
+            self.steps_issued += k
+        finally:
+            self._decode_S = 0
 
     def decode_step(self, sid: int, pos: int | None = None) -> None:
         """One token for sequence `sid` whose input token (not yet in `tokens`) is already in
@@ -718,6 +751,7 @@ class Runner:
                     self._decode_body(B)
             if self.is_gpu:
                 self._adv_next = (sids[0], poss[0] + 1) if B == 1 else (tuple(sids), tuple(p + 1 for p in poss))
+            self.steps_issued += 1
         finally:
             self._decode_S = 0
 
@@ -871,14 +905,22 @@ class Runner:
         R = self._ring_n
         evs: list = [None] * R
         issued = 0
+        # steps per graph replay (decode_steps): groups of G when this rank decides alone; TP ranks step
+        # one token at a time, as the leader's go / stop signal does
+        G = self.decode_group if ctrl is None else 1
 
-        def issue():
+        def issue(cap: int):
             nonlocal issued
-            self.decode_step(sid, base + issued)
+            k = max(1, min(G, cap - issued))
+            if k == 1:
+                self.decode_step(sid, base + issued)
+            else:
+                self.decode_steps(sid, base + issued, k)
             e = torch.cuda.Event()
             e.record()
-            evs[(base + issued) % R] = e
-            issued += 1
+            for j in range(k):
+                evs[(base + issued + j) % R] = e
+            issued += k
 
         n = 0
         tok = first
@@ -894,9 +936,10 @@ class Runner:
                 if not done:
                     if leader:
                         ctrl.signal(True)
-                    target = min(n + 1, max_tokens - 1)  # steps 0..n: tokens up to n+2
-                    while issued < target:
-                        issue()
+                    # steps 0..n (tokens up to n+2) at least; a group keeps up to G - 1 more queued
+                    target = min(n + (G if G > 1 else 1), max_tokens - 1)
+                    while issued < min(n + 1, max_tokens - 1) or (G > 1 and issued < target):
+                        issue(max_tokens - 1)
                     st.tokens.append(tok)  # step n-1 (issued) writes its KV
                 yield tok
                 if done:

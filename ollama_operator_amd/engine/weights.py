@@ -43,28 +43,15 @@ class DevQMat:
     wide: torch.Tensor | None = None
     # GPU, continuous batching: layout M copy for the matrix-core batched decode GEMV (gemv_mfma.hip)
     mt: torch.Tensor | None = None
-    # GPU, long prefill chunks: resident fp16 copy for the library GEMM (gemm.hip gemm_lib)
-    f16: torch.Tensor | None = None
 
     @property
     def tup(self) -> tuple:
         p = [s.data_ptr() for s in self.streams] + [0] * (4 - len(self.streams))
         t = (p[0], p[1], p[2], p[3], self.N, self.K, int(self.qtype))
         wide = self.wide.data_ptr() if self.wide is not None else 0
-        if self.f16 is not None:
-            return t + (wide, self.mt.data_ptr() if self.mt is not None else 0, self.f16.data_ptr())
         if self.mt is not None:
             return t + (wide, self.mt.data_ptr())
         return t + (wide,) if self.wide is not None else t
-
-    def build_f16(self) -> int:
-        """Resident fp16 copy in the prefill GEMM's K order (dequant_f16 perm = 1); returns its bytes."""
-        from ..ops import native, stream_handle
-        if self.f16 is None:
-            self.f16 = torch.empty(self.N * self.K, dtype=torch.float16, device=self.streams[0].device)
-            native().dequant_f16(self.tup[:7] + ((self.wide.data_ptr(),) if self.wide is not None else ()),
-                                 self.f16.data_ptr(), stream_handle(), 1)
-        return self.f16.numel() * 2
 
     def build_mfma_layout(self) -> int:
         """Layout M copy (gemv_mfma.hip `repack_m`, built on the device from the v2 streams) for the
@@ -84,15 +71,26 @@ class DevQMat:
 
 
 def _np_repack_rows(src: np.ndarray, qtype: int, K_src: int, rows: np.ndarray, dst_rows: np.ndarray,
-                    kb0: int, kb1: int, dst: list[np.ndarray]) -> None:
-    """numpy twin of csrc/gguf/gguf.cpp repack_rows (CPU-only environments / tests)."""
+                    kb0: int, kb1: int, dst: list[np.ndarray], K_out: int = 0) -> None:
+    """numpy twin of csrc/gguf/gguf.cpp repack_rows (CPU-only environments / tests). K_out > K: the
+    destination rows are K_out wide (zero super-blocks past K, every stream's stride grown to match)."""
     from ..quant import repack
     blk, nb = BLOCK_GEOMETRY[GGMLType(qtype)]
     b = src.reshape(-1, K_src // blk, nb)[rows][:, kb0:kb1]
     K = (kb1 - kb0) * blk
     st = repack(b.reshape(-1), qtype, len(rows), K)
+    sb, sbo = (K + 255) // 256, (max(K, K_out) + 255) // 256
     for i, n in enumerate(REPACK_STREAMS[GGMLType(qtype)]):
-        dst[i].reshape(-1, st[n].shape[1])[dst_rows] = st[n]
+        a = st[n]
+        if sbo > sb:  # per-row streams are [8 pieces][SB][w] (codes) or [SB][w] (scales): pad the SB axis
+            w = a.shape[1] // sb
+            piece_major = n in ("qs", "ql", "qh")
+            if piece_major:
+                a3 = a.reshape(len(rows), 8, sb, w // 8)
+                a = np.concatenate([a3, np.zeros((len(rows), 8, sbo - sb, w // 8), a.dtype)], 2).reshape(len(rows), -1)
+            else:
+                a = np.concatenate([a, np.zeros((len(rows), (sbo - sb) * w), a.dtype)], 1)
+        dst[i].reshape(-1, a.shape[1])[dst_rows] = a
 
 
 class WeightSource:
@@ -127,24 +125,25 @@ class WeightSource:
         return self._requant[name]
 
     def repack_into(self, name: str, K_src: int, rows: np.ndarray, dst_rows: np.ndarray, kb0: int, kb1: int,
-                    dst: list[np.ndarray]) -> None:
+                    dst: list[np.ndarray], K_out: int = 0) -> None:
         t = self.info(name)
         rows = np.ascontiguousarray(rows, dtype=np.int64)
         dst_rows = np.ascontiguousarray(dst_rows, dtype=np.int64)
         if t.ggml_type in NATIVE_QTYPES:
             if self.nat is not None:
-                self.nat.repack(name, rows, dst_rows, K_src, kb0, kb1, [d.ctypes.data for d in dst], self.threads)
+                self.nat.repack(name, rows, dst_rows, K_src, kb0, kb1, [d.ctypes.data for d in dst], self.threads,
+                                K_out)
                 if hasattr(self.nat, "release"):
                     self.nat.release(name)  # the blob's pages leave RSS as soon as their copy exists
             else:
-                _np_repack_rows(self.g.raw(name), int(t.ggml_type), K_src, rows, dst_rows, kb0, kb1, dst)
+                _np_repack_rows(self.g.raw(name), int(t.ggml_type), K_src, rows, dst_rows, kb0, kb1, dst, K_out)
         else:
             src = self._requantized(name)
             if self.nat is not None:
                 native().repack_ptr(src.ctypes.data, int(GGMLType.Q8_0), K_src, rows, dst_rows, kb0, kb1,
-                                    [d.ctypes.data for d in dst], self.threads)
+                                    [d.ctypes.data for d in dst], self.threads, K_out)
             else:
-                _np_repack_rows(src, int(GGMLType.Q8_0), K_src, rows, dst_rows, kb0, kb1, dst)
+                _np_repack_rows(src, int(GGMLType.Q8_0), K_src, rows, dst_rows, kb0, kb1, dst, K_out)
 
 
 _HUGE = 2 << 20
@@ -171,19 +170,22 @@ def host_buffer(nbytes: int, device) -> np.ndarray:
 
 
 def build_qmat(src: WeightSource, parts: list[tuple[str, np.ndarray, np.ndarray]], N: int, K_src: int,
-               kb: tuple[int, int] | None, device, expert_rows: int = 0, widen: bool = False) -> DevQMat:
-    """parts: (tensor, source rows, destination rows). All parts must share one device qtype."""
+               kb: tuple[int, int] | None, device, expert_rows: int = 0, widen: bool = False,
+               k_pad: int = 0) -> DevQMat:
+    """parts: (tensor, source rows, destination rows). All parts must share one device qtype.
+    k_pad > K: the matrix is stored (and presented to the kernels) with K = k_pad, zero weights past the
+    real K (the consumer's activation columns past it are zero too: DeviceWeights.ffn_pad)."""
     qts = {src.qtype_of(p[0]) for p in parts}
     if len(qts) != 1:
         raise ValueError(f"mixed quant types in one matrix: {qts}")
     qt = qts.pop()
     blk = BLOCK_GEOMETRY[GGMLType(qt)][0]
     kb0, kb1 = kb if kb is not None else (0, K_src // blk)
-    K = (kb1 - kb0) * blk
+    K = max((kb1 - kb0) * blk, k_pad)
     sb = stream_bytes(qt, K)
     host = [host_buffer(N * b, device) for b in sb]
     for name, rows, drows in parts:
-        src.repack_into(name, K_src, rows, drows, kb0, kb1, host)
+        src.repack_into(name, K_src, rows, drows, kb0, kb1, host, K)
     streams = [torch.from_numpy(h).to(device) for h in host]
     m = DevQMat(qt, expert_rows or N, K, streams)
     # opt-in (OMX_Q6K_WIDEN=1): Q6_K projections (down, V, O) get int8-widened codes for the batch-1
@@ -211,6 +213,25 @@ def rope_inv_freq(n_rot: int, base: float) -> np.ndarray:
     return (base ** (-2.0 * i / n_rot)).astype(np.float32)
 
 
+def ffn_pad(F: int, device, tp: int, moe: bool) -> int:
+    """Zero columns appended to ffn_down's K on the GPU (tp == 1, dense FFN) so its layout-v2 piece runs
+    start on 256-B boundaries: piece t of a row sits at byte (t * SB + sb) * 16, so with SB % 8 != 0 every
+    16-lane run of the decode GEMV straddles an extra 128-B line. Llama-2-7B's 11008 = 43 super-blocks is
+    padded to 48 (+11.6 % storage; the r5 probe: down Q6_K 13.1 -> 10.9 us, Q4_K 8.9 -> 8.2 us at the padded
+    K, profiles/r5_decode/align_full_*.log). OMX_FFN_PAD: auto (<= 12.5 % growth, SB % 8 != 0), force
+    (any SB % 16 != 0; tests), 0 (off)."""
+    mode = os.environ.get("OMX_FFN_PAD", "auto").strip().lower()
+    if mode in ("0", "off") or tp != 1 or moe or not str(device).startswith("cuda"):
+        return 0
+    sb = (F + 255) // 256
+    sb16 = (sb + 15) // 16 * 16
+    if mode == "force":
+        return sb16 * 256 - F if sb % 16 else 0
+    if sb % 8 and sb16 * 8 <= sb * 9:
+        return sb16 * 256 - F
+    return 0
+
+
 class DeviceWeights:
     """All weights of one model (one TP rank) resident on `device`."""
 
@@ -234,7 +255,10 @@ class DeviceWeights:
         self.f_range = (f0, f1)
         Hl, Hkvl, Fl, Vl = H // T, Hkv // T, (f1 - f0) if not cfg.n_expert else F // T, V // T
         self.cfg = cfg
-        self.local = dict(E=E, H=Hl, Hkv=Hkvl, D=D, F=Fl, V=Vl)
+        self.ffn_pad = ffn_pad(Fl, device, T, bool(cfg.n_expert))
+        # the executor's FFN width: the padded K of ffn_down (the gate/up rows stay Fl; the activation
+        # columns past Fl are never written, so they stay zero, like the padded weights)
+        self.local = dict(E=E, H=Hl, Hkv=Hkvl, D=D, F=Fl + self.ffn_pad, V=Vl)
         dev = device
         t = lambda a: torch.from_numpy(np.array(a, np.float32)).to(dev)  # noqa: E731
         phi = cfg.arch == "phi2"
@@ -278,7 +302,8 @@ class DeviceWeights:
                 L["wgu"] = build_qmat(src, [(b + "ffn_up.weight", ar(Fl, f0), ar(Fl))], Fl, E, None, dev)
                 L["bup"] = t(src.f32(b + "ffn_up.bias")[f0:f1])
                 L["wdown"] = build_qmat(src, [(b + "ffn_down.weight", ar(E), ar(E))], E, F,
-                                        kblocks(F, b + "ffn_down.weight"), dev, widen=True)
+                                        kblocks(F, b + "ffn_down.weight"), dev, widen=True,
+                                        k_pad=Fl + self.ffn_pad)
                 L["bdown"] = t(src.f32(b + "ffn_down.bias")) if r == 0 else None
             else:
                 rq = head_rows(r * Hl, Hl, cfg.rope_mode == ROPE_NEOX)
@@ -312,7 +337,8 @@ class DeviceWeights:
                     loc = ar(Fl, f0)
                     L["wgu"] = build_qmat(src, [(ng, loc, 2 * ar(Fl)), (nu, loc, 2 * ar(Fl) + 1)], 2 * Fl, E, None, dev)
                     L["wdown"] = build_qmat(src, [(b + "ffn_down.weight", ar(E), ar(E))], E, F,
-                                            kblocks(F, b + "ffn_down.weight"), dev, widen=True)
+                                            kblocks(F, b + "ffn_down.weight"), dev, widen=True,
+                                            k_pad=Fl + self.ffn_pad)
             self.layers.append(L)
         self.out_norm = t(src.f32("output_norm.weight"))
         self.out_norm_b = t(src.f32("output_norm.bias")) if src.has("output_norm.bias") else None
@@ -333,17 +359,6 @@ class DeviceWeights:
                 if isinstance(v, DevQMat) and k not in ("gu_exps", "down_exps"):
                     n += v.build_mfma_layout()
         return n
-
-    def build_f16_copies(self, budget: int) -> int:
-        """Resident fp16 copies of every dense layer projection for the library prefill GEMM, if they
-        fit in `budget` bytes (else none). MoE expert stacks and the LM head keep the per-call path.
-        Returns the bytes added."""
-        mats = [v for L in self.layers for k, v in L.items()
-                if isinstance(v, DevQMat) and k not in ("gu_exps", "down_exps", "router")]
-        need = sum(v.N * v.K * 2 for v in mats if v.f16 is None)
-        if need > budget:
-            return 0
-        return sum(v.build_f16() for v in mats)
 
     @property
     def nbytes(self) -> int:

@@ -224,6 +224,10 @@ PRESETS: dict[str, ModelConfig] = {
     "tiny-phi2-tp": ModelConfig(name="tiny-phi2-tp", arch="phi2", n_vocab=512, n_embd=1024, n_layer=2,
                                 n_head=16, n_head_kv=16, n_ff=2048, n_rot=32, rope_mode=ROPE_NEOX,
                                 ctx_len=256, bos_id=0, eos_id=0),
+    # TP = 8 (BASELINE config 4's degree, Llama-2-70B's 8:1 query / KV head ratio): one KV head, four query
+    # heads, one FFN super-block and 64 vocab rows per rank
+    "tiny-llama-tp8": ModelConfig(name="tiny-llama-tp8", n_vocab=512, n_embd=2048, n_layer=2, n_head=32,
+                                  n_head_kv=8, n_ff=2048, n_rot=64, ctx_len=256),
     "tiny-mixtral-tp": ModelConfig(name="tiny-mixtral-tp", n_vocab=512, n_embd=1024, n_layer=2, n_head=16,
                                    n_head_kv=4, n_ff=1024, n_rot=64, ctx_len=256, n_expert=4,
                                    n_expert_used=2),

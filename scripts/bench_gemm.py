@@ -1,7 +1,9 @@
 """Prefill GEMM microbenchmark on Llama-2-7B Q4_K_M shapes: the stream-order dequant GEMM
 (csrc/kernels/gemm_dq.hip, "dq", the default), the 128 x 128 natural-order tile (gemm.hip, "tile") and
-the hipBLASLt path (prep + dequant to fp16 + library GEMM + epilogue pass; csrc/runtime/blas.cpp):
-time per call (everything the path launches) and TFLOP/s vs M (prompt tokens). On the GPU box:
+the hipBLASLt path (prep + dequant to fp16 + library GEMM + epilogue pass; csrc/runtime/blas.cpp; opt-in
+since round 6) and the register-ring edition of the dq kernel ("ring", the default since round 6; "dq" is
+the glds edition): time per call (everything the path launches) and TFLOP/s vs M (prompt tokens). On the
+GPU box:
   python scripts/bench_gemm.py   (OMX_BENCH_SHAPES / OMX_BENCH_M / OMX_BENCH_PATHS filter, e.g. for PMC runs)"""
 import os
 import sys
@@ -40,13 +42,14 @@ def main():
             yws = torch.empty(M * N, device="cuda")
             ws = {"xws": xws.data_ptr(), "xws_elems": xws.numel(), "gws": gws.data_ptr(), "gws_elems": gws.numel(), "w16ws": w16.data_ptr(),
                   "w16_elems": w16.numel(), "yws": yws.data_ptr(), "yws_elems": yws.numel()}
-            fn = lambda: C.gemv(tup, M, x.data_ptr(), K, 0, 0, 0, 1e-5, 0, y.data_ptr(), N, 0, 0, ws, s)  # noqa: E731
-            paths = os.environ.get("OMX_BENCH_PATHS", "dq,tile,hipblaslt").split(",")
-            for path, min_m, dq in (("dq", 0, 1), ("tile", 0, 0), ("hipblaslt", 1, 0)):
+            paths = os.environ.get("OMX_BENCH_PATHS", "ring,dq,tile,hipblaslt").split(",")
+            for path, min_m, dq in (("ring", 0, 1), ("dq", 0, 1), ("tile", 0, 0), ("hipblaslt", 1, 0)):
                 if path not in paths:
                     continue
+                fn = lambda: C.gemv(tup, M, x.data_ptr(), K, 0, 0, 0, 1e-5, 0, y.data_ptr(), N, 0, 0, ws, s)  # noqa: E731
                 C.set_gemm_lib_min_m(min_m)
                 C.set_dq_gemm(dq)
+                C.set_dq_ring(1 if path == "ring" else 0)
                 for _ in range(3):
                     fn()
                 torch.cuda.synchronize()

@@ -87,7 +87,7 @@ def _ar_worker(rank, world, port, out_dir):
         os._exit(0)
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_custom_allreduce_graph_replays(tmp_path, world):
     mp.start_processes(_ar_worker, args=(world, _port(), str(tmp_path)), nprocs=world, start_method="spawn",
                        join=True)
@@ -195,11 +195,13 @@ def _emit_worker(rank, world, port, out_dir):
         os._exit(0)
 
 
-def test_allreduce_emits_int8_chain_image(tmp_path):
-    """TP decode on the int8 chain: the all-reduce itself writes the next GEMV's image + RMS partials."""
+@pytest.mark.parametrize("world", [2, 8])
+def test_allreduce_emits_int8_chain_image(tmp_path, world):
+    """TP decode on the int8 chain: the all-reduce itself writes the next GEMV's image + RMS partials
+    (world 8: the ar_add_emit_kernel<8> instantiation TP=8 decode runs)."""
     from test_gemv8_gpu import decode_image
     from ollama_operator_amd.ops import native
-    world, E, B = 2, 4096, 2
+    E, B = 4096, 2
     mp.start_processes(_emit_worker, args=(world, _port(), str(tmp_path)), nprocs=world, start_method="spawn",
                        join=True)
     C = native()
@@ -290,9 +292,9 @@ def test_tp2_graph_decode_matches_tp1(tmp_path, name, ft):
             assert on == 1 and n8 > 0, (rank, n8, on)
 
 
-def _check_tp(tmp_path, ref):
+def _check_tp(tmp_path, ref, world=2):
     p0 = np.load(tmp_path / "p0.npy")
-    for rank in range(2):
+    for rank in range(world):
         got = np.load(tmp_path / f"p{rank}.npy")
         assert np.array_equal(got, p0), "TP ranks must hold bit-identical logits"
         for i in range(len(ref)):
@@ -314,3 +316,21 @@ def test_tp2_collective_stage_paths_match_tp1(tmp_path, mode):
     mp.start_processes(_tp_worker, args=(2, _port(), path, str(tmp_path), mode), nprocs=2, start_method="spawn",
                        join=True)
     _check_tp(tmp_path, ref)
+
+
+def test_tp8_graph_decode_matches_tp1(tmp_path):
+    """TP = 8 (BASELINE config 4's degree) with 8 ranks sharing one GPU: the whole decode step of every rank
+    is one graph on the int8 chain with the fused all-reduce emission at world 8, and the logits match
+    TP = 1. No cross-GPU run exists here (one GPU per box); the collective code path is the same."""
+    path = str(tmp_path / "tiny-tp8.gguf")
+    write_random_gguf(path, preset("tiny-llama-tp8"), FileType.MOSTLY_Q4_K_M, seed=5)
+    from ollama_operator_amd.engine.runner import Runner
+    r1 = Runner(path, device="cuda:0", max_batch=4, max_seqs=2, ctx=64)
+    ref = _run(r1)
+    del r1
+    mp.start_processes(_tp_worker, args=(8, _port(), path, str(tmp_path)), nprocs=8, start_method="spawn",
+                       join=True)
+    _check_tp(tmp_path, ref, world=8)
+    for rank in range(8):
+        n8, on = np.load(tmp_path / f"n{rank}.npy")
+        assert on == 1 and n8 > 0, (rank, n8, on)

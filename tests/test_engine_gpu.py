@@ -80,10 +80,9 @@ def test_prefill_gemm_path_vs_torch(tiny_models, name):
 @pytest.mark.parametrize("name", ["tiny-llama", "tiny-mixtral", "tiny-phi2", "tiny-llama-q8", "tiny-llama-q40",
                                   "tiny-llama-q5km", "tiny-gemma", "tiny-orca"])
 def test_prefill_dq_path_vs_torch(tiny_models, name, monkeypatch):
-    """Prompts >= 128 tokens take the stream-order dequant GEMM (gemm_dq.hip) for every dense matrix when
-    no resident fp16 copies exist (OMX_PREFILL_F16=0; with them the library path takes >= 128 rows):
-    logits must match the torch twin, before and after a decode step on the KV it wrote."""
-    monkeypatch.setenv("OMX_PREFILL_F16", "0")
+    """Prompts >= 128 tokens take the stream-order dequant GEMM (gemm_dq.hip, the default prefill path;
+    no fp16 weight copy exists): logits must match the torch twin, before and after a decode step on the
+    KV it wrote."""
     C = native()
     assert C.dq_gemm_enabled() and (C.gemm_lib_min_m() == 0 or C.gemm_lib_min_m() > 230)
     path = tiny_models[name]
@@ -110,7 +109,6 @@ def test_prefill_library_path_vs_torch(tiny_models, name, monkeypatch):
     rows with the GLU / routing-weighted scatter epilogues, moe_gemm_lib) forced from 16 rows: logits
     must match the torch twin, and the dequantised-weight scratch must have been used (per-call
     dequantisation: no resident fp16 copies)."""
-    monkeypatch.setenv("OMX_PREFILL_F16", "0")
     C = native()
     old = C.gemm_lib_min_m()
     C.set_gemm_lib_min_m(16)
@@ -313,29 +311,71 @@ def test_admit_many_gpu_matches_sequential(tiny_models, name):
         assert rel(g.logits[i, :V].float().cpu(), lg) < 2e-2, i
 
 
-@pytest.mark.parametrize("name", ["tiny-llama", "tiny-gemma", "tiny-llama-q40"])
-def test_prefill_library_resident_f16(tiny_models, name):
-    """Resident fp16 weight copies (OMX_PREFILL_F16, default on): the library prefill GEMM reads them
-    and never touches the per-call dequantisation scratch; logits match the torch twin."""
+@pytest.mark.parametrize("group", [2, 4])
+def test_grouped_decode_graph_matches_single_steps(tiny_models, monkeypatch, group):
+    """generate() replays `group` decode steps per graph (OMX_DECODE_GROUP): the same tokens as one step
+    per replay, for a generation length that is not a multiple of the group and crosses KV pages."""
+    path = tiny_models["tiny-llama"]
+    o = SamplingOptions(temperature=0.7, top_k=20, top_p=0.95, seed=7)
+    monkeypatch.setenv("OMX_DECODE_GROUP", "1")
+    a = Runner(path, device="cuda", max_batch=8, max_seqs=2, ctx=128)
+    monkeypatch.setenv("OMX_DECODE_GROUP", str(group))
+    b = Runner(path, device="cuda", max_batch=8, max_seqs=2, ctx=128, weights=a.w)
+    b.warmup()
+    assert b.decode_group == group
+    prompt = [1, 9, 8, 7, 6, 5]
+    ta = list(a.generate(a.new_sequence(), prompt, o, max_tokens=37))
+    tb = list(b.generate(b.new_sequence(), prompt, o, max_tokens=37))
+    assert ta == tb and len(ta) == 37
+    assert any(k[2] == group for k in b.graphs), "no grouped graph was replayed"
+
+
+@pytest.mark.parametrize("name", ["tiny-llama", "tiny-llama-q40", "tiny-llama-q8"])
+def test_ffn_down_k_padding(tiny_models, monkeypatch, name):
+    """ffn_down stored with a padded K (weights.py ffn_pad, zero super-blocks; the GLU image and the fp32
+    / fp16 activation rows carry zeros there): prefill logits and greedy decode match the unpadded
+    model on the int8 chain, the fp32 GEMV and the prefill GEMM paths."""
+    path = tiny_models[name]
+    monkeypatch.setenv("OMX_FFN_PAD", "0")
+    a = Runner(path, device="cuda", max_batch=64, max_seqs=2, ctx=128)
+    monkeypatch.setenv("OMX_FFN_PAD", "force")
+    b = Runner(path, device="cuda", max_batch=64, max_seqs=2, ctx=128)
+    assert a.w.ffn_pad == 0 and b.w.ffn_pad > 0
+    assert b.w.layers[0]["wdown"].K == a.w.layers[0]["wdown"].K + b.w.ffn_pad
+    V = a.cfg.n_vocab
+    toks = [1] + list(range(3, 40))  # 39 rows: the prefill GEMM path
+    for r in (a, b):
+        r._sid = r.new_sequence()
+        r.prefill(r._sid, toks)
+    assert rel(b.logits[0, :V].cpu(), a.logits[0, :V].cpu()) < 1e-3
+    o = SamplingOptions(temperature=0)
+    ta = list(a.generate(a.new_sequence(), [1, 5, 6, 7], o, max_tokens=12))
+    tb = list(b.generate(b.new_sequence(), [1, 5, 6, 7], o, max_tokens=12))
+    assert ta == tb
+
+
+@pytest.mark.parametrize("ring", [0, 1])
+@pytest.mark.parametrize("name", ["tiny-llama", "tiny-llama-q40", "tiny-llama-q8", "tiny-llama-q5km", "tiny-phi2"])
+def test_prefill_dq_ring_and_glds_kernels(tiny_models, name, ring):
+    """Both editions of the hand-written prefill GEMM (gemm_dq_impl.h: the register-ring default and the
+    glds kernel, set_dq_ring) over 240 prompt rows (128- and 256-row tiles with a partial last tile,
+    split-K for the narrow shapes): logits match the torch twin and every dense projection ran on the dq
+    kernel."""
     C = native()
-    old = C.gemm_lib_min_m()
-    C.set_gemm_lib_min_m(16)
+    C.set_dq_ring(ring)
     try:
         path = tiny_models[name]
-        g = Runner(path, device="cuda", max_batch=128, max_seqs=2, ctx=160)
-        c = Runner(path, device="cpu", max_batch=64, max_seqs=2, ctx=160)
-        assert g.f16_bytes > 0
-        g.w16.fill_(float("nan"))
-        rng = np.random.default_rng(3)
-        toks = [1] + [int(x) for x in rng.integers(3, 500, 69)]
+        g = Runner(path, device="cuda", max_batch=256, max_seqs=2, ctx=256)
+        c = Runner(path, device="cpu", max_batch=256, max_seqs=2, ctx=256)
+        rng = np.random.default_rng(11)
+        toks = [1] + [int(x) for x in rng.integers(3, 500, 239)]
         sg, sc = g.new_sequence(), c.new_sequence()
         C.reset_launch_counts()
         g.prefill(sg, toks)
-        torch.cuda.synchronize()
-        assert C.launch_counts()["gemm_lib"] >= 2 * g.cfg.n_layer
-        assert torch.isnan(g.w16).all()  # the scratch stayed unused
+        n = C.launch_counts()
+        assert n["dq_gemm"] >= 2 * g.cfg.n_layer and n["gemm_lib"] == 0, n
         c.prefill(sc, toks)
         V = g.cfg.n_vocab
         assert rel(g.logits[0, :V].cpu(), c.logits[0, :V]) < 3e-2
     finally:
-        C.set_gemm_lib_min_m(old)
+        C.set_dq_ring(1)

@@ -188,3 +188,35 @@ def test_native_repack_matches_numpy(t):
     want = repack(np.ascontiguousarray(sub).reshape(-1), t, 3, kk)
     for name, d in zip(REPACK_STREAMS[t], dst):
         np.testing.assert_array_equal(d, want[name].reshape(3, -1), err_msg=name)
+
+
+@pytest.mark.parametrize("t", QTYPES)
+def test_repack_padded_k_native_matches_numpy(t):
+    """K_out > K (the GPU loader's ffn_down padding, weights.ffn_pad): every stream keeps the real
+    super-blocks at their piece-major places with the padded stride, zeros past K; the native repacker
+    and its numpy twin agree, and unrepacking the padded rows gives the source columns then zeros."""
+    from ollama_operator_amd.engine.weights import _np_repack_rows
+    from ollama_operator_amd.ops import native
+    from ollama_operator_amd.quant import repack_row_bytes, unrepack
+    rng = np.random.default_rng(5)
+    n, k, k_out = 4, 768, 1536  # 3 super-blocks stored as 6
+    raw = random_blocks(t, n, k, rng)
+    blk = BLOCK_GEOMETRY[t][0]
+    rows, dst_rows = np.arange(n, dtype=np.int64), np.arange(n, dtype=np.int64)
+    want = [np.zeros((n, b), np.uint8) for b in repack_row_bytes(t, k_out)]
+    _np_repack_rows(raw, int(t), k, rows, dst_rows, 0, k // blk, want, k_out)
+    try:
+        nat = native()
+    except Exception:
+        nat = None
+    if nat is not None:
+        got = [np.zeros((n, b), np.uint8) for b in repack_row_bytes(t, k_out)]
+        nat.repack_ptr(raw.ctypes.data, int(t), k, rows, dst_rows, 0, k // blk, [d.ctypes.data for d in got], 2, k_out)
+        for a, b in zip(got, want):
+            np.testing.assert_array_equal(a, b)
+    from ollama_operator_amd.quant import REPACK_STREAMS
+    back = unrepack({nm: w for nm, w in zip(REPACK_STREAMS[t], want)}, t, n, k_out)
+    y = dequantize(back.reshape(-1), t, n * k_out).reshape(n, k_out)
+    x = dequantize(raw.reshape(-1), t, n * k).reshape(n, k)
+    np.testing.assert_array_equal(y[:, :k], x)
+    assert not y[:, k:].any()

@@ -49,11 +49,12 @@ def _worker(rank, world, port, path, out_dir):
         os._exit(0)
 
 
-@pytest.mark.parametrize("name,ft", [("tiny-llama-tp", FileType.MOSTLY_Q4_K_M),
-                                     ("tiny-llama-tp-odd", FileType.MOSTLY_Q4_K_M),
-                                     ("tiny-phi2-tp", FileType.MOSTLY_Q4_0),
-                                     ("tiny-mixtral-tp", FileType.MOSTLY_Q8_0)])
-def test_tp2_matches_tp1(tmp_path, name, ft):
+@pytest.mark.parametrize("name,ft,world", [("tiny-llama-tp", FileType.MOSTLY_Q4_K_M, 2),
+                                           ("tiny-llama-tp-odd", FileType.MOSTLY_Q4_K_M, 2),
+                                           ("tiny-phi2-tp", FileType.MOSTLY_Q4_0, 2),
+                                           ("tiny-mixtral-tp", FileType.MOSTLY_Q8_0, 2),
+                                           ("tiny-llama-tp8", FileType.MOSTLY_Q4_K_M, 8)])
+def test_tp2_matches_tp1(tmp_path, name, ft, world):
     path = str(tmp_path / f"{name}.gguf")
     write_random_gguf(path, preset(name), ft, seed=5)
     from ollama_operator_amd.engine.runner import Runner
@@ -64,8 +65,9 @@ def test_tp2_matches_tp1(tmp_path, name, ft):
     ref = r1.logits[0, :r1.cfg.n_vocab].numpy().copy()
     ref_toks = list(r1.generate(r1.new_sequence(), PROMPT, SamplingOptions(temperature=0, repeat_penalty=1.0),
                                 max_tokens=5))
-    mp.start_processes(_worker, args=(2, _port(), path, str(tmp_path)), nprocs=2, start_method="spawn", join=True)
-    for rank in range(2):
+    mp.start_processes(_worker, args=(world, _port(), path, str(tmp_path)), nprocs=world, start_method="spawn",
+                       join=True)
+    for rank in range(world):
         got = np.load(tmp_path / f"logits{rank}.npy")
         np.testing.assert_allclose(got, ref, rtol=1e-3, atol=1e-3)
         assert np.load(tmp_path / f"toks{rank}.npy").tolist() == ref_toks
