@@ -413,6 +413,17 @@ PYBIND11_MODULE(_C, m) {
     P.ws = Pp<float>(d.contains("ws") ? d["ws"].cast<uintptr_t>() : 0);
     P.counters = Pp<int>(d.contains("counters") ? d["counters"].cast<uintptr_t>() : 0);
     P.err = Pp<int>(d.contains("err") ? d["err"].cast<uintptr_t>() : 0);
+    if (d.contains("fb_step")) {
+      P.fb_step = Pp<int>(d["fb_step"].cast<uintptr_t>());
+      P.fb_ld = d["fb_ld"].cast<int>();
+      P.fb_block_table = Pp<const int>(d["fb_block_table"].cast<uintptr_t>());
+      P.fb_max_blocks = d["fb_max_blocks"].cast<int>();
+      P.fb_bs = d["fb_bs"].cast<int>();
+      P.fb_host_ring = Pp<int>(d.contains("fb_host_ring") ? d["fb_host_ring"].cast<uintptr_t>() : 0);
+      P.fb_ring = d.contains("fb_ring") ? d["fb_ring"].cast<int>() : 0;
+      if (P.B > P.fb_ld || P.fb_bs <= 0 || P.fb_max_blocks <= 0) throw std::runtime_error("sample: bad feedback args");
+      if (P.fb_host_ring && P.fb_ring <= 0) throw std::runtime_error("sample: bad feedback ring");
+    }
     sample(P, S(stream));
   });
 

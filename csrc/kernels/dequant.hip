@@ -1,6 +1,7 @@
 // Row gather + dequantisation from the repacked quant streams (SURVEY.md §2.2 N15 embedding
 // gather) and whole-matrix dequantisation to fp16 (resident fp16 copies for MFMA prefill GEMMs).
 #include "common.h"
+#include "feedback.h"
 #include "gemv8_core.h"
 #include "ops.h"
 
@@ -12,19 +13,23 @@ namespace omx {
 // stat (optional, the batched fp16 decode chain): per-16-element sum-of-squares partials [n][K / 16] of
 // the gathered rows, the "residual before the add" of layer 0's O emission (gemv_mfma.hip range scale)
 // one 16-element group of a gathered row into layer 0's int8 input image (img8 != null)
-__device__ __forceinline__ void embed_emit(void* img8, const float* nw, float* ist, int K, int G, const float* v) {
-  float xv[16], sq[16];
+// (isum: the group's sum of the row too, for a LayerNorm'd consumer)
+__device__ __forceinline__ void embed_emit(void* img8, const float* nw, float* ist, float* isum, int K, int G,
+                                           const float* v) {
+  float xv[16], sq[16], sx = 0.f;
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
     xv[j] = v[j] * nw[16 * G + j];
     sq[j] = v[j] * v[j];
+    sx += v[j];
   }
   emit_group(img8, K, G, xv, sq, ist);
+  if (isum) isum[G] = sx;
 }
 
 __global__ __launch_bounds__(256) void embed_rows_kernel(QMat w, const int* rows, float* out, int ldo, float scale,
                                                          const float* ext, float* stat, void* img8, const float* img_nw,
-                                                         float* img_stat) {
+                                                         float* img_stat, float* img_sum) {
   const int b = blockIdx.x;
   const long long row = rows[b];
   const int P = w.K / 32;
@@ -32,6 +37,7 @@ __global__ __launch_bounds__(256) void embed_rows_kernel(QMat w, const int* rows
   float* st = stat ? stat + (long long)b * (w.K / 16) : nullptr;
   void* im = img8 ? (char*)img8 + (size_t)b * x8_slots_dev(w.K) * 24 : nullptr;
   float* ist = img8 ? img_stat + (size_t)b * x8_stat_ld_dev(w.K) : nullptr;
+  float* isum = img8 && img_sum ? img_sum + (size_t)b * x8_stat_ld_dev(w.K) : nullptr;
   if (row < 0) {
     const float* src = ext + (-row - 1) * (long long)w.K;
     OMX_KASSERT(ext != nullptr);
@@ -45,7 +51,7 @@ __global__ __launch_bounds__(256) void embed_rows_kernel(QMat w, const int* rows
         s += v[i] * v[i];
       }
       if (st) st[g] = s;
-      if (im) embed_emit(im, img_nw, ist, w.K, g, v);
+      if (im) embed_emit(im, img_nw, ist, isum, w.K, g, v);
     }
     return;
   }
@@ -71,18 +77,18 @@ __global__ __launch_bounds__(256) void embed_rows_kernel(QMat w, const int* rows
       st[ohi >> 4] = shi;
     }
     if (im) {  // a piece's halves are whole 16-groups: each emitted by the thread that holds it
-      embed_emit(im, img_nw, ist, w.K, olo >> 4, lo);
-      embed_emit(im, img_nw, ist, w.K, ohi >> 4, hi);
+      embed_emit(im, img_nw, ist, isum, w.K, olo >> 4, lo);
+      embed_emit(im, img_nw, ist, isum, w.K, ohi >> 4, hi);
     }
   }
 }
 
 void embed_rows(const QMat& w, const int* rows, int n, float* out, int ldo, hipStream_t s, float scale,
-                const float* ext, float* stat, void* img8, const float* img_nw, float* img_stat) {
+                const float* ext, float* stat, void* img8, const float* img_nw, float* img_stat, float* img_sum) {
   if (n <= 0) return;
   if (img8 && (!img_nw || !img_stat || w.K % 16)) img8 = nullptr;
   hipLaunchKernelGGL(embed_rows_kernel, dim3(n), dim3(256), 0, s, w, rows, out, ldo, scale, ext, stat, img8, img_nw,
-                     img_stat);
+                     img_stat, img_sum);
 }
 
 // rows on blockIdx.y (grid-stride), pieces of a row on x (no 64-bit index division per piece); PERM:
@@ -174,30 +180,16 @@ void add_inplace(float* y, const float* x, long long n, hipStream_t s) {
   hipLaunchKernelGGL(add_inplace_kernel, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, s, y, x, n);
 }
 
-// Decode-step feedback, the last node of every decode graph: row b's sampled token becomes its next
-// input (step row 5), and with `advance` (B == 1 pipelined decode) the step inputs move to the next
-// position on device -- pos + 1, its KV slot from the block table, q_len -- so consecutive replays
-// need no host upload (no H2D copy or torch kernel inside the step). step: int32 [6][ld] =
-// (pos, slot, q_len, q_seq, logit_idx, tokens), engine/runner.py d_step.
-// host_ring (B == 1, optional): the sampled token also goes straight to host-mapped pinned memory,
-// slot = input position % ring, so the host reads it after the step's event (no D2H copy command).
+// Decode-step feedback: row b's sampled token becomes its next input (step row 5), and with
+// `advance` the step inputs move to the next position on device -- pos + 1, its KV slot from the
+// block table, q_len -- so consecutive replays need no host upload (feedback.h).
+// (The sampler does the same per row when given SampleParams::fb_step; this launch stays for the
+// paths that sample on the host.)
 __global__ void decode_feedback_kernel(int* step, int ld, const int* sampled, int B, int advance,
                                        const int* block_table, int max_blocks, int bs, int* host_ring, int ring) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
-  const int tok = sampled[b];
-  step[5 * ld + b] = tok;
-  if (host_ring && b == 0) {
-    __hip_atomic_store(host_ring + step[0] % ring, tok, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __threadfence_system();
-  }
-  if (!advance) return;
-  const int pos = step[b] + 1;
-  const int row = step[3 * ld + b];
-  const int bi = min(pos / bs, max_blocks - 1);  // past the context end the host re-uploads anyway
-  step[b] = pos;
-  step[ld + b] = block_table[(long long)row * max_blocks + bi] * bs + pos % bs;
-  step[2 * ld + b] = pos + 1;
+  decode_feedback_row(step, ld, b, sampled[b], advance, block_table, max_blocks, bs, host_ring, ring);
 }
 
 void decode_feedback(int* step, int ld, const int* sampled, int B, int advance, const int* block_table,

@@ -1,0 +1,24 @@
+// Decode-step token feedback for one row, shared by the decode_feedback kernel (dequant.hip) and the
+// sampler's finishing lane (sampling.hip, SampleParams::fb_step). step: int32 [6][ld] =
+// (pos, slot, q_len, q_seq, logit_idx, tokens), engine/runner.py d_step.
+// host_ring (row 0 only): the sampled token also goes straight to host-mapped pinned memory,
+// slot = input position % ring, so the host reads it after the step's event (no D2H copy command).
+#pragma once
+#include <hip/hip_runtime.h>
+
+__device__ __forceinline__ void decode_feedback_row(int* step, int ld, int b, int tok, int advance,
+                                                    const int* block_table, int max_blocks, int bs,
+                                                    int* host_ring, int ring) {
+  step[5 * ld + b] = tok;
+  if (host_ring && b == 0) {
+    __hip_atomic_store(host_ring + step[0] % ring, tok, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __threadfence_system();
+  }
+  if (!advance) return;
+  const int pos = step[b] + 1;
+  const int row = step[3 * ld + b];
+  const int bi = min(pos / bs, max_blocks - 1);  // past the context end the host re-uploads anyway
+  step[b] = pos;
+  step[ld + b] = block_table[(long long)row * max_blocks + bi] * bs + pos % bs;
+  step[2 * ld + b] = pos + 1;
+}

@@ -114,6 +114,14 @@ struct GemvParams {
                                //   padded: the image slots past N / 2 stay zero)
   int dbg8;                    // microbenchmarks only (scripts/bench_gemv8.py): 1 = gemv8 memory path alone
                                // (weights loaded and folded, no dot products); 0 in production
+  // LayerNorm'd consumers (Phi-2 int8 chain, batch 1): the image holds x * ln_w and the producer also
+  // writes per-group sums of x (x8_sum, same layout as x8_stat). With mu = sum / K and
+  // rstd = rsqrt(sumsq / K - mu^2 + eps), W . LN(x) = rstd * (W . (x * ln_w) - mu * c1) + c2 for the
+  // per-row constants c1 = W . ln_w, c2 = W . ln_b (computed at load: engine/weights.py ln_consts)
+  const float* x8_sum;         // consumer: per-group sums of x (non-null = LayerNorm input)
+  const float* ln_c1;          //   [N] W . ln_w
+  const float* ln_c2;          //   [N] W . ln_b (+ nothing else: the GEMV's own bias stays in `bias`)
+  float* emit8_sum;            // producer (EPI_ADD): per-16-row sums of the new residual (LN consumers)
 };
 // int8 activation image of a K-wide row (gemv8.hip): [slots] i32x4 codes + [slots] {scale, scale * sum}
 // with one pad slot per 256-element super-block and a trailing dummy slot (the GEMV's LDS layout)
@@ -184,9 +192,10 @@ void set_gemv_tuning(int blocks_per_cu, int rows, int debug, int ks = -1, int xf
 // img8 / img_nw / img_stat (optional, the int8 decode chain): the gathered rows also go out as layer 0's
 // QKV input image (x8_bytes(K) per row: int8(row * img_nw) per 16-group + RMS partials, x8_stat_ld(K)
 // floats per row), exactly what the residual-adding producers emit for the later layers
+// img_sum (optional): per-group sums of the rows too, for a LayerNorm'd consumer (GemvParams::x8_sum)
 void embed_rows(const QMat& w, const int* rows, int n, float* out, int ldo, hipStream_t s, float scale = 1.f,
                 const float* ext = nullptr, float* stat = nullptr, void* img8 = nullptr, const float* img_nw = nullptr,
-                float* img_stat = nullptr);
+                float* img_stat = nullptr, float* img_sum = nullptr);
 // rows [row0, row0 + w.N) of w (an expert's slice of a stacked MoE matrix); perm: prep_x16 K order
 void dequant_f16(const QMat& w, void* out_f16, hipStream_t s, int perm = 0, long long row0 = 0);
 
@@ -245,6 +254,13 @@ struct SampleParams {
   // optional error word: set to 1 when a row's choice was out of range (non-finite logits); the id
   // itself is clamped to 0 so the next step's embedding read stays in bounds, the host fails the request
   int* err = nullptr;
+  // optional decode feedback (null fb_step = none): the row's finishing lane also does what
+  // decode_feedback does -- token into the step block, host ring (row 0), advance to the next
+  // position -- so a decode step has no separate feedback launch
+  int* fb_step = nullptr;
+  int fb_ld = 0, fb_max_blocks = 0, fb_bs = 0, fb_ring = 0;
+  const int* fb_block_table = nullptr;
+  int* fb_host_ring = nullptr;
 };
 constexpr int SAMPLE_WS_FLOATS_PER_ROW(int V) { return ((V + 1023) / 1024) * 2 * 64; }
 void sample(const SampleParams& P, hipStream_t s);

@@ -6,6 +6,7 @@
 // fine bins locates the k-th largest, the survivors are bitonic-sorted in LDS; an exact 4-pass
 // radix select over order-preserving float keys is the fallback when too many logits tie.
 #include "common.h"
+#include "feedback.h"
 #include "ops.h"
 #include "wave_shuffle.h"
 
@@ -295,6 +296,8 @@ __device__ __forceinline__ void finish_sample(const SampleParams& P, int b, int 
   P.history[(long long)b * P.hist_cap + (seen % P.hist_cap)] = chosen;
   P.hist_count[b] = seen + 1;
   P.step[b] += 1;
+  if (P.fb_step) decode_feedback_row(P.fb_step, P.fb_ld, b, chosen, 1, P.fb_block_table, P.fb_max_blocks, P.fb_bs,
+                                     P.fb_host_ring, P.fb_ring);
 }
 
 __global__ __launch_bounds__(SAMPLE_NT) void sample_kernel(SampleParams P) {

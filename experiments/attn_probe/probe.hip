@@ -396,6 +396,7 @@ void launch_kind(int kind, dim3 grid, const AttnParams& P, u64* ts, hipStream_t 
 }
 void launch(const Cfg& c, dim3 grid, const AttnParams& P, u64* ts, hipStream_t s) {
   if (c.NW == 8 && c.U == 4) launch_kind<8, 4>(c.kind, grid, P, ts, s);
+  else if (c.NW == 8 && c.U == 8) launch_kind<8, 8>(c.kind, grid, P, ts, s);
   else if (c.NW == 4 && c.U == 4) launch_kind<4, 4>(c.kind, grid, P, ts, s);
   else if (c.NW == 4 && c.U == 2) launch_kind<4, 2>(c.kind, grid, P, ts, s);
   else if (c.NW == 2 && c.U == 4) launch_kind<2, 4>(c.kind, grid, P, ts, s);
@@ -432,10 +433,9 @@ static void ref_partial(const std::vector<float>& q, const std::vector<uint16_t>
 int main(int argc, char** argv) {
   const int H = 32, D = 128, bs = 16, NL = 32;
   const float scale = 1.f / sqrtf((float)D);
-  const Cfg cfgs[] = {{"base nw8 u4", 0, 8, 4}, {"v2 nw8 u4", 1, 8, 4}, {"v2 nw4 u4", 1, 4, 4}, {"v2 nw4 u2", 1, 4, 2},
-                      {"v2 nw2 u4", 1, 2, 4}, {"v2 nw2 u8", 1, 2, 8}, {"v2 nw1 u8", 1, 1, 8}, {"v2 nw1 u4", 1, 1, 4}};
-  const int lens[] = {150, 400, 1024, 2048};
-  const int Ss[] = {1, 2, 4, 8};
+  const Cfg cfgs[] = {{"base nw8 u4", 0, 8, 4}, {"v2 nw8 u4", 1, 8, 4}, {"v2 nw8 u8", 1, 8, 8}, {"v2 nw4 u4", 1, 4, 4}};
+  const int lens[] = {2048, 4000};
+  const int Ss[] = {4, 8};
   hipStream_t st;
   CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
   float* q;

@@ -565,17 +565,24 @@ class Runner:
         self.s_hcount[row] = len(h)
         self._host_sampler[row] = (o, list(history), seed, step)
 
-    def _sample(self, B: int):
+    def _sample(self, B: int, feedback: bool = False):
+        """feedback (GPU): the sampler's finishing lane of each row also feeds the token back and
+        advances the row (what decode_feedback does), saving that launch in every decode step."""
         lg = self.full_logits
         if self.is_gpu:
             p = lambda t: t.data_ptr()  # noqa: E731
-            native().sample(dict(logits=p(lg), B=B, V=self.cfg.n_vocab, ld=lg.shape[1], temperature=p(self.s_temp),
-                                 top_k=p(self.s_topk), top_p=p(self.s_topp), min_p=p(self.s_minp),
-                                 repeat_penalty=p(self.s_rpen), presence_penalty=p(self.s_ppen),
-                                 frequency_penalty=p(self.s_fpen), history=p(self.s_hist),
-                                 hist_count=p(self.s_hcount), hist_cap=HIST_CAP, repeat_last_n=p(self.s_lastn),
-                                 seed=p(self.s_seed), step=p(self.s_step), out=p(self.s_out),
-                                 ws=p(self.s_ws), counters=p(self.s_tickets), err=p(self.s_err)), stream_handle())
+            d = dict(logits=p(lg), B=B, V=self.cfg.n_vocab, ld=lg.shape[1], temperature=p(self.s_temp),
+                     top_k=p(self.s_topk), top_p=p(self.s_topp), min_p=p(self.s_minp),
+                     repeat_penalty=p(self.s_rpen), presence_penalty=p(self.s_ppen),
+                     frequency_penalty=p(self.s_fpen), history=p(self.s_hist),
+                     hist_count=p(self.s_hcount), hist_cap=HIST_CAP, repeat_last_n=p(self.s_lastn),
+                     seed=p(self.s_seed), step=p(self.s_step), out=p(self.s_out),
+                     ws=p(self.s_ws), counters=p(self.s_tickets), err=p(self.s_err))
+            if feedback:
+                d.update(fb_step=p(self.d_step), fb_ld=self.d_step.shape[1], fb_block_table=p(self.d_block_table),
+                         fb_max_blocks=self.max_blocks, fb_bs=self.block_size,
+                         fb_host_ring=self._host_ring_dev if B == 1 else 0, fb_ring=self._ring_n)
+            native().sample(d, stream_handle())
         else:
             for b in range(B):
                 o, hist, seed, step = self._host_sampler[b]
@@ -587,12 +594,9 @@ class Runner:
     # ------------------------------------------------------------------ decode
     def _decode_body(self, B: int):
         self.forward(B, B, use_idx=False)
-        self._sample(B)
-        if self.is_gpu:  # token feedback + on-device advance of every row to its next position
-            native().decode_feedback(self.d_step.data_ptr(), self.d_step.shape[1], self.s_out.data_ptr(), B,
-                                     1, self.d_block_table.data_ptr(), self.max_blocks, self.block_size,
-                                     self._host_ring_dev if B == 1 else 0, self._ring_n, stream_handle())
-        else:
+        # GPU: the sampler also feeds each token back and advances its row on device (feedback.h)
+        self._sample(B, feedback=True)
+        if not self.is_gpu:
             self.d_tokens[:B].copy_(self.s_out[:B])
 
     def _graph(self, B: int, steps: int = 1):
