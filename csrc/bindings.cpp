@@ -486,6 +486,14 @@ PYBIND11_MODULE(_C, m) {
         L.down_exps = qm("down_exps");
         L.kc = Pp<void>(ptr("kc"));
         L.vc = Pp<void>(ptr("vc"));
+        L.c1_qkv = Pp<const float>(ptr("c1_qkv"));
+        L.c2_qkv = Pp<const float>(ptr("c2_qkv"));
+        L.c1_up = Pp<const float>(ptr("c1_up"));
+        L.c2_up = Pp<const float>(ptr("c2_up"));
+      })
+      .def("set_head_ln", [](Executor& e, uintptr_t c1, uintptr_t c2) {
+        e.lm_c1 = Pp<const float>(c1);
+        e.lm_c2 = Pp<const float>(c2);
       })
       .def("set_workspace", [](Executor& e, py::dict d) {
         auto ptr = [&](const char* k) -> uintptr_t { return d.contains(k) ? d[k].cast<uintptr_t>() : 0; };
@@ -527,6 +535,7 @@ PYBIND11_MODULE(_C, m) {
         w.x8e = Pp<void>(ptr("x8e"));
         w.x8f = Pp<void>(ptr("x8f"));
         w.x8st = Pp<float>(ptr("x8st"));
+        w.x8sum = Pp<float>(ptr("x8sum"));
         w.x8_ok = (d.contains("x8_ok") ? d["x8_ok"].cast<int>() : 0) && e.x8_capable() ? 1 : 0;
         {  // continuous-batching rows on the chain: as many as asked for and every emitter covers
           const int want = d.contains("x8_bmax") ? d["x8_bmax"].cast<int>() : 1;

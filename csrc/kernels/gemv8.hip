@@ -42,7 +42,7 @@ __global__ __launch_bounds__(GEMV_NT) void qgemv8_dual_kernel(GemvParams PA, Gem
 // host side
 namespace {
 
-size_t lds8(int K, int KS, int BT = 1) { return BT * x8_bytes(K) + (size_t)BT * (32 + (KS - 1) * GEMV_NT) * 4; }
+size_t lds8(int K, int KS, int BT = 1) { return BT * x8_bytes(K) + (size_t)BT * (48 + (KS - 1) * GEMV_NT) * 4; }
 
 // batch rows per launch: exactly B (1-4)
 int bt_of(int B) { return B; }
@@ -65,11 +65,12 @@ int emit_mode(const GemvParams& P) {
   if (!P.emit8) return EM_NONE;
   if (P.epi == EPI_ADD) return EM_ADD;
   if (P.epi == EPI_GLU || P.epi == EPI_GEGLU) return EM_GLU;
+  if (P.epi == EPI_GELU) return EM_ACT;
   return -1;
 }
 
 int in_mode(const GemvParams& P) {
-  if (P.x8) return P.x8_stat ? IN_X8_RMS : IN_X8;
+  if (P.x8) return P.x8_sum ? IN_X8_LN : P.x8_stat ? IN_X8_RMS : IN_X8;
   if (P.norm != NORM_NONE) return -1;  // fp32 input with a norm: gemv.hip's prologue
   return IN_MERGE;                      // merge slabs (O) or a plain fp32 row
 }
@@ -116,6 +117,9 @@ bool covered(const GemvParams& P, Geo& G) {
   if (in == IN_MERGE && P.merge_S > 0 && !(P.merge_S == 2 || P.merge_S == 4 || P.merge_S == 8)) return false;
   if (in == IN_MERGE && P.w.K % 16) return false;
   if (in == IN_X8_RMS && (P.w.K > 8192 || P.w.K % 64)) return false;
+  // LayerNorm'd images (Phi-2): batch 1, constants present, K split at most in 2
+  if (in == IN_X8_LN && (P.B != 1 || !P.x8_stat || !P.ln_c1 || !P.ln_c2 || P.w.K > 8192 || P.w.K % 64)) return false;
+  if (em == EM_ACT && (in != IN_X8_LN || P.w.N % 16 || P.row_offset)) return false;
   if (em == EM_ADD && (!P.emit8_nw || !P.emit8_stat || P.w.N % 16)) return false;
   if (em == EM_GLU && P.w.N % 32) return false;
   const int q = P.w.qtype;
@@ -127,6 +131,7 @@ bool covered(const GemvParams& P, Geo& G) {
   if (em == EM_GLU && G.J != 2) return false;  // a block owns whole groups: two tiles, unsplit K
   if (in != IN_MERGE && (size_t)G.ks * GEMV_NT * X8_NWI * 16 < x8_bytes(P.w.K)) return false;
   if (bt_of(P.B) >= 3 && !bt4_ok(q, G.ks, in)) return false;
+  if (in == IN_X8_LN && (G.ks > 2 || (G.nsb == 2 && G.J == 2))) return false;
   return lds8(P.w.K, G.ks, bt_of(P.B)) <= (P.B > 1 ? 160 : 64) * 1024;
 }
 
@@ -169,6 +174,12 @@ void launch_in(const GemvParams& P, const Geo& G, hipStream_t s) {
   const int em = emit_mode(P), in = in_mode(P);
   if (in == IN_X8) launch_em<QT, NSB, J, KS, IN_X8, 0>(P, em, G.grid, s);
   else if (in == IN_X8_RMS) launch_em<QT, NSB, J, KS, IN_X8_RMS, 0>(P, em, G.grid, s);
+  else if (in == IN_X8_LN) {  // batch 1; no emission (QKV, LM head) or the activated FFN up
+    if constexpr (KS <= 2) {
+      if (em == EM_ACT) launch_k<QT, NSB, J, KS, IN_X8_LN, 0, EM_ACT, 1>(P, G.grid, s);
+      else launch_k<QT, NSB, J, KS, IN_X8_LN, 0, EM_NONE, 1>(P, G.grid, s);
+    }
+  }
   else if constexpr (NSB == 1 && KS == 2 && J == 1) {  // O at 4096 < K <= 8192: plain fp32 rows
     launch_em<QT, 1, 1, 2, IN_MERGE, 1>(P, em, G.grid, s);
   } else if constexpr (NSB == 1 && KS == 1 && J == 1) {  // the O projection: merge slabs or plain fp32
@@ -261,6 +272,7 @@ bool gemv8(const GemvParams& P, hipStream_t s) {
 bool gemv8_2(const GemvParams& A, const GemvParams& B, hipStream_t s) {
   Geo GA, GB;
   if (!A.x8 || !B.x8 || A.x8 != B.x8 || A.emit8 || B.emit8 || A.w.K != B.w.K || A.B != B.B) return false;
+  if (A.x8_sum || B.x8_sum) return false;  // LayerNorm'd images: single launches
   if (!covered(A, GA) || !covered(B, GB) || GA.nsb != 1 || GA.ks != 1 || GB.nsb != 1 || GB.ks != 1) return false;
   const int gxa = (A.w.N + 15) / 16, gxb = (B.w.N + 15) / 16;  // one tile per block on both sides
   count_launch(LC_GEMV8_DUAL);

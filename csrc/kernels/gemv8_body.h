@@ -18,18 +18,23 @@ struct EpiPre {
   float pbias[J];    // EPI_QKV: bias[vn ^ 1] (RoPE pair partner)
   float fr[J];       // EPI_QKV: inv_freq[d / 2] of this row (0 beyond n_rot)
   float cs[J], sn[J];
+  float c1[J], c2[J];  // IN_X8_LN: the row's LayerNorm constants (GemvParams::ln_c1 / ln_c2)
   int pos, slot;     // EPI_QKV: row min(s, B - 1)
 };
 
 // PRE = false: the EM_ADD operands are read in the epilogue instead (the register-heaviest
 // instantiations, 2+ batch rows at a 3-4 way K split, would spill holding them)
-template <int EMIT, int J, int BT, bool PRE = true>
+template <int EMIT, int J, int BT, bool PRE = true, int IN = IN_X8>
 __device__ __forceinline__ void epi_prefetch(const GemvParams& P, int tile0, int rbase, int s, EpiPre<J, BT>& E) {
   const int N = P.w.N, bl = min(s, P.B - 1);
 #pragma unroll
   for (int j = 0; j < J; ++j) {
     const int n = min((tile0 + j) * 16 + rbase, N - 1), vn = n + P.row_offset;
     E.bias[j] = P.bias && PRE ? P.bias[vn] : 0.f;
+    if constexpr (IN == IN_X8_LN) {
+      E.c1[j] = P.ln_c1[n];
+      E.c2[j] = P.ln_c2[n];
+    }
     if constexpr (EMIT == EM_ADD && PRE) {
 #pragma unroll
       for (int b = 0; b < BT; ++b) E.res[j][b] = P.y[(long long)min(b, P.B - 1) * P.ldy + n];
@@ -125,14 +130,16 @@ __device__ __forceinline__ void epi_rows(const GemvParams& P, float (&acc)[1][BT
 template <int QT, int NSB, int J, int KS, int IN, int MS, int EMIT, int BT = 1>
 __device__ __forceinline__ void gemv8_body(const GemvParams& P, const int bx) {
   static_assert(BT == 1 || MS <= 1, "batched rows take the plain fp32 input (no deferred merge)");
+  static_assert(IN != IN_X8_LN || BT == 1, "LayerNorm'd images: batch 1 (Phi-2 decode)");
+  static_assert(EMIT != EM_ACT || IN == IN_X8_LN, "EM_ACT: Phi-2's FFN up only");
   constexpr int NT = GEMV_NT * KS;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const QMat& w = P.w;
   const int K = w.K, N = w.N, SB = n_sb(K), XS = SB * XPAD, XSP = x8_slots_dev(K);
   i32x4* lq = (i32x4*)smem;                           // [BT][XSP]
   f32x2* lf = (f32x2*)(smem + (size_t)BT * XSP * 16);  // [BT][XSP]
-  float* stage = (float*)(lf + BT * XSP);             // [BT][32]: emitted values, their squares
-  float* part = stage + 32 * BT;                      // [KS - 1][BT][GEMV_NT] partial sums of the K split
+  float* stage = (float*)(lf + BT * XSP);             // [BT][48]: emitted values, their squares, plain values
+  float* part = stage + 48 * BT;                      // [KS - 1][BT][GEMV_NT] partial sums of the K split
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = lane >> 4, s = lane & 15;
   const int kg = KS > 1 ? wave / GEMV_NW : 0, gtid = tid - kg * GEMV_NT;
   // K-split groups (ks_chunk): aligned to 16 super-blocks when the row stride keeps piece runs on lines
@@ -148,9 +155,10 @@ __device__ __forceinline__ void gemv8_body(const GemvParams& P, const int bx) {
   // 0. epilogue operands (EpiPre), then 1. the activation operands: both return ahead of the weights
   constexpr bool PRE = BT == 1 || KS <= 2;
   EpiPre<J, BT> pre;
-  epi_prefetch<EMIT, J, BT, PRE>(P, tile0, rbase, s, pre);
+  epi_prefetch<EMIT, J, BT, PRE, IN>(P, tile0, rbase, s, pre);
   u32x4 xw[BT][X8_NWI];
   f32x4 stv[BT][X8_NSTW];
+  f32x4 sxv[IN == IN_X8_LN ? X8_NSTW : 1];  // IN_X8_LN: the per-group sums
   // groups per thread of the merge prologue: the block's NT = GEMV_NT * KS threads cover KS * 4096
   // elements per group slot (O at K = 5120, Llama-2-13B, takes KS = 2)
   constexpr int MG = IN == IN_MERGE ? NSB : 1;
@@ -168,13 +176,17 @@ __device__ __forceinline__ void gemv8_body(const GemvParams& P, const int bx) {
 #pragma unroll
       for (int i = 0; i < X8_NWI; ++i)
         xw[b][i] = ((const u32x4*)((const char*)P.x8 + min(b, blast) * img_b))[min(tid + NT * i, nwords - 1)];
-    if constexpr (IN == IN_X8_RMS) {
+    if constexpr (IN == IN_X8_RMS || IN == IN_X8_LN) {
       const int n4 = K / 64;  // f32x4 of partials (K / 16 floats)
 #pragma unroll
       for (int b = 0; b < BT; ++b)
 #pragma unroll
         for (int i = 0; i < X8_NSTW; ++i)
           stv[b][i] = ((const f32x4*)(P.x8_stat + min(b, blast) * st_ld))[min(lane + 64 * i, n4 - 1)];
+      if constexpr (IN == IN_X8_LN) {
+#pragma unroll
+        for (int i = 0; i < X8_NSTW; ++i) sxv[i] = ((const f32x4*)P.x8_sum)[min(lane + 64 * i, n4 - 1)];
+      }
     }
   } else {
 #pragma unroll
@@ -209,7 +221,7 @@ __device__ __forceinline__ void gemv8_body(const GemvParams& P, const int bx) {
 
   // 3. the activation images into LDS (the copy waits for the activation loads only); a row's image
   //    is [XSP] int8 words then [XSP] (d, d * sum q) pairs, split here into the lq / lf planes
-  float rstd[BT];
+  float rstd[BT], mu_rstd = 0.f;  // IN_X8_LN: mean * rstd (batch 1)
 #pragma unroll
   for (int b = 0; b < BT; ++b) rstd[b] = 1.f;
   if constexpr (IN != IN_MERGE) {
@@ -233,6 +245,18 @@ __device__ __forceinline__ void gemv8_body(const GemvParams& P, const int bx) {
           if (lane + 64 * i < n4) ss += stv[b][i].x + stv[b][i].y + stv[b][i].z + stv[b][i].w;
         rstd[b] = rsqrtf(wave_sum(ss) / K + P.eps);
       }
+    } else if constexpr (IN == IN_X8_LN) {
+      const int n4 = K / 64;
+      float ss = 0.f, sx = 0.f;
+#pragma unroll
+      for (int i = 0; i < X8_NSTW; ++i)
+        if (lane + 64 * i < n4) {
+          ss += stv[0][i].x + stv[0][i].y + stv[0][i].z + stv[0][i].w;
+          sx += sxv[i].x + sxv[i].y + sxv[i].z + sxv[i].w;
+        }
+      const float mu = wave_sum(sx) / K;
+      rstd[0] = rsqrtf(fmaxf(wave_sum(ss) / K - mu * mu, 0.f) + P.eps);
+      mu_rstd = mu * rstd[0];
     }
   } else {
 #pragma unroll
@@ -334,6 +358,10 @@ __device__ __forceinline__ void gemv8_body(const GemvParams& P, const int bx) {
     }
 #pragma unroll
     for (int b = 0; b < BT; ++b) acc[0][b] *= rstd[b];
+    // LayerNorm: rstd * (dot - mu * c1) + c2, the row's constant terms on one lane of its 16
+    if constexpr (IN == IN_X8_LN) {
+      if (s == 0) acc[0][0] += pre.c2[j] - mu_rstd * pre.c1[j];
+    }
     if constexpr (EMIT == EM_NONE) {
       if (kg == 0) epi_rows<J, BT>(P, acc, t * 16 + rbase, s, j, pre);
     } else {
@@ -354,17 +382,31 @@ __device__ __forceinline__ void gemv8_body(const GemvParams& P, const int bx) {
               nv = (PRE ? pre.res[j][b] + pre.bias[j] : *dst + (P.bias ? P.bias[n] : 0.f)) + v[b];
               *dst = nv;
             }
-            stage[32 * b + rbase] = n < N ? nv * (PRE ? pre.nw[j] : P.emit8_nw[n]) : 0.f;
-            stage[32 * b + 16 + rbase] = nv * nv;
+            stage[48 * b + rbase] = n < N ? nv * (PRE ? pre.nw[j] : P.emit8_nw[n]) : 0.f;
+            stage[48 * b + 16 + rbase] = nv * nv;
+            stage[48 * b + 32 + rbase] = nv;
           }
         }
         __syncthreads();
         if (tid < 16 * nb) {  // batch row tid / 16 on 16 lanes of wave 0
           const int b = tid >> 4, i = tid & 15;
-          emit_group16((char*)P.emit8 + (size_t)b * x8_slots_dev(N) * 24, N, t, stage[32 * b + i], stage[32 * b + 16 + i],
-                       P.emit8_stat + b * x8_stat_ld_dev(N), i);
+          emit_group16((char*)P.emit8 + (size_t)b * x8_slots_dev(N) * 24, N, t, stage[48 * b + i], stage[48 * b + 16 + i],
+                       P.emit8_stat + b * x8_stat_ld_dev(N), i, stage[48 * b + 32 + i],
+                       P.emit8_sum ? P.emit8_sum + b * x8_stat_ld_dev(N) : nullptr);
         }
         __syncthreads();  // the stage is reused by the next tile
+      } else if constexpr (EMIT == EM_ACT) {  // one group per tile: act(v + bias) (EPI_GELU)
+        if (kg == 0 && s == 0) {
+          const float h = n < N ? gelu_tanh(v[0] + pre.bias[j]) : 0.f;
+          if (n < N) P.y[n] = h;
+          stage[rbase] = h;
+        }
+        __syncthreads();
+        if (tid < 16) {
+          const int Kc = P.emit8_k > 0 ? P.emit8_k : N;  // the consumer's (possibly padded) K
+          emit_group16(P.emit8, Kc, t, stage[tid], 0.f, nullptr, tid);
+        }
+        __syncthreads();
       } else {  // EM_GLU: even row = gate, odd = up; 8 outputs per tile, a group per tile pair
         const int half = (t & 1) * 8;
         if (kg == 0 && s == 0 && (rbase & 1) == 0) {
@@ -372,8 +414,8 @@ __device__ __forceinline__ void gemv8_body(const GemvParams& P, const int bx) {
           for (int b = 0; b < BT; ++b) {
             const float h = n < N ? (P.epi == EPI_GEGLU ? gelu_tanh(v[b]) : silu(v[b])) * pv[b] : 0.f;
             if (n < N && b < nb) P.y[(long long)b * P.ldy + (n >> 1)] = h;
-            stage[32 * b + half + (rbase >> 1)] = h;
-            if (half == 0 && t + 1 >= n_tiles) stage[32 * b + 8 + (rbase >> 1)] = 0.f;  // trailing half group
+            stage[48 * b + half + (rbase >> 1)] = h;
+            if (half == 0 && t + 1 >= n_tiles) stage[48 * b + 8 + (rbase >> 1)] = 0.f;  // trailing half group
           }
         }
         if ((t & 1) || t + 1 >= n_tiles) {
@@ -381,7 +423,7 @@ __device__ __forceinline__ void gemv8_body(const GemvParams& P, const int bx) {
           if (tid < 16 * nb) {
             const int b = tid >> 4, i = tid & 15;
             const int Kc = P.emit8_k > 0 ? P.emit8_k : N / 2;  // the consumer's (possibly padded) K
-            emit_group16((char*)P.emit8 + (size_t)b * x8_slots_dev(Kc) * 24, Kc, t >> 1, stage[32 * b + i], 0.f,
+            emit_group16((char*)P.emit8 + (size_t)b * x8_slots_dev(Kc) * 24, Kc, t >> 1, stage[48 * b + i], 0.f,
                          nullptr, i);
           }
           __syncthreads();

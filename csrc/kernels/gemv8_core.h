@@ -5,8 +5,10 @@
 
 namespace omx {
 
-enum { IN_X8 = 0, IN_X8_RMS = 1, IN_MERGE = 2 };
-enum { EM_NONE = 0, EM_ADD = 1, EM_GLU = 2 };
+// IN_X8_LN: a LayerNorm'd image (x * ln_w) with sums and sums of squares (Phi-2, GemvParams::x8_sum)
+enum { IN_X8 = 0, IN_X8_RMS = 1, IN_MERGE = 2, IN_X8_LN = 3 };
+// EM_ACT: a plain activated output (EPI_GELU: Phi-2's FFN up), one group per 16-row tile, no partials
+enum { EM_NONE = 0, EM_ADD = 1, EM_GLU = 2, EM_ACT = 3 };
 
 __device__ __forceinline__ int x8_slots_dev(int K) { return ((n_sb(K) * XPAD + 1) + 1) & ~1; }
 
@@ -54,7 +56,9 @@ __device__ __forceinline__ void emit_group(void* img, int Kc, int G, const float
 // 16-lane shuffles, one byte store per lane, lane 0 writes the scale pair and the RMS partial. The same
 // codes and scales as emit_group (integer sum, exact max); the partial's float sum is a tree. The
 // producers' tails ran the one-lane form: ~0.6 us of gate_up's 12 us (scripts/bench_gemv8.py NOEMIT)
-__device__ __forceinline__ void emit_group16(void* img, int Kc, int G, float v, float sq, float* stat, int i) {
+// sx / ssum (optional): the group's plain sum as well (a LayerNorm'd consumer's mean)
+__device__ __forceinline__ void emit_group16(void* img, int Kc, int G, float v, float sq, float* stat, int i,
+                                             float sx = 0.f, float* ssum = nullptr) {
   float amax = fabsf(v);
 #pragma unroll
   for (int m = 8; m >= 1; m >>= 1) amax = fmaxf(amax, __shfl_xor(amax, m, 16));
@@ -72,6 +76,11 @@ __device__ __forceinline__ void emit_group16(void* img, int Kc, int G, float v, 
 #pragma unroll
     for (int m = 8; m >= 1; m >>= 1) ss += __shfl_xor(ss, m, 16);
     if (i == 0) stat[G] = ss;
+  }
+  if (ssum) {
+#pragma unroll
+    for (int m = 8; m >= 1; m >>= 1) sx += __shfl_xor(sx, m, 16);
+    if (i == 0) ssum[G] = sx;
   }
 }
 

@@ -90,13 +90,26 @@ bool Executor::chain_capable() const {
 // Under tensor parallelism the chain runs inside forward_tp only (the custom all-reduce is what emits
 // the QKV / gate_up / LM-head images there: ar_allreduce_add_emit); the RCCL prefill path keeps fp32.
 bool Executor::x8(const StepInputs& in) const {
+  if (cfg.arch == 1) return ws.x8_ok && in.B == 1 && !in.prefill && cfg.tp == 1 && ln8();
   return ws.x8_ok && (in.B == 1 || in.B <= ws.x8_bmax) && !in.prefill && (cfg.tp == 1 || ar_active_) &&
          cfg.arch == 0 && cfg.n_expert == 0;
 }
 
+// Phi-2 (parallel attention/FFN block, LayerNorm): the same chain, batch 1. down emits the next layer's
+// image of resid * attn_norm_w with sums and sums of squares (the LayerNorm's mean and variance); QKV
+// and FFN up both consume it (rstd * (dot - mu * c1) + c2, GemvParams::ln_c1 / ln_c2), FFN up emits
+// gelu(.) for down. O adds to the residual without emitting (its consumer is down, through resid).
+bool Executor::ln8() const {
+  if (cfg.arch != 1 || cfg.tp != 1 || cfg.n_expert != 0 || !ws.x8sum || cfg.E % 16) return false;
+  for (const LayerW& L : layers)
+    if (!L.c1_qkv || !L.c2_qkv || !L.c1_up || !L.c2_up || !L.attn_norm || !L.attn_norm_b) return false;
+  return true;
+}
+
 // layer 0's QKV input image written by the embedding gather (E % 16 == 0, a dense llama-family stack)
 bool Executor::x8_layer0(const StepInputs& in) const {
-  return x8(in) && !layers.empty() && cfg.E % 16 == 0 && layers[0].attn_norm && ws.x8e && ws.x8st;
+  return x8(in) && !layers.empty() && cfg.E % 16 == 0 && layers[0].attn_norm && ws.x8e && ws.x8st &&
+         (cfg.arch != 1 || ws.x8sum);
 }
 
 static void x8_in(GemvParams& P, const void* img, const float* stat) {
@@ -114,6 +127,29 @@ static void x8_emit(GemvParams& P, void* img, const float* nw, float* stat) {
 // residual / GLU rows too); an emitter the int8 kernel does not cover would leave its consumer a stale
 // image, so the chain is on only when every emitter is covered
 bool Executor::x8_capable(int B) const {
+  if (cfg.arch == 1 && B == 1 && ln8() && ws.x8e && ws.x8f && ws.x8st) {  // the emitters: FFN up, down
+    static const float dummy[4] = {0.f, 0.f, 0.f, 0.f};
+    for (const LayerW& L : layers) {
+      GemvParams U{};
+      U.w = L.wgu;
+      U.B = 1;
+      U.epi = EPI_GELU;
+      U.n_sel = 1;
+      x8_in(U, dummy, dummy);
+      U.x8_sum = U.ln_c1 = U.ln_c2 = dummy;
+      U.emit8 = (void*)dummy;
+      GemvParams D{};
+      D.w = L.wdown;
+      D.B = 1;
+      D.epi = EPI_ADD;
+      D.n_sel = 1;
+      x8_in(D, dummy, nullptr);
+      x8_emit(D, (void*)dummy, dummy, (float*)dummy);
+      D.emit8_sum = (float*)dummy;
+      if (!gemv8_supported(U) || !gemv8_supported(D)) return false;
+    }
+    return true;
+  }
   if (cfg.arch != 0 || cfg.n_expert != 0 || layers.empty() || !ws.x8e || !ws.x8f || !ws.x8st) return false;
   const bool tp = cfg.tp > 1;  // O and down write partial sums to the all-reduce slabs, which emits
   static const float dummy[4] = {0.f, 0.f, 0.f, 0.f};
@@ -150,7 +186,8 @@ void Executor::embed(const StepInputs& in, hipStream_t s) {
   // for every later layer, so layer 0 takes the same int8 GEMV instead of the fp32-prologue one
   const bool q8 = x8_layer0(in);
   embed_rows(tok_embd, in.tokens, in.B, ws.resid, cfg.E, s, cfg.embed_scale, ws.ext, chain(in) ? ws.st[1] : nullptr,
-             q8 ? ws.x8e : nullptr, q8 ? layers[0].attn_norm : nullptr, q8 ? ws.x8st : nullptr);
+             q8 ? ws.x8e : nullptr, q8 ? layers[0].attn_norm : nullptr, q8 ? ws.x8st : nullptr,
+             q8 && cfg.arch == 1 ? ws.x8sum : nullptr);
 }
 
 void Executor::attn_block(int i, const StepInputs& in, hipStream_t s) {
@@ -184,7 +221,14 @@ void Executor::attn_block(int i, const StepInputs& in, hipStream_t s) {
   const bool q8 = x8(in);
   if (ch && i > 0) chain_in(P, ws.xa16, ws.ld_e, ws.st[1], (E + 15) / 16);  // emitted by layer i-1's down
   if (ch) P.rexp_out = ws.st[1] + 16 * ((E + 15) / 16) + 16;  // O's range exponents (layer 0: from resid)
-  if (q8 && (i > 0 || x8_layer0(in))) x8_in(P, ws.x8e, ws.x8st);  // emitted by layer i-1's down / the embed
+  if (q8 && (i > 0 || x8_layer0(in))) {  // emitted by layer i-1's down / the embed
+    x8_in(P, ws.x8e, ws.x8st);
+    if (phi) {
+      P.x8_sum = ws.x8sum;
+      P.ln_c1 = L.c1_qkv;
+      P.ln_c2 = L.c2_qkv;
+    }
+  }
   if (!L.qkv_fused) {  // q,k and v rows of different quant types: one dual launch at B == 1
     GemvParams V = P;
     V.w = L.wv;
@@ -203,6 +247,14 @@ void Executor::attn_block(int i, const StepInputs& in, hipStream_t s) {
     U.bias = L.bup;
     U.y = ws.hbuf;
     U.ldy = cfg.F;
+    if (q8 && (i > 0 || x8_layer0(in))) {  // same image as QKV; emits down's input
+      x8_in(U, ws.x8e, ws.x8st);
+      U.x8_sum = ws.x8sum;
+      U.ln_c1 = L.c1_up;
+      U.ln_c2 = L.c2_up;
+      U.emit8 = ws.x8f;
+      U.emit8_k = cfg.F;
+    }
     gemv(U, s);
   }
   // --- attention over the paged cache
@@ -271,7 +323,7 @@ void Executor::attn_block(int i, const StepInputs& in, hipStream_t s) {
     chain_emit(O, ws.xa16, ws.ld_e, L.ffn_norm, ws.st[0], nullptr);  // gate_up's RMSNorm input
     O.rexp_in = ws.st[1] + 16 * ((E + 15) / 16) + 16;
   }
-  if (q8 && cfg.tp == 1) x8_emit(O, ws.x8e, L.ffn_norm, ws.x8st);  // gate_up's RMSNorm input, int8
+  if (q8 && cfg.tp == 1 && !phi) x8_emit(O, ws.x8e, L.ffn_norm, ws.x8st);  // gate_up's RMSNorm input, int8
   gemv(O, s);
 }
 
@@ -286,6 +338,13 @@ void Executor::ffn_block(int i, const StepInputs& in, hipStream_t s) {
     Dn.bias = L.bdown;
     Dn.y = dst;
     Dn.ldy = E;
+    Dn.k_valid = cfg.F_valid;
+    if (x8(in)) {  // FFN up's image in; the next layer's QKV / up (or the LM head) image out
+      const bool last = i + 1 >= (int)layers.size();
+      x8_in(Dn, ws.x8f, nullptr);
+      x8_emit(Dn, ws.x8e, last ? out_norm : layers[i + 1].attn_norm, ws.x8st);
+      Dn.emit8_sum = ws.x8sum;
+    }
     gemv(Dn, s);
     return;
   }
@@ -436,7 +495,16 @@ void Executor::head(const StepInputs& in, hipStream_t s) {
   P.ldy = lm_head.N;
   if (chain(in) && x == ws.resid && in.n_logits == in.B && cfg.n_layer > 0)
     chain_in(P, ws.xa16, ws.ld_e, ws.st[1], (E + 15) / 16);
-  if (x8(in) && x == ws.resid && in.n_logits == in.B && cfg.n_layer > 0) x8_in(P, ws.x8e, ws.x8st);
+  if (x8(in) && x == ws.resid && in.n_logits == in.B && cfg.n_layer > 0) {
+    if (cfg.arch != 1) {
+      x8_in(P, ws.x8e, ws.x8st);
+    } else if (lm_c1 && lm_c2 && out_norm && out_norm_b) {  // else the fp32 LayerNorm prologue
+      x8_in(P, ws.x8e, ws.x8st);
+      P.x8_sum = ws.x8sum;
+      P.ln_c1 = lm_c1;
+      P.ln_c2 = lm_c2;
+    }
+  }
   gemv(P, s);
 }
 

@@ -45,6 +45,11 @@ struct LayerW {
   QMat down_exps{};      // [X][E][F]
   void* kc = nullptr;    // fp16 [nblk][Hkv][bs][D]
   void* vc = nullptr;
+  // phi2 int8 chain: LayerNorm constants of the two attn_norm consumers (GemvParams::ln_c1 / ln_c2)
+  const float* c1_qkv = nullptr;
+  const float* c2_qkv = nullptr;
+  const float* c1_up = nullptr;
+  const float* c2_up = nullptr;
 };
 
 struct Workspace {
@@ -91,6 +96,7 @@ struct Workspace {
   void* x8e = nullptr;
   void* x8f = nullptr;
   float* x8st = nullptr;
+  float* x8sum = nullptr;    // phi2: per-group sums of the E-wide rows (LayerNorm mean), x8st's layout
   int x8_ok = 0;
   int x8_bmax = 1;           // batch rows the chain takes (continuous batching: up to X8_MAX_B)
 };
@@ -124,6 +130,8 @@ class Executor {
   QMat lm_head{};
   const float* lm_bias = nullptr;
   const float* inv_freq = nullptr;
+  const float* lm_c1 = nullptr;  // phi2 int8 chain: the LM head's LayerNorm constants (out_norm)
+  const float* lm_c2 = nullptr;
   Workspace ws;
 
   void embed(const StepInputs& in, hipStream_t s);
@@ -146,6 +154,7 @@ class Executor {
   bool chain(const StepInputs& in) const;  // this step runs the fp16 matrix-core decode chain
   bool x8_layer0(const StepInputs& in) const;  // the embed writes layer 0's int8 QKV image
   bool x8(const StepInputs& in) const;     // this step runs the batch-1 int8 activation chain
+  bool ln8() const;                        // the phi2 (LayerNorm) form of that chain is set up
   int ar_active_ = 0;
 };
 

@@ -52,6 +52,8 @@ class NativeExec:
                          kv8=int(getattr(r, "kv8", False)), F_valid=loc["F"] - getattr(w, "ffn_pad", 0)))
         p = lambda t: t.data_ptr() if t is not None else 0  # noqa: E731
         e.set_globals(w.tok_embd.tup, p(w.out_norm), p(w.out_norm_b), w.lm_head.tup, p(w.lm_bias), p(w.inv_freq))
+        if getattr(w, "lm_c1", None) is not None and self.on_gpu:  # phi2 int8 chain (executor.cpp ln8)
+            e.set_head_ln(p(w.lm_c1), p(w.lm_c2))
         for i, L in enumerate(w.layers):
             d = {}
             for k, v in L.items():
@@ -100,6 +102,7 @@ class NativeExec:
         if not b:
             return {}
         return dict(x8e=b["x8e"].data_ptr(), x8f=b["x8f"].data_ptr(), x8st=b["x8st"].data_ptr(), x8_ok=1,
+                    x8sum=b["x8sum"].data_ptr(),
                     # batch rows on the chain: B = 2 measured 1.73 vs 2.08 ms per step on the int8 rows, B = 3
                     # 2.15 vs 2.19 ms; at 4 rows layout M's MFMA GEMVs win (profiles/r4_batch), so 3 by default
                     x8_bmax=int(os.environ.get("OMX_X8_BATCH", "3")))
@@ -222,7 +225,8 @@ class Runner:
             u8 = dict(device=dev, dtype=torch.uint8)
             nb = 4  # batch rows of the chain (gemv8.hip X8_MAX_B): row b's image at b * x8_bytes
             self.x8_bufs = dict(x8e=torch.zeros(nb * C.x8_bytes(E), **u8), x8f=torch.zeros(nb * C.x8_bytes(Fl), **u8),
-                                x8st=torch.zeros(nb * C.x8_stat_ld(E) + 4, **f32))
+                                x8st=torch.zeros(nb * C.x8_stat_ld(E) + 4, **f32),
+                                x8sum=torch.zeros(nb * C.x8_stat_ld(E) + 4, **f32))  # phi2: LayerNorm means
         # MoE prefill grouping (csrc/kernels/moe.hip moe_sort -> grouped MFMA GEMM)
         n_pairs = max_batch * ksel
         self.moe_rows = torch.zeros(n_pairs, **i32)

@@ -346,9 +346,40 @@ class DeviceWeights:
         self.lm_head = build_qmat(src, [(out_name, ar(Vl, r * Vl), ar(Vl))], Vl, E, None, dev)
         self.lm_bias = t(src.f32("output.bias")[r * Vl:(r + 1) * Vl]) if src.has("output.bias") else None
         self.inv_freq = t(rope_inv_freq(cfg.n_rot, cfg.rope_base))
+        self.lm_c1 = self.lm_c2 = None
+        if phi and T == 1 and str(dev).startswith("cuda") and os.environ.get("OMX_X8_LN", "1") != "0":
+            self._ln_consts()
         # the GGUF mapping (and any requantised copies) is no longer needed: dropping it releases the
         # file's resident pages (a CPU server would otherwise hold the blob twice in RSS)
         self.src = None
+
+    def _ln_consts(self) -> None:
+        """Phi-2 int8 decode chain (executor.cpp ln8): the LayerNorm constants c1 = W . ln_w and
+        c2 = W . ln_b of every LayerNorm'd consumer (QKV and FFN up with attn_norm, the LM head with
+        output_norm), so the GEMV computes W . LN(x) = rstd * (W . (x * ln_w) - mu * c1) + c2 from the
+        producer's int8 image of x * ln_w. W is this matrix as stored (fp16-dequantised on the device,
+        gemm.hip's dequant_f16), the dot products in fp32."""
+        from ..ops import stream_handle
+        C = native()
+        dev = self.device
+
+        def consts(q: "DevQMat", w: torch.Tensor, b: torch.Tensor | None):
+            buf = torch.empty(q.N, q.K, dtype=torch.float16, device=dev)
+            C.dequant_f16(q.tup, buf.data_ptr(), stream_handle(), 0)
+            c1 = torch.empty(q.N, dtype=torch.float32, device=dev)
+            c2 = torch.zeros(q.N, dtype=torch.float32, device=dev)
+            for r0 in range(0, q.N, 8192):
+                blk = buf[r0:r0 + 8192].float()
+                c1[r0:r0 + 8192] = blk @ w
+                if b is not None:
+                    c2[r0:r0 + 8192] = blk @ b
+            return c1, c2
+
+        for L in self.layers:
+            L["c1_qkv"], L["c2_qkv"] = consts(L["wqk"], L["attn_norm"], L["attn_norm_b"])
+            L["c1_up"], L["c2_up"] = consts(L["wgu"], L["attn_norm"], L["attn_norm_b"])
+        if self.out_norm_b is not None:
+            self.lm_c1, self.lm_c2 = consts(self.lm_head, self.out_norm, self.out_norm_b)
 
     def build_mfma_layouts(self) -> int:
         """Layout M copies of every dense projection (+ LM head) for continuous-batching decode steps

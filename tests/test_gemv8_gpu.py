@@ -188,6 +188,55 @@ def test_engine_x8_chain_on_and_matches_torch(tmp_path):
         assert rel(g.logits[0, :V].cpu(), c.logits[0, :V]) < 3e-2
 
 
+@pytest.mark.parametrize("ftype", ["MOSTLY_Q4_0", "MOSTLY_Q4_K_M"])
+def test_engine_phi2_ln_chain_matches_torch(tmp_path, ftype):
+    """Phi-2 batch-1 decode on the LayerNorm form of the int8 chain (executor.cpp ln8): down emits
+    x * ln_w with per-group sums and sums of squares, QKV / FFN up / the LM head apply
+    rstd * (dot - mu * c1) + c2 (engine/weights.py _ln_consts), FFN up emits gelu(.) for down.
+    Teacher-forced decode steps track the fp32 torch twin; with the chain off (OMX_X8_LN=0) the fp32
+    LayerNorm prologue path gives the same logits."""
+    import os
+    from ollama_operator_amd.engine.runner import Runner
+    from ollama_operator_amd.gguf.constants import FileType
+    from ollama_operator_amd.models.config import preset
+    from ollama_operator_amd.models.random_init import write_random_gguf
+    p = str(tmp_path / "phi.gguf")
+    write_random_gguf(p, preset("tiny-phi2"), getattr(FileType, ftype), seed=6, quantize_from_float=True)
+    g = Runner(p, device="cuda:0", max_batch=16, max_seqs=1, ctx=256)
+    assert g.exe.exe.x8_on == 1
+    os.environ["OMX_X8_LN"] = "0"
+    try:
+        g0 = Runner(p, device="cuda:0", max_batch=16, max_seqs=1, ctx=256)
+    finally:
+        del os.environ["OMX_X8_LN"]
+    assert g0.exe.exe.x8_on == 0
+    c = Runner(p, device="cpu", max_batch=16, max_seqs=1, ctx=256, cpu_backend="torch")
+    prompt = [1, 17, 33, 49, 65]
+    sg, s0, sc = g.new_sequence(), g0.new_sequence(), c.new_sequence()
+    for r, sid in ((g, sg), (g0, s0), (c, sc)):
+        r.prefill(sid, prompt)
+    V = g.cfg.n_vocab
+    L = g.cfg.n_layer
+    for i, t in enumerate([8, 9, 10, 11, 12]):
+        eager = i == 4
+        outs = []
+        for r, sid in ((g, sg), (g0, s0)):
+            r.set_tokens([t])
+            r.use_graphs = not eager
+            C().reset_launch_counts()
+            r.decode_step(sid)
+            torch.cuda.synchronize()
+            if eager and r is g:
+                n = C().launch_counts()
+                # QKV, FFN up and down of every layer plus the LM head on the chain (O: the merge GEMV)
+                assert n["gemv8_row1"] >= 3 * L + 1, n
+            r.kv.seqs[sid].tokens.append(t)
+            outs.append(r.logits[0, :V].float().cpu().clone())
+        c.prefill(sc, [t])
+        assert rel(outs[0], c.logits[0, :V]) < 3e-2, i
+        assert rel(outs[0], outs[1]) < 2e-2, i
+
+
 def images(xs, nw=None):
     """B rows -> the batched image buffer (row b at b * x8_bytes(K)) and RMS partials (stride x8_stat_ld)."""
     K = xs.shape[1]
