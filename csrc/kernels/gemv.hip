@@ -856,7 +856,9 @@ void reset_launch_counts() {
 }
 
 void gemv(const GemvParams& P0, hipStream_t s) {
-  if ((P0.x8 || P0.emit8) && gemv8(P0, s)) return;  // int8 activation chain (gemv8.hip)
+  // int8 activation chain (gemv8.hip); also the batch-1 deferred-merge residual add (Phi-2's O)
+  const bool merge_add = P0.merge_S > 1 && P0.epi == EPI_ADD && P0.B == 1 && !P0.expert_ids;
+  if ((P0.x8 || P0.emit8 || merge_add) && gemv8(P0, s)) return;
   if (P0.emit8) throw std::runtime_error("gemv: int8 activation emitter not covered by gemv8");
   if (P0.w.qtype == QT_F16) {  // fp16 weights (vision tower): the stream-order GEMM only
     if (!dq_gemm(P0, s)) throw std::runtime_error("gemv: F16 weights need >= 128 rows and an fp16 workspace");

@@ -31,11 +31,13 @@ __global__ __launch_bounds__(GEMV_NT * KS) void qgemv8_kernel(GemvParams P) {
   gemv8_body<QT, NSB, J, KS, IN, MS, EMIT, BT>(P, blockIdx.x);
 }
 
-// q,k rows + v rows of different quant types (Q4_K_M QKV) over the same image: one launch
-template <int QA, int QB, int IN, int BT>
+// q,k rows + v rows of different quant types (Q4_K_M QKV) over the same image: one launch. Phi-2: QKV
+// and the FFN up (EMB = EM_ACT, emitting down's image) over the same LayerNorm'd image
+// NSB = 2: 4096 < K <= 8192 (Llama-2-13B's QKV at K = 5120, two super-blocks per lane on both sides)
+template <int QA, int QB, int IN, int BT, int EMB = EM_NONE, int NSB = 1>
 __global__ __launch_bounds__(GEMV_NT) void qgemv8_dual_kernel(GemvParams PA, GemvParams PB, int gxa) {
-  if ((int)blockIdx.x < gxa) gemv8_body<QA, 1, 1, 1, IN, 0, EM_NONE, BT>(PA, blockIdx.x);
-  else gemv8_body<QB, 1, 1, 1, IN, 0, EM_NONE, BT>(PB, (int)blockIdx.x - gxa);
+  if ((int)blockIdx.x < gxa) gemv8_body<QA, NSB, 1, 1, IN, 0, EM_NONE, BT>(PA, blockIdx.x);
+  else gemv8_body<QB, NSB, 1, 1, IN, 0, EMB, BT>(PB, (int)blockIdx.x - gxa);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -86,6 +88,7 @@ bool geometry(const GemvParams& P, Geo& G) {
   if (need == 1) { G.nsb = 1; G.ks = 1; }
   else if (need == 2) { G.nsb = tiles > 512 ? 2 : 1; G.ks = tiles > 512 ? 1 : 2; }
   else if (need <= 4) { G.nsb = 1; G.ks = need; }
+  else if (need <= 8) { G.nsb = 2; G.ks = (need + 1) / 2; }  // Llama-2-70B ffn_down (K = 28672): 4 x 32 SBs
   else return false;
   if (G.ks > 1) {
     G.J = 1;
@@ -113,7 +116,9 @@ bool covered(const GemvParams& P, Geo& G) {
   const int em = emit_mode(P), in = in_mode(P);
   if (em < 0 || in < 0) return false;
   if (P.B > 1 && in == IN_MERGE && P.merge_S > 0) return false;  // batched rows: plain fp32 attention rows
-  if (!P.x8 && !P.emit8) return false;  // nothing for this path to do
+  // nothing for this path to do -- except the batch-1 deferred-merge residual add without emission
+  // (Phi-2's O: its consumer reads the residual through down's emission)
+  if (!P.x8 && !P.emit8 && !(in == IN_MERGE && P.merge_S > 1 && P.epi == EPI_ADD && P.B == 1)) return false;
   if (in == IN_MERGE && P.merge_S > 0 && !(P.merge_S == 2 || P.merge_S == 4 || P.merge_S == 8)) return false;
   if (in == IN_MERGE && P.w.K % 16) return false;
   if (in == IN_X8_RMS && (P.w.K > 8192 || P.w.K % 64)) return false;
@@ -129,9 +134,15 @@ bool covered(const GemvParams& P, Geo& G) {
   // (merge_S > 1) exists for the unsplit geometry only
   if (in == IN_MERGE && (P.w.K > GEMV_NT * G.ks * G.nsb * 16 || (P.merge_S > 1 && G.ks > 1))) return false;
   if (em == EM_GLU && G.J != 2) return false;  // a block owns whole groups: two tiles, unsplit K
-  if (in != IN_MERGE && (size_t)G.ks * GEMV_NT * X8_NWI * 16 < x8_bytes(P.w.K)) return false;
+  if (in != IN_MERGE && (size_t)G.ks * GEMV_NT * x8_nwi(G.nsb, G.ks) * 16 < x8_bytes(P.w.K)) return false;
   if (bt_of(P.B) >= 3 && !bt4_ok(q, G.ks, in)) return false;
   if (in == IN_X8_LN && (G.ks > 2 || (G.nsb == 2 && G.J == 2))) return false;
+  // two super-blocks per lane at a 3-4 way K split (K > 16384): the plain image in (down), batch 1; at
+  // the 4-way split (1024 threads, <= 128 VGPRs) only the Q4_0 / Q4_K tiles fit without spilling
+  // (tests/test_isa.py)
+  if (G.nsb == 2 && G.ks > 2 &&
+      (in != IN_X8 || (em != EM_ADD && em != EM_NONE) || P.B > 1 || (G.ks == 4 && q != QT_Q4_0 && q != QT_Q4_K)))
+    return false;
   return lds8(P.w.K, G.ks, bt_of(P.B)) <= (P.B > 1 ? 160 : 64) * 1024;
 }
 
@@ -198,9 +209,20 @@ void launch_glu_nsb2(const GemvParams& P, const Geo& G, hipStream_t s) {
   else launch_k<QT, 2, 2, 1, IN_X8_RMS, 0, EM_GLU, 2>(P, G.grid, s);
 }
 
+// K > 16384 (Llama-2-70B ffn_down): two super-blocks per lane, K split in 3-4, IN_X8, batch 1
+template <int QT, int KS>
+void launch_wide(const GemvParams& P, const Geo& G, hipStream_t s) {
+  if constexpr (KS == 3 || QT == QT_Q4_0 || QT == QT_Q4_K) {
+    if (emit_mode(P) == EM_ADD) launch_k<QT, 2, 1, KS, IN_X8, 0, EM_ADD, 1>(P, G.grid, s);
+    else launch_k<QT, 2, 1, KS, IN_X8, 0, EM_NONE, 1>(P, G.grid, s);
+  }
+}
+
 template <int QT>
 void launch_q(const GemvParams& P, const Geo& G, hipStream_t s) {
-  if (G.ks == 1 && G.nsb == 2 && G.J == 2) launch_glu_nsb2<QT>(P, G, s);
+  if (G.nsb == 2 && G.ks == 3) launch_wide<QT, 3>(P, G, s);
+  else if (G.nsb == 2 && G.ks == 4) launch_wide<QT, 4>(P, G, s);
+  else if (G.ks == 1 && G.nsb == 2 && G.J == 2) launch_glu_nsb2<QT>(P, G, s);
   else if (G.ks == 1 && G.nsb == 1 && G.J == 1) launch_in<QT, 1, 1, 1>(P, G, s);
   else if (G.ks == 1 && G.nsb == 1) launch_in<QT, 1, 2, 1>(P, G, s);
   else if (G.ks == 1 && G.nsb == 2) launch_in<QT, 2, 1, 1>(P, G, s);
@@ -214,10 +236,10 @@ bool launchable(const GemvParams& P, const Geo& G) {
   return in_mode(P) != IN_MERGE || (G.ks <= 2 && G.nsb == 1 && G.J == 1);
 }
 
-template <int QA, int QB, int IN, int BT>
+template <int QA, int QB, int IN, int BT, int EMB = EM_NONE, int NSB = 1>
 void launch_dual_k(const GemvParams& A, const GemvParams& B, int gxa, int gxb, hipStream_t s) {
   const size_t lds = lds8(A.w.K, 1, BT);
-  auto k = qgemv8_dual_kernel<QA, QB, IN, BT>;
+  auto k = qgemv8_dual_kernel<QA, QB, IN, BT, EMB, NSB>;
   lds_attr(k, lds);
   hipLaunchKernelGGL(k, dim3(gxa + gxb), dim3(GEMV_NT), lds, s, A, B, gxa);
 }
@@ -234,7 +256,13 @@ void launch_dual_in(const GemvParams& A, const GemvParams& B, int gxa, int gxb, 
 
 template <int QA, int QB>
 void launch_dual(const GemvParams& A, const GemvParams& B, int gxa, int gxb, hipStream_t s) {
-  if (A.x8_stat) launch_dual_in<QA, QB, IN_X8_RMS>(A, B, gxa, gxb, s);
+  if ((A.w.K + 255) / 256 > 16) {  // two super-blocks per lane (gemv8_2: RMS image, <= 2 rows)
+    if (bt_of(A.B) == 1) launch_dual_k<QA, QB, IN_X8_RMS, 1, EM_NONE, 2>(A, B, gxa, gxb, s);
+    else launch_dual_k<QA, QB, IN_X8_RMS, 2, EM_NONE, 2>(A, B, gxa, gxb, s);
+    return;
+  }
+  if (A.x8_sum) launch_dual_k<QA, QB, IN_X8_LN, 1, EM_ACT>(A, B, gxa, gxb, s);  // Phi-2 QKV + FFN up
+  else if (A.x8_stat) launch_dual_in<QA, QB, IN_X8_RMS>(A, B, gxa, gxb, s);
   else launch_dual_in<QA, QB, IN_X8>(A, B, gxa, gxb, s);
 }
 
@@ -244,6 +272,7 @@ bool dual_b(const GemvParams& A, const GemvParams& B, int gxa, int gxb, hipStrea
     case QT_Q6_K: launch_dual<QA, QT_Q6_K>(A, B, gxa, gxb, s); return true;
     case QT_Q4_K: launch_dual<QA, QT_Q4_K>(A, B, gxa, gxb, s); return true;
     case QT_Q8_0: launch_dual<QA, QT_Q8_0>(A, B, gxa, gxb, s); return true;
+    case QT_Q4_0: launch_dual<QA, QT_Q4_0>(A, B, gxa, gxb, s); return true;
     default: return false;
   }
 }
@@ -271,9 +300,16 @@ bool gemv8(const GemvParams& P, hipStream_t s) {
 
 bool gemv8_2(const GemvParams& A, const GemvParams& B, hipStream_t s) {
   Geo GA, GB;
-  if (!A.x8 || !B.x8 || A.x8 != B.x8 || A.emit8 || B.emit8 || A.w.K != B.w.K || A.B != B.B) return false;
-  if (A.x8_sum || B.x8_sum) return false;  // LayerNorm'd images: single launches
-  if (!covered(A, GA) || !covered(B, GB) || GA.nsb != 1 || GA.ks != 1 || GB.nsb != 1 || GB.ks != 1) return false;
+  if (!A.x8 || !B.x8 || A.x8 != B.x8 || A.emit8 || A.w.K != B.w.K || A.B != B.B) return false;
+  // LayerNorm'd images (Phi-2): B is the FFN up emitting down's image; otherwise neither side emits
+  if (A.x8_sum != B.x8_sum || (A.x8_sum ? emit_mode(B) != EM_ACT : B.emit8 != nullptr)) return false;
+  if (!covered(A, GA) || !covered(B, GB)) return false;
+  const int need = ((A.w.K + 255) / 256 + 15) / 16;  // 16-super-block groups of K
+  if (need == 2) {  // 4096 < K <= 8192: both sides two super-blocks per lane, RMS image, <= 2 rows
+    if (in_mode(A) != IN_X8_RMS || A.B > 2) return false;
+  } else if (GA.nsb != 1 || GA.ks != 1 || GB.nsb != 1 || GB.ks != 1) {
+    return false;
+  }
   const int gxa = (A.w.N + 15) / 16, gxb = (B.w.N + 15) / 16;  // one tile per block on both sides
   count_launch(LC_GEMV8_DUAL);
   switch (A.w.qtype) {

@@ -156,7 +156,8 @@ __device__ __forceinline__ void gemv8_body(const GemvParams& P, const int bx) {
   constexpr bool PRE = BT == 1 || KS <= 2;
   EpiPre<J, BT> pre;
   epi_prefetch<EMIT, J, BT, PRE, IN>(P, tile0, rbase, s, pre);
-  u32x4 xw[BT][X8_NWI];
+  constexpr int NWI = x8_nwi(NSB, KS);
+  u32x4 xw[BT][NWI];
   f32x4 stv[BT][X8_NSTW];
   f32x4 sxv[IN == IN_X8_LN ? X8_NSTW : 1];  // IN_X8_LN: the per-group sums
   // groups per thread of the merge prologue: the block's NT = GEMV_NT * KS threads cover KS * 4096
@@ -174,7 +175,7 @@ __device__ __forceinline__ void gemv8_body(const GemvParams& P, const int bx) {
 #pragma unroll
     for (int b = 0; b < BT; ++b)
 #pragma unroll
-      for (int i = 0; i < X8_NWI; ++i)
+      for (int i = 0; i < NWI; ++i)
         xw[b][i] = ((const u32x4*)((const char*)P.x8 + min(b, blast) * img_b))[min(tid + NT * i, nwords - 1)];
     if constexpr (IN == IN_X8_RMS || IN == IN_X8_LN) {
       const int n4 = K / 64;  // f32x4 of partials (K / 16 floats)
@@ -228,7 +229,7 @@ __device__ __forceinline__ void gemv8_body(const GemvParams& P, const int bx) {
 #pragma unroll
     for (int b = 0; b < BT; ++b)
 #pragma unroll
-      for (int i = 0; i < X8_NWI; ++i) {
+      for (int i = 0; i < NWI; ++i) {
         const int wd = tid + NT * i;
         if (wd < nwords) {
           u32x4* dst = wd < XSP ? (u32x4*)lq + b * XSP + wd : (u32x4*)(lf + b * XSP) + (wd - XSP);

@@ -17,7 +17,10 @@ __device__ __forceinline__ int x8_slots_dev(int K) { return ((n_sb(K) * XPAD + 1
 constexpr int X8_MAX_B = 4;
 __device__ __forceinline__ int x8_stat_ld_dev(int K) { return ((K >> 4) + 3) & ~3; }
 
-constexpr int X8_NWI = 3;   // 16-byte image words per thread (K <= 16384 at 256 threads x KS)
+constexpr int X8_NWI = 3;   // 16-byte image words per thread (K <= 7424 per 256 threads of the K split)
+// two super-blocks per lane, unsplit K (4096 < K <= 8192: Llama-2-70B's QKV / gate_up / LM head at
+// K = 8192 need 13104 image bytes > 256 x 3 x 16): one word more
+constexpr int x8_nwi(int nsb, int ks) { return nsb == 2 && ks == 1 ? 4 : X8_NWI; }
 constexpr int X8_NSTW = 2;  // f32x4 RMS partials per lane (K <= 8192)
 
 // quantise the 16 staged values of group G into the consumer image (one lane)

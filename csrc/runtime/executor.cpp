@@ -234,7 +234,7 @@ void Executor::attn_block(int i, const StepInputs& in, hipStream_t s) {
     V.w = L.wv;
     V.row_offset = Eq + Ekv;
     gemv2(P, V, s);
-  } else {
+  } else if (!phi) {
     gemv(P, s);
   }
   if (phi) {  // parallel block: FFN up reads the same normed input, before O touches resid
@@ -255,7 +255,11 @@ void Executor::attn_block(int i, const StepInputs& in, hipStream_t s) {
       U.emit8 = ws.x8f;
       U.emit8_k = cfg.F;
     }
-    gemv(U, s);
+    // on the chain QKV and up share one launch over the same image (gemv8_2), else two
+    if (!(L.qkv_fused && P.x8 && U.x8 && gemv8_2(P, U, s))) {
+      if (L.qkv_fused) gemv(P, s);
+      gemv(U, s);
+    }
   }
   // --- attention over the paged cache
   AttnParams A{};
