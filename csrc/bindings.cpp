@@ -307,9 +307,12 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("set_gemm_lib_min_m", &set_gemm_lib_min_m, "prefill rows from which the hipBLASLt path runs (0 = off)");
   m.def("gemm_lib_min_m", &gemm_lib_min_m);
+  m.def("set_moe_lib_min_m", &set_moe_lib_min_m, "MoE prefill pairs from which experts run on hipBLASLt (0 = off)");
+  m.def("moe_lib_min_m", &moe_lib_min_m);
   m.def("set_dq_gemm", &set_dq_gemm, "1: prefill GEMMs from 128 rows on the stream-order dequant kernel (gemm_dq.hip)");
   m.def("set_dq_tuning", &set_dq_tuning, "microbenchmarks: force the dq GEMM tile config (0..3, -1 auto) and split-K factor (0 auto)");
   m.def("dq_gemm_enabled", &dq_gemm_enabled);
+  m.def("set_gemv8_geo", [](int nsb, int ks) { set_gemv8_geo(nsb, ks); });
   m.def("set_dq_ring", &set_dq_ring, "1: prefill dq GEMMs on the register-ring kernel, 0: the glds kernel");
   // launch counters (ops.h LC_*): tests assert which kernel family a call enqueued
   m.def("launch_counts", []() {

@@ -490,14 +490,14 @@ void moe_gemm(const GemvParams& P, hipStream_t s) {
 }
 
 bool moe_gemm_lib(const GemvParams& P, const int* counts, int X, hipStream_t s) {
-  const int lm = gemm_lib_min_m();
+  const int lm = moe_lib_min_m();
   const long long N = P.w.N, K = P.w.K;  // per-expert rows
   int maxc = 0, total = 0;
   for (int e = 0; e < X; ++e) {
     maxc = counts[e] > maxc ? counts[e] : maxc;
     total += counts[e];
   }
-  if (lm <= 0 || total != P.B || !P.w16ws || !P.yws || N * K > P.w16_elems || (long long)maxc * N > P.yws_elems)
+  if (lm <= 0 || P.B < lm || total != P.B || !P.w16ws || !P.yws || N * K > P.w16_elems || (long long)maxc * N > P.yws_elems)
     return false;
   const size_t wsb = P.gws ? (size_t)P.gws_elems * 4 : 0;
   const long long xrows = P.xws_elems ? P.xws_elems / K : P.B, yrows = P.yws_elems / N;
@@ -564,6 +564,19 @@ static bool lib_glu() {
 }
 
 void set_gemm_lib_min_m(int m) { g_lib_min_m = m; }
+
+// MoE prefill (default 256 pairs = 128 tokens at top-2): the per-expert GEMMs are plain dense GEMMs over
+// contiguous sorted rows, and the grouped tile kernel (moe_gemm) they replace has no register-ring
+// edition -- Mixtral's 2048-token TTFT is 196 ms on it vs 116 ms per expert on hipBLASLt (profiles/r6_models)
+static int g_moe_lib_min_m = -1;
+int moe_lib_min_m() {
+  if (g_moe_lib_min_m < 0) {
+    const char* e = getenv("OMX_MOE_LIB_MIN_M");
+    g_moe_lib_min_m = e ? atoi(e) : 256;
+  }
+  return g_moe_lib_min_m;
+}
+void set_moe_lib_min_m(int m) { g_moe_lib_min_m = m; }
 
 static bool gemm_lib(const GemvParams& P, const f16* x16, hipStream_t s) {
   const int lm = lib_min_for(P.w);

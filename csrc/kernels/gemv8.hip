@@ -82,12 +82,28 @@ struct Geo {
   int nsb = 0, ks = 0, J = 0, grid = 0;
 };
 
+// microbenchmarks only (scripts/bench_gemv8.py OMX_BENCH_GEO): force (NSB, KS) of the K-split plain-image
+// launches (down) where that geometry covers K; 0 = the rule below
+static int g_geo_nsb = 0, g_geo_ks = 0;
+
 bool geometry(const GemvParams& P, Geo& G) {
   const int SB = (P.w.K + 255) / 256, need = (SB + 15) / 16;
   const int tiles = (P.w.N + 15) / 16;
+  if (g_geo_nsb > 0 && g_geo_ks > 1 && need > 2 && P.x8 && !P.x8_stat && g_geo_nsb * g_geo_ks >= need) {
+    G.nsb = g_geo_nsb;
+    G.ks = g_geo_ks;
+    G.J = 1;
+    G.grid = tiles;
+    return true;
+  }
   if (need == 1) { G.nsb = 1; G.ks = 1; }
   else if (need == 2) { G.nsb = tiles > 512 ? 2 : 1; G.ks = tiles > 512 ? 1 : 2; }
-  else if (need <= 4) { G.nsb = 1; G.ks = need; }
+  else if (need == 4 && P.w.qtype == QT_Q4_K && P.x8 && !P.x8_stat && P.B == 1) {
+    // Llama-2-13B's Q4_K ffn_down (K = 13824, 54 SBs): 2 super-blocks per lane over a 2-way split, 14.4
+    // vs 16.7 us at 4 x 1 (the Q6_K rows and the 3-way 7B shapes measured slower: profiles/r6_gemv8/geo.log)
+    G.nsb = 2;
+    G.ks = 2;
+  } else if (need <= 4) { G.nsb = 1; G.ks = need; }
   else if (need <= 8) { G.nsb = 2; G.ks = (need + 1) / 2; }  // Llama-2-70B ffn_down (K = 28672): 4 x 32 SBs
   else return false;
   if (G.ks > 1) {
@@ -140,7 +156,7 @@ bool covered(const GemvParams& P, Geo& G) {
   // two super-blocks per lane at a 3-4 way K split (K > 16384): the plain image in (down), batch 1; at
   // the 4-way split (1024 threads, <= 128 VGPRs) only the Q4_0 / Q4_K tiles fit without spilling
   // (tests/test_isa.py)
-  if (G.nsb == 2 && G.ks > 2 &&
+  if (G.nsb == 2 && G.ks > 1 &&
       (in != IN_X8 || (em != EM_ADD && em != EM_NONE) || P.B > 1 || (G.ks == 4 && q != QT_Q4_0 && q != QT_Q4_K)))
     return false;
   return lds8(P.w.K, G.ks, bt_of(P.B)) <= (P.B > 1 ? 160 : 64) * 1024;
@@ -212,7 +228,7 @@ void launch_glu_nsb2(const GemvParams& P, const Geo& G, hipStream_t s) {
 // K > 16384 (Llama-2-70B ffn_down): two super-blocks per lane, K split in 3-4, IN_X8, batch 1
 template <int QT, int KS>
 void launch_wide(const GemvParams& P, const Geo& G, hipStream_t s) {
-  if constexpr (KS == 3 || QT == QT_Q4_0 || QT == QT_Q4_K) {
+  if constexpr (KS <= 3 || QT == QT_Q4_0 || QT == QT_Q4_K) {
     if (emit_mode(P) == EM_ADD) launch_k<QT, 2, 1, KS, IN_X8, 0, EM_ADD, 1>(P, G.grid, s);
     else launch_k<QT, 2, 1, KS, IN_X8, 0, EM_NONE, 1>(P, G.grid, s);
   }
@@ -220,7 +236,8 @@ void launch_wide(const GemvParams& P, const Geo& G, hipStream_t s) {
 
 template <int QT>
 void launch_q(const GemvParams& P, const Geo& G, hipStream_t s) {
-  if (G.nsb == 2 && G.ks == 3) launch_wide<QT, 3>(P, G, s);
+  if (G.nsb == 2 && G.ks == 2) launch_wide<QT, 2>(P, G, s);
+  else if (G.nsb == 2 && G.ks == 3) launch_wide<QT, 3>(P, G, s);
   else if (G.nsb == 2 && G.ks == 4) launch_wide<QT, 4>(P, G, s);
   else if (G.ks == 1 && G.nsb == 2 && G.J == 2) launch_glu_nsb2<QT>(P, G, s);
   else if (G.ks == 1 && G.nsb == 1 && G.J == 1) launch_in<QT, 1, 1, 1>(P, G, s);
@@ -278,6 +295,11 @@ bool dual_b(const GemvParams& A, const GemvParams& B, int gxa, int gxb, hipStrea
 }
 
 }  // namespace
+
+void set_gemv8_geo(int nsb, int ks) {
+  g_geo_nsb = nsb;
+  g_geo_ks = ks;
+}
 
 bool gemv8_supported(const GemvParams& P) {
   Geo G;

@@ -132,6 +132,7 @@ inline int x8_stat_ld(int K) { return ((K >> 4) + 3) & ~3; }  // RMS-partial flo
 bool gemv8(const GemvParams& P, hipStream_t s);
 bool gemv8_2(const GemvParams& A, const GemvParams& B, hipStream_t s);  // q,k + v rows, one launch
 bool gemv8_supported(const GemvParams& P);
+void set_gemv8_geo(int nsb, int ks);  // microbenchmarks: force (NSB, KS) of K-split plain-image launches
 struct AttnParams;
 
 // y = epi(W x): the quantised GEMV for small B (decode), the MFMA dequant GEMM for B >= GEMM_MIN_B
@@ -144,6 +145,10 @@ constexpr int GEMM_MIN_B = 16;
 // prefill rows from which the library GEMM path is taken (0 = never); OMX_GEMM_LIB_MIN_M overrides
 void set_gemm_lib_min_m(int m);
 int gemm_lib_min_m();
+// MoE prefill: routed (token, expert) pairs from which each expert's GEMM runs on hipBLASLt over its
+// dequantised weights (gemm.hip moe_gemm_lib; 0 = never, the grouped tile GEMM). OMX_MOE_LIB_MIN_M
+void set_moe_lib_min_m(int m);
+int moe_lib_min_m();
 // D[M][N] (fp32, row-major) = X[M][K] . W[N][K]^T, X and W fp16 row-major, on hipBLASLt; false when
 // no algorithm fits (the caller falls back)
 // m_cap: rows of x16 / d the buffers hold (>= M); when the M-bucket's algorithm does not accept M

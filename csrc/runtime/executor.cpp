@@ -391,8 +391,8 @@ void Executor::ffn_block(int i, const StepInputs& in, hipStream_t s) {
       std::vector<int> counts;
       hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
       (void)hipStreamIsCapturing(s, &cap);
-      const int lm = gemm_lib_min_m();
-      if (lm > 0 && B >= lm && ws.w16 && ws.yws && cap == hipStreamCaptureStatusNone) {
+      const int lm = moe_lib_min_m();
+      if (lm > 0 && pairs >= lm && ws.w16 && ws.yws && cap == hipStreamCaptureStatusNone) {
         std::vector<int> e_host(pairs);
         if (hipMemcpyAsync(e_host.data(), ws.eids, sizeof(int) * pairs, hipMemcpyDeviceToHost, s) == hipSuccess &&
             hipStreamSynchronize(s) == hipSuccess) {

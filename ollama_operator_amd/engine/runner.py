@@ -169,6 +169,9 @@ class Runner:
         # prefill GEMM runs the hand-written dequant kernel over the resident quantised weights, and no fp16
         # weight copy exists -- OMX_GEMM_LIB_MIN_M=<rows> is the A/B knob)
         self.lib_min = native().gemm_lib_min_m() if self.is_gpu else 0
+        # MoE prefill: (token, expert) pairs from which each expert's GEMM runs on hipBLASLt over its
+        # per-call dequantised weights (gemm.hip moe_gemm_lib; default 256, OMX_MOE_LIB_MIN_M)
+        self.moe_lib = native().moe_lib_min_m() if self.is_gpu and self.w.cfg.n_expert else 0
         cfg = self.cfg = self.w.cfg
         loc = self.w.local
         self.max_batch = max_batch
@@ -243,12 +246,15 @@ class Runner:
         # OMX_GEMM_LIB_MIN_M, 0 = never): fp16 dequantised-weight scratch sized for the largest dense
         # layer matrix and its fp32 output slab at max_batch rows
         self.w16 = self.yws = None
-        if self.is_gpu and self.lib_min > 0 and max_batch >= max(16, self.lib_min):
+        dense_lib = self.lib_min > 0 and max_batch >= max(16, self.lib_min)
+        moe_lib = self.moe_lib > 0 and max_batch * ksel >= self.moe_lib
+        if self.is_gpu and (dense_lib or moe_lib):
             # expert stacks count per expert (DevQMat.N = rows of one expert): moe_gemm_lib
-            mats = [v for L in self.w.layers for k, v in L.items() if isinstance(v, DevQMat) and k != "router"]
+            mats = [v for L in self.w.layers for k, v in L.items() if isinstance(v, DevQMat) and k != "router"
+                    and (dense_lib or k in ("gu_exps", "down_exps"))]
             if mats:
                 self.w16 = torch.empty(max(m.N * m.K for m in mats), device=dev, dtype=torch.float16)
-                self.yws = torch.empty(max_batch * max(m.N for m in mats), **f32)
+                self.yws = torch.empty(max_batch * (ksel if moe_lib else 1) * max(m.N for m in mats), **f32)
         ws = max(self._ws_floats(B) for B in range(1, max_batch + 1))
         self.attn_ws = torch.zeros(max(ws, 1), **f32)
         self.attn_cnt = torch.zeros(max_batch * loc["H"], **i32)  # self re-arming tickets
@@ -641,9 +647,9 @@ class Runner:
         if self.w16 is not None:  # hipBLASLt plans for the long-prefill path (gemm.hip gemm_lib)
             C = native()
             lm = self.lib_min
-            if lm > 0 and self.max_batch >= lm:
+            if (lm > 0 and self.max_batch >= lm) or self.moe_lib > 0:
                 shapes = {(v.N, v.K) for L in self.w.layers for k, v in L.items()
-                          if isinstance(v, DevQMat) and k != "router"}
+                          if isinstance(v, DevQMat) and k != "router" and (lm > 0 or k in ("gu_exps", "down_exps"))}
                 for N, K in sorted(shapes):
                     if N * K <= self.w16.numel():  # from 128: MoE experts see any row count
                         C.gemm_lib_prepare(N, K, 128, self.max_batch, self.gws.numel() * 4)

@@ -29,6 +29,15 @@ SHAPES = [
     ("down_q6k", GGMLType.Q6_K, 4096, 11008, EPI_ADD, False, True),
     ("lm_head", GGMLType.Q6_K, 32000, 4096, EPI_STORE, True, False),
 ]
+# OMX_BENCH_BIG=1: the K-split down projections of Llama-2-13B (54 super-blocks) and 70B (112), and 7B's
+# padded K (44); OMX_BENCH_GEO=nsb,ks forces the launch geometry of those (gemv8.hip set_gemv8_geo)
+BIG = [
+    ("down7_q4k", GGMLType.Q4_K, 4096, 11264, EPI_ADD, False, True),
+    ("down7_q6k", GGMLType.Q6_K, 4096, 11264, EPI_ADD, False, True),
+    ("down13_q4k", GGMLType.Q4_K, 5120, 13824, EPI_ADD, False, True),
+    ("down13_q6k", GGMLType.Q6_K, 5120, 13824, EPI_ADD, False, True),
+    ("down70_q40", GGMLType.Q4_0, 8192, 28672, EPI_ADD, False, True),
+]
 # OMX_BENCH_ALIGN=1: down-shaped probes at K = 12288 (48 super-blocks: each K group of the 3-way split
 # gets exactly 16, piece segments 128-B aligned) vs the real K = 11008 (43: 15 + 15 + 13, 688-B strides)
 ALIGN = [
@@ -74,7 +83,11 @@ def main():
         big.add_(1)
     torch.cuda.synchronize()
     del big
-    for name, qt, N, K, epi, rms, emits in SHAPES + (ALIGN if os.environ.get("OMX_BENCH_ALIGN") else []):
+    if os.environ.get("OMX_BENCH_GEO"):
+        C.set_gemv8_geo(*[int(v) for v in os.environ["OMX_BENCH_GEO"].split(",")])
+    shapes = SHAPES + (ALIGN if os.environ.get("OMX_BENCH_ALIGN") else []) + \
+        (BIG if os.environ.get("OMX_BENCH_BIG") else [])
+    for name, qt, N, K, epi, rms, emits in shapes:
         if only and name not in only:
             continue
         tups, keep, nbytes = make(qt, N, K, hot)
@@ -120,7 +133,8 @@ def main():
             torch.cuda.synchronize()
             ts.append(e0.elapsed_time(e1) * 1e3 / n_launch)
         t = float(np.median(ts))
-        tag = ("hot " if hot else "cold") + (" mem-only" if ops["dbg8"] else "") + \
+        geo = os.environ.get("OMX_BENCH_GEO")
+        tag = ("hot " if hot else "cold") + (f" geo {geo}" if geo else "") + (" mem-only" if ops["dbg8"] else "") + \
             (" no-emit" if emits and os.environ.get("OMX_BENCH_NOEMIT") else "")
         print(f"{name:9s} {tag} {t:7.2f} us/launch  {nbytes / t / 1e3:7.1f} GB/s  "
               f"({len(tups)} copies, {nbytes / 1e6:.1f} MB)", flush=True)

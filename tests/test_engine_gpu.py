@@ -103,6 +103,30 @@ def test_prefill_dq_path_vs_torch(tiny_models, name, monkeypatch):
     assert rel(g.logits[0, :V].cpu(), c.logits[0, :V]) < 3e-2
 
 
+def test_moe_prefill_experts_on_library_by_default(tiny_models):
+    """MoE prefill: from moe_lib_min_m() routed pairs (default 256) each expert's GEMM runs on hipBLASLt
+    over its per-call dequantised weights (gemm.hip moe_gemm_lib) while every dense projection stays on
+    the hand-written kernel (gemm_lib_min_m() == 0): the expert scratch is used and logits match."""
+    C = native()
+    assert C.gemm_lib_min_m() == 0 and C.moe_lib_min_m() > 0
+    path = tiny_models["tiny-mixtral"]
+    g = Runner(path, device="cuda", max_batch=256, max_seqs=2, ctx=256)
+    c = Runner(path, device="cpu", max_batch=256, max_seqs=2, ctx=256)
+    assert g.w16 is not None
+    g.w16.fill_(float("nan"))
+    rng = np.random.default_rng(8)
+    toks = [1] + [int(x) for x in rng.integers(3, 500, 199)]  # 400 pairs at top-2
+    sg, sc = g.new_sequence(), c.new_sequence()
+    C.reset_launch_counts()
+    g.prefill(sg, toks)
+    torch.cuda.synchronize()
+    n = C.launch_counts()
+    assert not torch.isnan(g.w16).all() and n["gemm_lib"] == 0 and n["dq_gemm"] >= 2 * g.cfg.n_layer, n
+    c.prefill(sc, toks)
+    V = g.cfg.n_vocab
+    assert rel(g.logits[0, :V].cpu(), c.logits[0, :V]) < 3e-2
+
+
 @pytest.mark.parametrize("name", ["tiny-llama", "tiny-mixtral", "tiny-gemma", "tiny-phi2"])
 def test_prefill_library_path_vs_torch(tiny_models, name, monkeypatch):
     """The hipBLASLt prefill path (gemm.hip gemm_lib; for Mixtral per-expert GEMMs over the sorted
