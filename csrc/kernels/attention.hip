@@ -480,7 +480,12 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(AttnParams P) {
   __shared__ __attribute__((aligned(16))) char Vs[PF_BK * VROW];  // [key][VROW B] swizzled, zero-padded
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h2 = lane >> 5, qc = lane & 31;
   const int head = blockIdx.y, G = P.H / P.n_kv, kvh = head / G;
-  const int q0 = blockIdx.x * PF_BQ;
+  // causal load balance: block b and b + 256 share a CU in the first dispatch wave (2 blocks per CU), and
+  // consecutive heads hold the same query-block index, so the CUs that drew the last query blocks got twice
+  // the heaviest work. The upper half of the heads walks the query blocks in reverse: every CU pairs a
+  // heavy block with a light one.
+  const int qb = blockIdx.y >= gridDim.y / 2 ? (int)(gridDim.x - 1 - blockIdx.x) : (int)blockIdx.x;
+  const int q0 = qb * PF_BQ;
   const int NQ = P.NQ;
   const int qi = min(q0 + wave * 32 + qc, NQ - 1);  // this lane's query (clamped; stores masked)
   const int len_q = P.q_len[qi];                    // visible keys = pos + 1
@@ -496,8 +501,10 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(AttnParams P) {
   const int len_max = P.q_len[q_last];
   const int k_lo = P.window > 0 ? max(0, P.q_len[q0] - P.window) / PF_BK * PF_BK : 0;
 
-  // Q^T fragments (B operand of S^T): lane = query, 8 consecutive d per k-step, scaled
+  // Q^T fragments (B operand of S^T): lane = query, 8 consecutive d per k-step, scaled by scale * log2(e):
+  // the scores come out in the log2 domain, so the softmax takes v_exp_f32 directly (no multiply per score)
   f16x8 qf[NKS];
+  const float qs = P.scale * 1.44269504f;
   const int Dv = P.Dv > 0 ? P.Dv : D;  // valid dims (multiple of 4): q / output head stride
   {
     const float* qp = P.q + (long long)qi * P.ldq + head * Dv;
@@ -507,8 +514,8 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(AttnParams P) {
       const int d0 = 16 * kk + 8 * h2;  // padded dims load nothing (next head's q / past the row)
       const f32x4 a = d0 + 4 <= Dv ? *(const f32x4*)(qp + min(d0, Dv - 4)) : z4;
       const f32x4 b = d0 + 8 <= Dv ? *(const f32x4*)(qp + min(d0 + 4, Dv - 4)) : z4;
-      qf[kk] = (f16x8){(f16)(a.x * P.scale), (f16)(a.y * P.scale), (f16)(a.z * P.scale), (f16)(a.w * P.scale),
-                       (f16)(b.x * P.scale), (f16)(b.y * P.scale), (f16)(b.z * P.scale), (f16)(b.w * P.scale)};
+      qf[kk] = (f16x8){(f16)(a.x * qs), (f16)(a.y * qs), (f16)(a.z * qs), (f16)(a.w * qs),
+                       (f16)(b.x * qs), (f16)(b.y * qs), (f16)(b.z * qs), (f16)(b.w * qs)};
     }
   }
   f32x16a o[NDT];
@@ -578,31 +585,41 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(AttnParams P) {
       const f16x8 kf = *(const f16x8*)(Ks + qc * LDK + 16 * kk + 8 * h2);
       sacc = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf, qf[kk], sacc, 0, 0, 0);
     }
-    // causal / window / length mask + online softmax (per lane = per query; halves exchange)
+    // causal / window / length mask + online softmax (per lane = per query; halves exchange). The VALU
+    // work per tile is what bounds this kernel (~200 ops per lane vs 16 MFMAs per wave): tiles wholly
+    // inside every query's window of this wave skip the mask, and the accumulator rescale is skipped
+    // when no query's running max moved
     float tmax = -INFINITY;
+    if (__all(kt0 + PF_BK <= len_q && kt0 >= kstart_q)) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int t = kt0 + (r & 3) + 8 * (r >> 2) + 4 * h2;
-      const bool ok = t < len_q && t >= kstart_q;
-      sacc[r] = ok ? sacc[r] : -INFINITY;
-      tmax = fmaxf(tmax, sacc[r]);
+      for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, sacc[r]);
+    } else {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int t = kt0 + (r & 3) + 8 * (r >> 2) + 4 * h2;
+        const bool ok = t < len_q && t >= kstart_q;
+        sacc[r] = ok ? sacc[r] : -INFINITY;
+        tmax = fmaxf(tmax, sacc[r]);
+      }
     }
     tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
     const float mn = fmaxf(m, tmax);
-    const float corr = mn == -INFINITY ? 1.f : __expf(m - mn);
+    const float corr = mn == -INFINITY ? 1.f : __builtin_amdgcn_exp2f(m - mn);
     float ps = 0.f;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      sacc[r] = mn == -INFINITY ? 0.f : __expf(sacc[r] - mn);
+      sacc[r] = mn == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(sacc[r] - mn);
       ps += sacc[r];
     }
     ps += __shfl_xor(ps, 32, 64);
     l = l * corr + ps;
     m = mn;
+    if (__any(corr != 1.f)) {
 #pragma unroll
-    for (int i = 0; i < NDT; ++i)
+      for (int i = 0; i < NDT; ++i)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) o[i][r] *= corr;
+        for (int r = 0; r < 16; ++r) o[i][r] *= corr;
+    }
     // O^T += V^T . P^T : two k-steps of 16 keys; P^T fragment s = registers 8s..8s+7
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {

@@ -293,6 +293,9 @@ class Runner:
         # ~13 us boundary between two replays disappears inside a group, but the larger graph ran with
         # more idle time between its kernels)
         self.decode_group = max(1, int(os.environ.get("OMX_DECODE_GROUP", "1")))
+        # OMX_GRAPH_PAIR=1 (A/B knob): batch-1 decode alternates between two captured instances of each
+        # step graph, so a replay never re-launches the executable the previous replay is still running
+        self.graph_pair = os.environ.get("OMX_GRAPH_PAIR", "0") == "1"
         self.steps_issued = 0  # decode steps enqueued so far (batched steps count once): bench timing
         # past 8 x defer_kps keys, up to 8 x 512: 8 deferred splits of ceil(len / 8) keys (OMX_DEFER_LONG=1,
         # default: attention 14.4 -> 11.6 us at 2k keys, the O prologue's 8-slab merge 4.9 -> 7.1 us, net
@@ -609,10 +612,11 @@ class Runner:
         if not self.is_gpu:
             self.d_tokens[:B].copy_(self.s_out[:B])
 
-    def _graph(self, B: int, steps: int = 1):
+    def _graph(self, B: int, steps: int = 1, inst: int = 0):
         """The decode graph of `steps` consecutive steps for B rows (one replay = `steps` tokens per row:
-        the feedback kernel advances every row on device between them, so no host work sits in between)."""
-        key = (B, self._decode_S, steps)
+        the feedback kernel advances every row on device between them, so no host work sits in between).
+        inst: which of the two instances (graph_pair)."""
+        key = (B, self._decode_S, steps, inst)
         g = self.graphs.get(key)
         if g is None:
             s = torch.cuda.Stream()
@@ -723,7 +727,7 @@ class Runner:
         self._decode_S = self.decode_splits(pos + k)
         try:
             with trace_range(f"decode x{k}"):
-                self._graph(1, k).replay()
+                self._graph(1, k, self.steps_issued & 1 if self.graph_pair else 0).replay()
             self._adv_next = (sid, pos + k)
             self.steps_issued += k
         finally:
@@ -760,7 +764,7 @@ class Runner:
         try:
             with trace_range(f"decode B={B}"):
                 if self.use_graphs:
-                    self._graph(B).replay()
+                    self._graph(B, 1, self.steps_issued & 1 if self.graph_pair and B == 1 else 0).replay()
                 else:
                     self._decode_body(B)
             if self.is_gpu:
