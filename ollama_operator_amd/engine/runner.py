@@ -303,6 +303,11 @@ class Runner:
         # in-launch ticket merge (0; always past 4096 keys)
         self.defer_long = os.environ.get("OMX_DEFER_LONG", "1") != "0"
         self.defer_max_s = int(os.environ.get("OMX_DEFER_MAX_S", "8"))  # 2, 4 or 8 deferred splits at most
+        # past 8 x defer_kps keys and up to this length: 4 deferred splits instead of 8 (default 0 = never).
+        # The chain probe (profiles/r6_attn/attn_probe*.log) timed S = 4 1.1 us per layer ahead at 2048
+        # keys, but in the model it measured equal at 2.2k keys and 3 % behind at 2.6-2.9k
+        # (experiments/ab/defer_s4.py, profiles/r6_attn/defer_s4_ab.log)
+        self.defer_s4_max = int(os.environ.get("OMX_DEFER_S4_MAX", "0"))
         self._defer_ok = (self.is_gpu and os.environ.get("OMX_DEFER_MERGE", "1") != "0" and
                           native().gemv_merge_supported(1, Eq, loc["D"], 8) and self.n_splits(1) >= 8)
         self._decode_S = 0
@@ -405,6 +410,8 @@ class Runner:
         S = 1
         while S < self.defer_max_s and length > S * self.defer_kps:
             S *= 2
+        if S == 8 and self.defer_long and 8 * self.defer_kps < length <= self.defer_s4_max:
+            S = 4
         return S if length <= S * self.defer_kps or (self.defer_long and length <= 8 * 512) else 0
 
     def _ws_floats(self, B: int) -> int:

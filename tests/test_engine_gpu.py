@@ -195,6 +195,21 @@ def test_deferred_split_merge_decode(tmp_path, monkeypatch, name):
         assert rel(outs[0], outs[1]) < 2e-3, L
         assert rel(outs[0], outs[2]) < 3e-2, L
     assert seen == {1, 2, 4, 8}  # 1050 keys: 8 deferred splits of 132 (OMX_DEFER_LONG, default on)
+    monkeypatch.setenv("OMX_DEFER_S4_MAX", "3072")
+    monkeypatch.delenv("OMX_DEFER_MERGE")
+    g4 = Runner(path, device="cuda", max_batch=64, max_seqs=1, ctx=1100, weights=g.w)
+    # the opt-in 4-split bucket: up to 768 keys per split between 1024 and 3072 keys, 8 splits beyond
+    assert [g4.decode_splits(n) for n in (1000, 1050, 2049, 3072, 3073, 4096)] == [8, 4, 4, 4, 8, 8]
+    sid = g4.new_sequence()
+    toks = [1] + [int(x) for x in rng.integers(3, 500, 1049)]
+    g4.prefill(sid, toks)
+    g4.d_tokens[0] = 77
+    g4.decode_step(sid, 1050)
+    torch.cuda.synchronize()
+    out4 = g4.logits[0, :V].float().cpu().clone()
+    sc = c.new_sequence()
+    c.prefill(sc, toks + [77])
+    assert rel(out4, c.logits[0, :V]) < 3e-2
 
 
 @pytest.mark.parametrize("name", ["tiny-llama", "tiny-mixtral", "tiny-phi2", "tiny-gemma"])
