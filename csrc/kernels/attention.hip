@@ -83,8 +83,25 @@ __device__ __forceinline__ void load_krow(const f16* p, KRow<DPL>& r) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) r.v[j] = t[j];
   } else if constexpr (DPL % 2 == 0) {
+    // head dims 80 / 96 / 112 at 8 lanes per key (DPL 10 / 12 / 14): the lane's run is only 4-B aligned,
+    // so whole 16-B / 8-B pieces go through 4-B-aligned vector copies (dwordx4 / dwordx2 loads on gfx950's
+    // unaligned-access mode) instead of one 4-B load per pair
+    constexpr int J8 = DPL / 8 * 8, J4 = J8 + (DPL - J8) / 4 * 4;
 #pragma unroll
-    for (int j = 0; j < DPL; j += 2) {
+    for (int j = 0; j < J8; j += 8) {
+      f16x8 t;
+      __builtin_memcpy(&t, __builtin_assume_aligned(p + j, 4), 16);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) r.v[j + i] = t[i];
+    }
+    if constexpr (J4 > J8) {
+      f16x4 t;
+      __builtin_memcpy(&t, __builtin_assume_aligned(p + J8, 4), 8);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) r.v[J8 + i] = t[i];
+    }
+#pragma unroll
+    for (int j = J4; j < DPL; j += 2) {
       const f16x2 t = *(const f16x2*)(p + j);
       r.v[j] = t[0];
       r.v[j + 1] = t[1];
@@ -679,7 +696,9 @@ template <int D, bool KV8>
 static void launch_dk(const AttnParams& P, hipStream_t s) {
   const int G = heads_per_block(P);
   dim3 grid(P.NQ, P.H / G, P.n_splits);
-  constexpr int LPK8 = KV8 && D == 128 ? 8 : 16;  // fp8 rows at D = 128: 8 lanes x 16 B per key
+  // 8 lanes per key: fp8 rows at D = 128 (8 lanes x 16 B), and fp16 rows of head dims 80 / 96 / 112 (20-28 B
+  // per lane in 2-3 vector loads; at 16 lanes a lane's 10-14 B are 2-B aligned: one load per element)
+  constexpr int LPK8 = (KV8 && D == 128) || (!KV8 && (D == 80 || D == 96 || D == 112)) ? 8 : 16;
   switch (G) {
     case 1: hipLaunchKernelGGL((attn_decode_kernel<D, 1, KV8, LPK8>), grid, dim3(ATT_NT), 0, s, P); break;
     case 2: hipLaunchKernelGGL((attn_decode_kernel<D, 2, KV8, LPK8>), grid, dim3(ATT_NT), 0, s, P); break;

@@ -160,7 +160,7 @@ def test_gemv_qkv_rope_kv_scatter(D, n_rot):
         assert rel(vc[blk, :, off].float(), vr[b]) < 1.2e-2
 
 
-@pytest.mark.parametrize("D", [64, 80, 128])
+@pytest.mark.parametrize("D", [64, 80, 96, 112, 128])
 @pytest.mark.parametrize("G,hpb", [(1, 0), (2, 0), (4, 0), (4, 1), (4, 4), (8, 0), (8, 1), (8, 2), (8, 8), (3, 0)])
 @pytest.mark.parametrize("splits", [1, 5])
 def test_attention_paged(D, G, hpb, splits):
