@@ -244,6 +244,8 @@ PYBIND11_MODULE(_C, m) {
     P.emit8_nw = Pp<const float>(ip("emit8_nw"));
     P.emit8_stat = Pp<float>(ip("emit8_stat"));
     P.dbg8 = ii("dbg8");
+    P.kb_ws = Pp<float>(ip("kb_ws"));
+    P.kb_cnt = Pp<int>(ip("kb_cnt"));
     if (qkv.contains("merge_S")) {
       P.merge_S = ii("merge_S");
       P.merge_ml = Pp<const float>(ip("merge_ml"));
@@ -313,11 +315,12 @@ PYBIND11_MODULE(_C, m) {
   m.def("set_dq_tuning", &set_dq_tuning, "microbenchmarks: force the dq GEMM tile config (0..3, -1 auto) and split-K factor (0 auto)");
   m.def("dq_gemm_enabled", &dq_gemm_enabled);
   m.def("set_gemv8_geo", [](int nsb, int ks) { set_gemv8_geo(nsb, ks); });
+  m.def("set_gemv8_kb", [](int mode) { set_gemv8_kb(mode); });
   m.def("set_dq_ring", &set_dq_ring, "1: prefill dq GEMMs on the register-ring kernel, 0: the glds kernel");
   // launch counters (ops.h LC_*): tests assert which kernel family a call enqueued
   m.def("launch_counts", []() {
     static const char* names[LC_N] = {"dq_gemm", "gemm_tile", "gemm_lib", "gemv8_row1", "gemv8_rows", "gemv8_dual",
-                                      "gemv_mb", "gemv_flight", "attn_decode", "attn_prefill"};
+                                      "gemv_mb", "gemv_flight", "attn_decode", "attn_prefill", "gemv8_pair"};
     py::dict d;
     for (int i = 0; i < LC_N; ++i) d[names[i]] = launch_count(i);
     return d;
@@ -539,6 +542,8 @@ PYBIND11_MODULE(_C, m) {
         w.x8f = Pp<void>(ptr("x8f"));
         w.x8st = Pp<float>(ptr("x8st"));
         w.x8sum = Pp<float>(ptr("x8sum"));
+        w.kb_ws = Pp<float>(ptr("x8kb"));
+        w.kb_cnt = Pp<int>(ptr("x8cnt"));
         w.x8_ok = (d.contains("x8_ok") ? d["x8_ok"].cast<int>() : 0) && e.x8_capable() ? 1 : 0;
         {  // continuous-batching rows on the chain: as many as asked for and every emitter covers
           const int want = d.contains("x8_bmax") ? d["x8_bmax"].cast<int>() : 1;

@@ -296,6 +296,35 @@ bool dual_b(const GemvParams& A, const GemvParams& B, int gxa, int gxb, hipStrea
 
 }  // namespace
 
+// K split across blocks (GemvParams::kb): -1 = OMX_GEMV8_KB, read once (0 / unset = auto, 1 = off, 2 = on
+// wherever covered)
+static int g_kb = -1;
+
+static int kb_mode() {
+  if (g_kb < 0) {
+    const char* e = getenv("OMX_GEMV8_KB");
+    g_kb = e ? atoi(e) : 0;
+  }
+  return g_kb;
+}
+
+// two blocks per row tile for a batch-1 K-split launch; each block streams half of K over 2 in-block
+// groups and the tile's last block sums the halves (profiles/r6_gemv8/kb.log). Measured: Phi-2's ffn_down
+// (160 tiles) 6.96 -> 9.63 us, the 7B shapes slower too -- the ticket hand-off costs more than the extra
+// blocks win -- and only Llama-2-13B's Q6_K ffn_down (54 super-blocks) faster, 24.3 -> 22.0 us: the auto
+// rule takes that shape alone
+static int choose_kb(const GemvParams& P, const Geo& G) {
+  const int mode = kb_mode();
+  if (mode == 1 || !P.kb_ws || !P.kb_cnt || P.B != 1 || G.J != 1 || G.ks < 2 || G.nsb != 1) return 1;
+  const int in = in_mode(P), em = emit_mode(P);
+  if ((in != IN_X8 && in != IN_X8_RMS) || (em != EM_ADD && em != EM_NONE)) return 1;
+  if ((size_t)2 * GEMV_NT * X8_NWI * 16 < x8_bytes(P.w.K) || P.w.N > 65536) return 1;  // image fit; kb_ws rows
+  const int need = ((P.w.K + 255) / 256 + 15) / 16;
+  return mode == 2 || (P.w.qtype == QT_Q6_K && need == 4) ? 2 : 1;
+}
+
+void set_gemv8_kb(int mode) { g_kb = mode; }
+
 void set_gemv8_geo(int nsb, int ks) {
   g_geo_nsb = nsb;
   g_geo_ks = ks;
@@ -306,9 +335,15 @@ bool gemv8_supported(const GemvParams& P) {
   return covered(P, G) && launchable(P, G);
 }
 
-bool gemv8(const GemvParams& P, hipStream_t s) {
+bool gemv8(const GemvParams& P0, hipStream_t s) {
   Geo G;
-  if (!covered(P, G) || !launchable(P, G)) return false;
+  if (!covered(P0, G) || !launchable(P0, G)) return false;
+  GemvParams P = P0;
+  P.kb = choose_kb(P0, G);
+  if (P.kb > 1) {  // each block: 1 / kb of K over 2 in-block groups
+    G.ks = 2;
+    G.grid *= P.kb;
+  }
   count_launch(P.B > 1 ? LC_GEMV8_ROWS : LC_GEMV8_ROW1);
   switch (P.w.qtype) {
     case QT_Q4_K: launch_q<QT_Q4_K>(P, G, s); return true;

@@ -142,15 +142,25 @@ __device__ __forceinline__ void gemv8_body(const GemvParams& P, const int bx) {
   float* part = stage + 48 * BT;                      // [KS - 1][BT][GEMV_NT] partial sums of the K split
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = lane >> 4, s = lane & 15;
   const int kg = KS > 1 ? wave / GEMV_NW : 0, gtid = tid - kg * GEMV_NT;
-  // K-split groups (ks_chunk): aligned to 16 super-blocks when the row stride keeps piece runs on lines
-  const int CH = ks_chunk(SB, KS);
   // lanes stop at the last super-block holding weights: a padded K (weights.py ffn_pad) keeps its runs
   // line-aligned without streaming the zero super-blocks
   const int SBv = P.k_valid > 0 && P.k_valid < K ? n_sb(P.k_valid) : SB;
-  const int sb0 = kg * CH, se = min(SBv, sb0 + CH);
+  // K split across blocks (GemvParams::kb, batch 1 only): block part kp of a tile streams super-blocks
+  // [pa, pe), split again over the KS in-block groups
+  const int KB = BT == 1 && P.kb > 1 ? P.kb : 1;
+  const int kp = KB > 1 ? bx % KB : 0;
+  int pa = 0, pe = SBv;
+  if (KB > 1) {
+    const int SBp = (SBv + KB - 1) / KB;
+    pa = kp * SBp;
+    pe = min(SBv, pa + SBp);
+  }
+  // K-split groups (ks_chunk): aligned to 16 super-blocks when the row stride keeps piece runs on lines
+  const int CH = KB > 1 ? ks_chunk(pe - pa, KS) : ks_chunk(SB, KS);
+  const int sb0 = pa + kg * CH, se = min(pe, sb0 + CH);
   const int n_tiles = (N + 15) / 16;
   const int rbase = (wave - kg * GEMV_NW) * 4 + g;
-  const int tile0 = bx * J;
+  const int tile0 = (KB > 1 ? bx / KB : bx) * J;
 
   // 0. epilogue operands (EpiPre), then 1. the activation operands: both return ahead of the weights
   constexpr bool PRE = BT == 1 || KS <= 2;
@@ -359,6 +369,28 @@ __device__ __forceinline__ void gemv8_body(const GemvParams& P, const int bx) {
     }
 #pragma unroll
     for (int b = 0; b < BT; ++b) acc[0][b] *= rstd[b];
+    if constexpr (BT == 1 && J == 1 && IN != IN_MERGE && IN != IN_X8_LN && (EMIT == EM_ADD || EMIT == EM_NONE)) {
+      if (KB > 1) {  // the tile's K parts meet: sc1 partial stores, agent-scope ticket, last block sums
+        __shared__ int s_last;
+        const float v = row16_sum(acc[0][0]);
+        float* slot = P.kb_ws + ((long long)t * 16 + rbase) * KB;
+        if (kg == 0 && s == 0) __hip_atomic_store(slot + kp, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+          const int old = __hip_atomic_fetch_add(P.kb_cnt + t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const int last = old == KB - 1;
+          if (last) __hip_atomic_store(P.kb_cnt + t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+          s_last = last;
+        }
+        __syncthreads();
+        if (!s_last) return;  // block-uniform
+        float tot = 0.f;
+        if (kg == 0 && s == 0)
+          for (int p = 0; p < KB; ++p) tot += __hip_atomic_load(slot + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        acc[0][0] = tot;  // lane s == 0 of the row group carries the row's sum, the others 0
+      }
+    }
     // LayerNorm: rstd * (dot - mu * c1) + c2, the row's constant terms on one lane of its 16
     if constexpr (IN == IN_X8_LN) {
       if (s == 0) acc[0][0] += pre.c2[j] - mu_rstd * pre.c1[j];

@@ -122,6 +122,12 @@ struct GemvParams {
   const float* ln_c1;          //   [N] W . ln_w
   const float* ln_c2;          //   [N] W . ln_b (+ nothing else: the GEMV's own bias stays in `bias`)
   float* emit8_sum;            // producer (EPI_ADD): per-16-row sums of the new residual (LN consumers)
+  // K split across blocks (gemv8.hip, batch 1, K-split launches of < 256 row tiles): kb blocks share a tile,
+  // each streams 1 / kb of K; row partials meet in kb_ws [N][kb] and the last block of a tile (agent-scope
+  // ticket in kb_cnt[tile], zero-initialised, re-armed) sums them and runs the epilogue. Set by gemv8
+  float* kb_ws;
+  int* kb_cnt;
+  int kb;
 };
 // int8 activation image of a K-wide row (gemv8.hip): [slots] i32x4 codes + [slots] {scale, scale * sum}
 // with one pad slot per 256-element super-block and a trailing dummy slot (the GEMV's LDS layout)
@@ -132,6 +138,13 @@ inline int x8_stat_ld(int K) { return ((K >> 4) + 3) & ~3; }  // RMS-partial flo
 bool gemv8(const GemvParams& P, hipStream_t s);
 bool gemv8_2(const GemvParams& A, const GemvParams& B, hipStream_t s);  // q,k + v rows, one launch
 bool gemv8_supported(const GemvParams& P);
+// Phi-2's parallel block, batch 1 (gemv8_pair.hip): the attention output projection O (merge slabs or plain
+// fp32 input) and ffn_down (int8 image) add into the same residual row in ONE launch, which then emits the
+// next LayerNorm'd image (sums + sums of squares). D: the down GEMV's params (EPI_ADD + emission), O: the
+// O GEMV's (EPI_ADD, same y). false = not covered (the caller launches both)
+bool gemv8_pair(const GemvParams& D, const GemvParams& O, hipStream_t s);
+bool gemv8_pair_supported(const GemvParams& D, const GemvParams& O);
+void set_gemv8_kb(int mode);  // K split across blocks: 0 auto (< 256 row tiles), 1 off, 2 wherever covered
 void set_gemv8_geo(int nsb, int ks);  // microbenchmarks: force (NSB, KS) of K-split plain-image launches
 struct AttnParams;
 
@@ -322,6 +335,7 @@ enum {
   LC_GEMV_FLIGHT,    // gemv.hip / gemv_batch.hip fp32-prologue GEMVs
   LC_ATTN_DECODE,    // attention.hip split flash-decode kernel
   LC_ATTN_PREFILL,   // attention.hip MFMA flash prefill
+  LC_GEMV8_PAIR,     // gemv8_pair.hip Phi-2 O + ffn_down in one launch
   LC_N
 };
 void count_launch(int which);

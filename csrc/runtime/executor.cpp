@@ -1,6 +1,7 @@
 #include "executor.h"
 
 #include <cmath>
+#include <cstdlib>
 #include <stdexcept>
 #include <vector>
 
@@ -22,6 +23,8 @@ static GemvParams base_params(const QMat& w, int B, const float* x, int ldx, con
   P.ldx = ldx;
   P.eps = 1e-5f;
   P.n_sel = 1;
+  P.kb_ws = ws.kb_ws;
+  P.kb_cnt = ws.kb_cnt;
   return P;
 }
 
@@ -305,7 +308,25 @@ void Executor::attn_block(int i, const StepInputs& in, hipStream_t s) {
   } else {
     attention_decode(A, s);
   }
-  // --- output projection (+ residual, or partial sum under TP)
+  // --- output projection (+ residual, or partial sum under TP); Phi-2 on the int8 chain: launched with
+  // ffn_down as one pair kernel (ffn_block, gemv8_pair.hip) when covered
+  if (phi && phi_pair(i, in)) return;
+  GemvParams O = o_params(i, in);
+  if (ch) {
+    chain_in(O, ws.a16, ws.ld_q, nullptr, 0);
+    // range exponents of the residual before O: written by this layer's QKV (st[1] + 16 n + 16)
+    chain_emit(O, ws.xa16, ws.ld_e, L.ffn_norm, ws.st[0], nullptr);  // gate_up's RMSNorm input
+    O.rexp_in = ws.st[1] + 16 * ((E + 15) / 16) + 16;
+  }
+  if (q8 && cfg.tp == 1 && !phi) x8_emit(O, ws.x8e, L.ffn_norm, ws.x8st);  // gate_up's RMSNorm input, int8
+  gemv(O, s);
+}
+
+// the O projection's GEMV: merge slabs of the deferred split (B == 1) or the attention rows
+GemvParams Executor::o_params(int i, const StepInputs& in) const {
+  const LayerW& L = layers[i];
+  const int B = in.B, Eq = cfg.H * cfg.D;
+  const bool defer = ws.defer && B == 1 && ws.n_splits > 1;
   GemvParams O = base_params(L.wo, B, defer ? ws.attn_ws : ws.abuf, Eq, ws);
   if (defer) {
     O.merge_S = ws.n_splits;
@@ -320,15 +341,37 @@ void Executor::attn_block(int i, const StepInputs& in, hipStream_t s) {
     O.epi = EPI_ADD;
     O.y = ws.resid;
   }
-  O.ldy = E;
-  if (ch) {
-    chain_in(O, ws.a16, ws.ld_q, nullptr, 0);
-    // range exponents of the residual before O: written by this layer's QKV (st[1] + 16 n + 16)
-    chain_emit(O, ws.xa16, ws.ld_e, L.ffn_norm, ws.st[0], nullptr);  // gate_up's RMSNorm input
-    O.rexp_in = ws.st[1] + 16 * ((E + 15) / 16) + 16;
+  O.ldy = cfg.E;
+  return O;
+}
+
+// Phi-2's ffn_down on the int8 chain: FFN up's image in, the next layer's QKV / up (or the LM head) image out
+GemvParams Executor::phi_down_params(int i, const StepInputs& in) const {
+  const LayerW& L = layers[i];
+  GemvParams Dn = base_params(L.wdown, in.B, ws.hbuf, cfg.F, ws);
+  Dn.epi = cfg.tp > 1 ? EPI_STORE : EPI_ADD;
+  Dn.bias = L.bdown;
+  Dn.y = cfg.tp > 1 ? tp_dst(1, in.B) : ws.resid;
+  Dn.ldy = cfg.E;
+  Dn.k_valid = cfg.F_valid;
+  if (x8(in)) {
+    const bool last = i + 1 >= (int)layers.size();
+    x8_in(Dn, ws.x8f, nullptr);
+    x8_emit(Dn, ws.x8e, last ? out_norm : layers[i + 1].attn_norm, ws.x8st);
+    Dn.emit8_sum = ws.x8sum;
   }
-  if (q8 && cfg.tp == 1 && !phi) x8_emit(O, ws.x8e, L.ffn_norm, ws.x8st);  // gate_up's RMSNorm input, int8
-  gemv(O, s);
+  return Dn;
+}
+
+// O and ffn_down of a Phi-2 layer in one launch (gemv8_pair.hip): the int8 chain at batch 1, OMX_PHI_PAIR
+// unset or 1
+bool Executor::phi_pair(int i, const StepInputs& in) const {
+  static const int on = [] {
+    const char* e = getenv("OMX_PHI_PAIR");
+    return e ? atoi(e) : 1;
+  }();
+  if (!on || cfg.arch != 1 || cfg.tp != 1 || in.prefill || in.B != 1 || !x8(in)) return false;
+  return gemv8_pair_supported(phi_down_params(i, in), o_params(i, in));
 }
 
 void Executor::ffn_block(int i, const StepInputs& in, hipStream_t s) {
@@ -337,17 +380,10 @@ void Executor::ffn_block(int i, const StepInputs& in, hipStream_t s) {
   float* dst = cfg.tp > 1 ? tp_dst(1, B) : ws.resid;
   const int dst_epi = cfg.tp > 1 ? EPI_STORE : EPI_ADD;
   if (cfg.arch == 1) {  // phi2: up+GELU already done in attn_block
-    GemvParams Dn = base_params(L.wdown, B, ws.hbuf, F, ws);
-    Dn.epi = dst_epi;
-    Dn.bias = L.bdown;
-    Dn.y = dst;
-    Dn.ldy = E;
-    Dn.k_valid = cfg.F_valid;
-    if (x8(in)) {  // FFN up's image in; the next layer's QKV / up (or the LM head) image out
-      const bool last = i + 1 >= (int)layers.size();
-      x8_in(Dn, ws.x8f, nullptr);
-      x8_emit(Dn, ws.x8e, last ? out_norm : layers[i + 1].attn_norm, ws.x8st);
-      Dn.emit8_sum = ws.x8sum;
+    const GemvParams Dn = phi_down_params(i, in);
+    if (phi_pair(i, in)) {  // O (skipped in attn_block) + down, one launch
+      if (!gemv8_pair(Dn, o_params(i, in), s)) throw std::runtime_error("phi2: O + down pair launch declined");
+      return;
     }
     gemv(Dn, s);
     return;

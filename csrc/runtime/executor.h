@@ -97,6 +97,8 @@ struct Workspace {
   void* x8f = nullptr;
   float* x8st = nullptr;
   float* x8sum = nullptr;    // phi2: per-group sums of the E-wide rows (LayerNorm mean), x8st's layout
+  float* kb_ws = nullptr;    // gemv8 K split across blocks: row partials [N][2] and tile tickets (zeroed)
+  int* kb_cnt = nullptr;
   int x8_ok = 0;
   int x8_bmax = 1;           // batch rows the chain takes (continuous batching: up to X8_MAX_B)
 };
@@ -155,6 +157,9 @@ class Executor {
   bool x8_layer0(const StepInputs& in) const;  // the embed writes layer 0's int8 QKV image
   bool x8(const StepInputs& in) const;     // this step runs the batch-1 int8 activation chain
   bool ln8() const;                        // the phi2 (LayerNorm) form of that chain is set up
+  GemvParams o_params(int i, const StepInputs& in) const;         // layer i's O projection GEMV
+  GemvParams phi_down_params(int i, const StepInputs& in) const;  // phi2 layer i's ffn_down GEMV
+  bool phi_pair(int i, const StepInputs& in) const;               // phi2: O + down as one launch
   int ar_active_ = 0;
 };
 

@@ -102,7 +102,7 @@ class NativeExec:
         if not b:
             return {}
         return dict(x8e=b["x8e"].data_ptr(), x8f=b["x8f"].data_ptr(), x8st=b["x8st"].data_ptr(), x8_ok=1,
-                    x8sum=b["x8sum"].data_ptr(),
+                    x8sum=b["x8sum"].data_ptr(), x8kb=b["x8kb"].data_ptr(), x8cnt=b["x8cnt"].data_ptr(),
                     # batch rows on the chain: B = 2 measured 1.73 vs 2.08 ms per step on the int8 rows, B = 3
                     # 2.15 vs 2.19 ms; at 4 rows layout M's MFMA GEMVs win (profiles/r4_batch), so 3 by default
                     x8_bmax=int(os.environ.get("OMX_X8_BATCH", "3")))
@@ -229,7 +229,9 @@ class Runner:
             nb = 4  # batch rows of the chain (gemv8.hip X8_MAX_B): row b's image at b * x8_bytes
             self.x8_bufs = dict(x8e=torch.zeros(nb * C.x8_bytes(E), **u8), x8f=torch.zeros(nb * C.x8_bytes(Fl), **u8),
                                 x8st=torch.zeros(nb * C.x8_stat_ld(E) + 4, **f32),
-                                x8sum=torch.zeros(nb * C.x8_stat_ld(E) + 4, **f32))  # phi2: LayerNorm means
+                                x8sum=torch.zeros(nb * C.x8_stat_ld(E) + 4, **f32),  # phi2: LayerNorm means
+                                # gemv8 K split across blocks: row partials [N][2], tile tickets (self re-arming)
+                                x8kb=torch.zeros(2 * 65536, **f32), x8cnt=torch.zeros(8192, **i32))
         # MoE prefill grouping (csrc/kernels/moe.hip moe_sort -> grouped MFMA GEMM)
         n_pairs = max_batch * ksel
         self.moe_rows = torch.zeros(n_pairs, **i32)

@@ -37,6 +37,7 @@ BIG = [
     ("down13_q4k", GGMLType.Q4_K, 5120, 13824, EPI_ADD, False, True),
     ("down13_q6k", GGMLType.Q6_K, 5120, 13824, EPI_ADD, False, True),
     ("down70_q40", GGMLType.Q4_0, 8192, 28672, EPI_ADD, False, True),
+    ("downphi2_q40", GGMLType.Q4_0, 2560, 10240, EPI_ADD, False, True),
 ]
 # OMX_BENCH_ALIGN=1: down-shaped probes at K = 12288 (48 super-blocks: each K group of the 3-way split
 # gets exactly 16, piece segments 128-B aligned) vs the real K = 11008 (43: 15 + 15 + 13, 688-B strides)
@@ -103,7 +104,12 @@ def main():
         nw = torch.rand(max(N, K), device="cuda") + 0.5
         out = torch.zeros(C.x8_bytes(Ny), dtype=torch.uint8, device="cuda")
         ost = torch.zeros(Ny // 16 + 4, device="cuda")
-        ops = {"x8": img.data_ptr(), "dbg8": int(os.environ.get("OMX_BENCH_DBG8", "0"))}
+        # K split across blocks (OMX_GEMV8_KB in the kernel library: 0 auto, 1 off, 2 on): its row partials
+        # and self re-arming tile tickets
+        kb_ws = torch.zeros(2 * N + 64, device="cuda")
+        kb_cnt = torch.zeros((N + 15) // 16, dtype=torch.int32, device="cuda")
+        ops = {"x8": img.data_ptr(), "dbg8": int(os.environ.get("OMX_BENCH_DBG8", "0")),
+               "kb_ws": kb_ws.data_ptr(), "kb_cnt": kb_cnt.data_ptr()}
         if rms:
             ops["x8_stat"] = st.data_ptr()
         if emits and not os.environ.get("OMX_BENCH_NOEMIT"):  # NOEMIT: the producer without its int8 emission
@@ -134,7 +140,8 @@ def main():
             ts.append(e0.elapsed_time(e1) * 1e3 / n_launch)
         t = float(np.median(ts))
         geo = os.environ.get("OMX_BENCH_GEO")
-        tag = ("hot " if hot else "cold") + (f" geo {geo}" if geo else "") + (" mem-only" if ops["dbg8"] else "") + \
+        kbm = os.environ.get("OMX_GEMV8_KB")
+        tag = ("hot " if hot else "cold") + (f" geo {geo}" if geo else "") + (f" kb {kbm}" if kbm else "") + (" mem-only" if ops["dbg8"] else "") + \
             (" no-emit" if emits and os.environ.get("OMX_BENCH_NOEMIT") else "")
         print(f"{name:9s} {tag} {t:7.2f} us/launch  {nbytes / t / 1e3:7.1f} GB/s  "
               f"({len(tups)} copies, {nbytes / 1e6:.1f} MB)", flush=True)

@@ -149,6 +149,36 @@ def test_wide_k_down_two_superblocks_per_lane(qt, K, emit):
         assert rel(decode_image(out, N), (resid[0] * nw).cpu()) < 1e-2
 
 
+@pytest.mark.parametrize("qt", [GGMLType.Q4_0, GGMLType.Q4_K, GGMLType.Q6_K])
+@pytest.mark.parametrize("N,K,mode", [(2560, 10240, 2), (4096, 11008, 2), (512, 13824, 0)])
+def test_k_split_across_blocks(qt, N, K, mode):
+    """K-split down projections with two blocks per row tile (GemvParams::kb): forced on Phi-2 / 7B shapes,
+    the auto rule at 13B's K (Q6_K). Residual add + emitted image match the fp32 reference and the tile
+    tickets re-arm (the same launch three times)."""
+    m = QM(qt, N, K, seed=31 + int(qt))
+    h = torch.randn(K, device="cuda")
+    img_in, _ = make_image(h)
+    nw = torch.rand(N, device="cuda") + 0.5
+    kb_ws = torch.zeros(2 * N + 64, device="cuda")
+    kb_cnt = torch.zeros((N + 15) // 16, dtype=torch.int32, device="cuda")
+    C().set_gemv8_kb(mode)
+    try:
+        for _ in range(3):
+            resid0 = torch.randn(1, N, device="cuda") * 4
+            resid = resid0.clone()
+            out = torch.zeros(C().x8_bytes(N), dtype=torch.uint8, device="cuda")
+            st = torch.zeros(N // 16 + 4, device="cuda")
+            call(m, 1, None, resid, EPI_ADD, {"x8": img_in.data_ptr(), "emit8": out.data_ptr(), "emit8_nw": nw.data_ptr(),
+                                              "emit8_stat": st.data_ptr(), "kb_ws": kb_ws.data_ptr(),
+                                              "kb_cnt": kb_cnt.data_ptr()})
+            torch.cuda.synchronize()
+            assert rel(resid - resid0, (h @ m.w.T)[None]) < 1.5e-2
+            assert rel(decode_image(out, N), (resid[0] * nw).cpu()) < 1e-2
+            assert int(kb_cnt.abs().sum()) == 0
+    finally:
+        C().set_gemv8_kb(0)
+
+
 @pytest.mark.parametrize("S_", [1, 2, 4])
 def test_merge_producer(S_):
     """O projection: deferred flash-decode partial slabs (or a plain fp32 row) in, residual + image out."""
@@ -255,14 +285,53 @@ def test_engine_phi2_ln_chain_matches_torch(tmp_path, ftype):
             torch.cuda.synchronize()
             if eager and r is g:
                 n = C().launch_counts()
-                # QKV + FFN up (one dual launch), down of every layer plus the LM head on the chain (O takes
-                # gemv8 too once attention defers its split merge: test_engine_gpu deferred-merge test)
-                assert n["gemv8_dual"] == L and n["gemv8_row1"] >= L + 1, n
+                # QKV + FFN up (one dual launch) and O + down (one pair launch, gemv8_pair.hip, when both
+                # have the same quant type) of every layer plus the LM head on the chain
+                assert n["gemv8_dual"] == L, n
+                if ftype == "MOSTLY_Q4_0":
+                    assert n["gemv8_pair"] == L and n["gemv_flight"] == 0, n
+                else:  # per layer: the pair, or O apart (fp32 rows at this length: gemv.hip) and down on gemv8
+                    assert n["gemv8_pair"] + n["gemv_flight"] == L, n
             r.kv.seqs[sid].tokens.append(t)
             outs.append(r.logits[0, :V].float().cpu().clone())
         c.prefill(sc, [t])
         assert rel(outs[0], c.logits[0, :V]) < 3e-2, i
         assert rel(outs[0], outs[1]) < 2e-2, i
+
+
+def test_engine_phi2_pair_deferred_splits(tmp_path):
+    """Phi-2 Q4_0 decode with O + ffn_down in one launch (gemv8_pair.hip) at lengths in every deferred split
+    bucket (the pair kernel merges 1 / 2 / 4 / 8 attention slabs itself): logits track the fp32 torch twin
+    and every layer took the pair launch."""
+    from ollama_operator_amd.engine.runner import Runner
+    from ollama_operator_amd.gguf.constants import FileType
+    from ollama_operator_amd.models.config import preset
+    from ollama_operator_amd.models.random_init import write_random_gguf
+    p = str(tmp_path / "phi.gguf")
+    write_random_gguf(p, preset("tiny-phi2", ctx_len=2048), FileType.MOSTLY_Q4_0, seed=8, quantize_from_float=True)
+    g = Runner(p, device="cuda:0", max_batch=64, max_seqs=1, ctx=1100)
+    assert g.exe.exe.x8_on == 1 and g._defer_ok
+    g.use_graphs = False  # launch counters count enqueues
+    c = Runner(p, device="cpu", max_batch=64, max_seqs=1, ctx=1100, cpu_backend="torch")
+    rng = np.random.default_rng(5)
+    V, L = g.cfg.n_vocab, g.cfg.n_layer
+    seen = set()
+    for n_keys in (60, 200, 400, 900):
+        toks = [1] + [int(x) for x in rng.integers(3, 500, n_keys - 1)]
+        seen.add(g.decode_splits(n_keys + 1))
+        sg, sc = g.new_sequence(), c.new_sequence()
+        g.prefill(sg, toks)
+        c.prefill(sc, toks + [77])
+        g.d_tokens[0] = 77
+        C().reset_launch_counts()
+        g.decode_step(sg, n_keys)
+        torch.cuda.synchronize()
+        n = C().launch_counts()
+        assert n["gemv8_pair"] == L and n["gemv_flight"] == 0, (n_keys, n)
+        assert rel(g.logits[0, :V].float().cpu(), c.logits[0, :V]) < 3e-2, n_keys
+        g.free_sequence(sg)
+        c.free_sequence(sc)
+    assert seen == {1, 2, 4, 8}
 
 
 def images(xs, nw=None):
