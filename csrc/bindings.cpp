@@ -356,13 +356,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("add_inplace", [](uintptr_t y, uintptr_t x, long long n, uintptr_t stream) {
     add_inplace(Pp<float>(y), Pp<const float>(x), n, S(stream));
   });
-  m.def("decode_feedback", [](uintptr_t step, int ld, uintptr_t sampled, int B, int advance, uintptr_t block_table,
-                              int max_blocks, int bs, uintptr_t host_ring, int ring, uintptr_t stream) {
-    if (B <= 0 || B > ld) throw std::runtime_error("decode_feedback: bad B");
-    if (host_ring && ring <= 0) throw std::runtime_error("decode_feedback: bad ring");
-    decode_feedback(Pp<int>(step), ld, Pp<const int>(sampled), B, advance, Pp<const int>(block_table), max_blocks,
-                    bs, Pp<int>(host_ring), ring, S(stream));
-  });
   m.def("mfma_layout_bytes", &mfma_layout_bytes);
   m.def("x8_bytes", [](int K) { return x8_bytes(K); });
   m.def("x8_stat_ld", [](int K) { return x8_stat_ld(K); });

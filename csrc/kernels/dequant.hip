@@ -1,7 +1,6 @@
 // Row gather + dequantisation from the repacked quant streams (SURVEY.md §2.2 N15 embedding
 // gather) and whole-matrix dequantisation to fp16 (resident fp16 copies for MFMA prefill GEMMs).
 #include "common.h"
-#include "feedback.h"
 #include "gemv8_core.h"
 #include "ops.h"
 
@@ -178,24 +177,6 @@ __global__ void add_inplace_kernel(float* y, const float* x, long long n) {
 void add_inplace(float* y, const float* x, long long n, hipStream_t s) {
   const int blocks = (int)((n + 255) / 256 < 2048 ? (n + 255) / 256 : 2048);
   hipLaunchKernelGGL(add_inplace_kernel, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, s, y, x, n);
-}
-
-// Decode-step feedback: row b's sampled token becomes its next input (step row 5), and with
-// `advance` the step inputs move to the next position on device -- pos + 1, its KV slot from the
-// block table, q_len -- so consecutive replays need no host upload (feedback.h).
-// (The sampler does the same per row when given SampleParams::fb_step; this launch stays for the
-// paths that sample on the host.)
-__global__ void decode_feedback_kernel(int* step, int ld, const int* sampled, int B, int advance,
-                                       const int* block_table, int max_blocks, int bs, int* host_ring, int ring) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= B) return;
-  decode_feedback_row(step, ld, b, sampled[b], advance, block_table, max_blocks, bs, host_ring, ring);
-}
-
-void decode_feedback(int* step, int ld, const int* sampled, int B, int advance, const int* block_table,
-                     int max_blocks, int bs, int* host_ring, int ring, hipStream_t s) {
-  hipLaunchKernelGGL(decode_feedback_kernel, dim3((B + 63) / 64), dim3(64), 0, s, step, ld, sampled, B, advance,
-                     block_table, max_blocks, bs, host_ring, ring);
 }
 
 __global__ __launch_bounds__(256) void rmsnorm_kernel(const float* x, const float* w, float eps, int n, float* out) {

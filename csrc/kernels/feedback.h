@@ -1,5 +1,5 @@
-// Decode-step token feedback for one row, shared by the decode_feedback kernel (dequant.hip) and the
-// sampler's finishing lane (sampling.hip, SampleParams::fb_step). step: int32 [6][ld] =
+// Decode-step token feedback for one row, run by the sampler's finishing lane (sampling.hip,
+// SampleParams::fb_step; it replaced a separate feedback launch per decode step). step: int32 [6][ld] =
 // (pos, slot, q_len, q_seq, logit_idx, tokens), engine/runner.py d_step.
 // host_ring (row 0 only): the sampled token also goes straight to host-mapped pinned memory,
 // slot = input position % ring, so the host reads it after the step's event (no D2H copy command).

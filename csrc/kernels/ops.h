@@ -272,9 +272,9 @@ struct SampleParams {
   // optional error word: set to 1 when a row's choice was out of range (non-finite logits); the id
   // itself is clamped to 0 so the next step's embedding read stays in bounds, the host fails the request
   int* err = nullptr;
-  // optional decode feedback (null fb_step = none): the row's finishing lane also does what
-  // decode_feedback does -- token into the step block, host ring (row 0), advance to the next
-  // position -- so a decode step has no separate feedback launch
+  // optional decode feedback (null fb_step = none): the row's finishing lane also feeds the token back
+  // (feedback.h) -- token into the step block, host ring (row 0), advance to the next position -- so a
+  // decode step has no separate feedback launch
   int* fb_step = nullptr;
   int fb_ld = 0, fb_max_blocks = 0, fb_bs = 0, fb_ring = 0;
   const int* fb_block_table = nullptr;
@@ -345,8 +345,6 @@ void reset_launch_counts();
 // small elementwise helpers
 void add_inplace(float* y, const float* x, long long n, hipStream_t s);
 void widen_q6k(const QMat& w, void* out, hipStream_t s);  // out: N * SB * 256 bytes
-void decode_feedback(int* step, int ld, const int* sampled, int B, int advance, const int* block_table,
-                     int max_blocks, int bs, int* host_ring, int ring, hipStream_t s);
 void rmsnorm(const float* x, const float* w, float eps, int rows, int n, float* out, hipStream_t s);
 
 }  // namespace omx

@@ -589,7 +589,7 @@ class Runner:
 
     def _sample(self, B: int, feedback: bool = False):
         """feedback (GPU): the sampler's finishing lane of each row also feeds the token back and
-        advances the row (what decode_feedback does), saving that launch in every decode step."""
+        advances the row (csrc/kernels/feedback.h; a separate launch per decode step before round 6)."""
         lg = self.full_logits
         if self.is_gpu:
             p = lambda t: t.data_ptr()  # noqa: E731
@@ -716,7 +716,7 @@ class Runner:
     def decode_steps(self, sid: int, pos: int, k: int) -> None:
         """k consecutive batch-1 decode steps of sequence `sid` from input position `pos`, as ONE graph
         replay when graphs are on (generate's pipelined loop): the boundary between two replayed graphs
-        costs ~13 us of idle GPU (profiles/r5_decode step traces, the gap after decode_feedback), paid once
+        costs ~13 us of idle GPU (profiles/r5_decode step traces, the gap after the step's last kernel), paid once
         per k tokens instead of once per token. Every step of the group uses the split bucket of the
         group's last length (any bucket is exact; only its speed depends on the length)."""
         if k <= 1 or not (self.is_gpu and self.use_graphs):

@@ -141,8 +141,8 @@ def main():
         t = float(np.median(ts))
         geo = os.environ.get("OMX_BENCH_GEO")
         kbm = os.environ.get("OMX_GEMV8_KB")
-        tag = ("hot " if hot else "cold") + (f" geo {geo}" if geo else "") + (f" kb {kbm}" if kbm else "") + (" mem-only" if ops["dbg8"] else "") + \
-            (" no-emit" if emits and os.environ.get("OMX_BENCH_NOEMIT") else "")
+        tag = ("hot " if hot else "cold") + (f" geo {geo}" if geo else "") + (f" kb {kbm}" if kbm else "")
+        tag += (" mem-only" if ops["dbg8"] else "") + (" no-emit" if emits and os.environ.get("OMX_BENCH_NOEMIT") else "")
         print(f"{name:9s} {tag} {t:7.2f} us/launch  {nbytes / t / 1e3:7.1f} GB/s  "
               f"({len(tups)} copies, {nbytes / 1e6:.1f} MB)", flush=True)
         del g, tups, keep
