@@ -316,6 +316,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("dq_gemm_enabled", &dq_gemm_enabled);
   m.def("set_gemv8_geo", [](int nsb, int ks) { set_gemv8_geo(nsb, ks); });
   m.def("set_gemv8_kb", [](int mode) { set_gemv8_kb(mode); });
+  m.def("gemv8_merge_supported", &gemv8_merge_supported);
   m.def("set_dq_ring", &set_dq_ring, "1: prefill dq GEMMs on the register-ring kernel, 0: the glds kernel");
   // launch counters (ops.h LC_*): tests assert which kernel family a call enqueued
   m.def("launch_counts", []() {

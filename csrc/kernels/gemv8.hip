@@ -148,7 +148,7 @@ bool covered(const GemvParams& P, Geo& G) {
   if (!geometry(P, G)) return false;
   // merge prologue: one 16-element group per thread and group slot (NSB slots); the deferred merge
   // (merge_S > 1) exists for the unsplit geometry only
-  if (in == IN_MERGE && (P.w.K > GEMV_NT * G.ks * G.nsb * 16 || (P.merge_S > 1 && G.ks > 1))) return false;
+  if (in == IN_MERGE && (P.w.K > GEMV_NT * G.ks * G.nsb * 16 || (P.merge_S > 1 && G.ks > 2))) return false;
   if (em == EM_GLU && G.J != 2) return false;  // a block owns whole groups: two tiles, unsplit K
   if (in != IN_MERGE && (size_t)G.ks * GEMV_NT * x8_nwi(G.nsb, G.ks) * 16 < x8_bytes(P.w.K)) return false;
   if (bt_of(P.B) >= 3 && !bt4_ok(q, G.ks, in)) return false;
@@ -207,8 +207,13 @@ void launch_in(const GemvParams& P, const Geo& G, hipStream_t s) {
       else launch_k<QT, NSB, J, KS, IN_X8_LN, 0, EM_NONE, 1>(P, G.grid, s);
     }
   }
-  else if constexpr (NSB == 1 && KS == 2 && J == 1) {  // O at 4096 < K <= 8192: plain fp32 rows
-    launch_em<QT, 1, 1, 2, IN_MERGE, 1>(P, em, G.grid, s);
+  else if constexpr (NSB == 1 && KS == 2 && J == 1) {  // O at 4096 < K <= 8192: merge slabs or plain fp32
+    switch (P.merge_S) {
+      case 2: launch_em<QT, 1, 1, 2, IN_MERGE, 2>(P, em, G.grid, s); break;
+      case 4: launch_em<QT, 1, 1, 2, IN_MERGE, 4>(P, em, G.grid, s); break;
+      case 8: launch_em<QT, 1, 1, 2, IN_MERGE, 8>(P, em, G.grid, s); break;
+      default: launch_em<QT, 1, 1, 2, IN_MERGE, 1>(P, em, G.grid, s); break;
+    }
   } else if constexpr (NSB == 1 && KS == 1 && J == 1) {  // the O projection: merge slabs or plain fp32
     switch (P.merge_S) {
       case 2: launch_em<QT, 1, 1, 1, IN_MERGE, 2>(P, em, G.grid, s); break;
@@ -324,6 +329,12 @@ static int choose_kb(const GemvParams& P, const Geo& G) {
 }
 
 void set_gemv8_kb(int mode) { g_kb = mode; }
+
+// the deferred flash-decode merge in the int8-chain O projection: K = H * D up to 8192 (Llama-2-13B /
+// 70B: a 2-way in-block K split), 2 / 4 / 8 slabs
+bool gemv8_merge_supported(int K, int D, int S) {
+  return K <= 8192 && K % 16 == 0 && D % 16 == 0 && D > 0 && K % D == 0 && (S == 2 || S == 4 || S == 8);
+}
 
 void set_gemv8_geo(int nsb, int ks) {
   g_geo_nsb = nsb;

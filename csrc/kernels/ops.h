@@ -152,6 +152,7 @@ struct AttnParams;
 // when an fp16 activation workspace is given (prefill); same epilogues either way.
 void gemv(const GemvParams& P, hipStream_t s);
 bool gemv_merge_supported(int B, int K, int D, int S);
+bool gemv8_merge_supported(int K, int D, int S);  // the same merge in the int8-chain O GEMV (K <= 8192)
 // two GEMVs over the same x (same K, RMS norm prologue) in one launch when B == 1, else two launches
 void gemv2(const GemvParams& A, const GemvParams& B, hipStream_t s);
 constexpr int GEMM_MIN_B = 16;

@@ -291,7 +291,8 @@ void Executor::attn_block(int i, const StepInputs& in, hipStream_t s) {
   A.prefill = in.prefill;
   // deferred split merge (B == 1): the O projection's prologue merges the partial slabs
   const bool defer = ws.defer && B == 1 && ws.n_splits > 1;
-  if (defer && !gemv_merge_supported(B, Eq, cfg.D, ws.n_splits))
+  if (defer && !gemv_merge_supported(B, Eq, cfg.D, ws.n_splits) &&
+      !(x8(in) && cfg.tp == 1 && gemv8_merge_supported(Eq, cfg.D, ws.n_splits)))
     throw std::runtime_error("deferred attention merge: unsupported (K, D, splits)");
   A.defer = defer;
   if (ch) A.out16 = ws.a16;

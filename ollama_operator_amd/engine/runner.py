@@ -310,8 +310,14 @@ class Runner:
         # keys, but in the model it measured equal at 2.2k keys and 3 % behind at 2.6-2.9k
         # (experiments/ab/defer_s4.py, profiles/r6_attn/defer_s4_ab.log)
         self.defer_s4_max = int(os.environ.get("OMX_DEFER_S4_MAX", "0"))
-        self._defer_ok = (self.is_gpu and os.environ.get("OMX_DEFER_MERGE", "1") != "0" and
-                          native().gemv_merge_supported(1, Eq, loc["D"], 8) and self.n_splits(1) >= 8)
+        # the O GEMV merges the slabs: gemv.hip for K <= 4096; the int8-chain GEMV up to K = 8192 (13B / 70B)
+        # only with OMX_DEFER_KSPLIT=1 -- measured 343 vs 341 tok/s for 13B at short context but 273 vs 297
+        # at 2k keys, and no gain for 70B (profiles/r6_models/defer_ksplit); checked again once the executor
+        # reports the chain on, below
+        ksplit = os.environ.get("OMX_DEFER_KSPLIT", "0") == "1"
+        self._defer_ok = (self.is_gpu and os.environ.get("OMX_DEFER_MERGE", "1") != "0" and self.n_splits(1) >= 8 and
+                          (native().gemv_merge_supported(1, Eq, loc["D"], 8) or
+                           (ksplit and tp_size == 1 and native().gemv8_merge_supported(Eq, loc["D"], 8))))
         self._decode_S = 0
         self._adv_next = None  # (sid, pos) the device step inputs were advanced to by the last decode
         # TP decode collectives: one-shot all-reduce over peer-mapped slabs (parallel/custom_ar.py),
@@ -323,6 +329,8 @@ class Runner:
             self.ar = CustomAllReduce(tp_group, tp_rank, tp_size, rows * max(E, Vl))
         if self.is_gpu:
             self.exe = NativeExec(self)
+            if self._defer_ok and not native().gemv_merge_supported(1, Eq, loc["D"], 8) and not self.exe.exe.x8_on:
+                self._defer_ok = False  # K > 4096 merges only on the int8 chain
         else:
             from ..ops.cpu import cpu_module
             choice = cpu_backend or os.environ.get("OMX_CPU_BACKEND") or ("native" if cpu_module() else "torch")

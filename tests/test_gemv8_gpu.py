@@ -481,7 +481,7 @@ def test_plain_o_projection_k_split(qt, B, K):
         assert rel(decode_image(out[b * nbE:(b + 1) * nbE], E), (resid[b] * nw).cpu()) < 1e-2, b
 
 
-def test_engine_x8_chain_covers_13b_shapes(tmp_path):
+def test_engine_x8_chain_covers_13b_shapes(tmp_path, monkeypatch):
     """A 2-layer model with Llama-2-13B's widths (E = 5120, 40 heads, F = 13824) decodes on the int8
     chain and matches the fp32 torch twin."""
     from ollama_operator_amd.engine.runner import Runner
@@ -489,13 +489,14 @@ def test_engine_x8_chain_covers_13b_shapes(tmp_path):
     from ollama_operator_amd.models.config import preset
     from ollama_operator_amd.models.random_init import write_random_gguf
     import dataclasses
-    cfg = dataclasses.replace(preset("llama2-13b", ctx_len=256), n_layer=2, n_vocab=512)
+    cfg = dataclasses.replace(preset("llama2-13b", ctx_len=512), n_layer=2, n_vocab=512)
     p = str(tmp_path / "m.gguf")
     write_random_gguf(p, cfg, FileType.MOSTLY_Q4_K_M, seed=3, quantize_from_float=True)
-    g = Runner(p, device="cuda:0", max_batch=64, max_seqs=1, ctx=256)
-    assert g.exe.exe.x8_on == 1
+    monkeypatch.setenv("OMX_DEFER_KSPLIT", "1")  # opt-in: K = 5120, the int8-chain O merges the deferred slabs
+    g = Runner(p, device="cuda:0", max_batch=64, max_seqs=1, ctx=512)
+    assert g.exe.exe.x8_on == 1 and g._defer_ok
     g.use_graphs = False  # launch counters count enqueues
-    c = Runner(p, device="cpu", max_batch=64, max_seqs=1, ctx=256, cpu_backend="torch")
+    c = Runner(p, device="cpu", max_batch=64, max_seqs=1, ctx=512, cpu_backend="torch")
     prompt = [1] + [(11 * i + 3) % 500 for i in range(1, 20)]
     sids = {id(r): r.new_sequence() for r in (g, c)}
     for r in (g, c):
@@ -514,6 +515,25 @@ def test_engine_x8_chain_covers_13b_shapes(tmp_path):
         g.kv.seqs[sids[id(g)]].tokens.append(t)
         c.prefill(sids[id(c)], [t])
         assert rel(g.logits[0, :V].float().cpu(), c.logits[0, :V]) < 3e-2
+    # past 128 / 256 keys: 2 / 4 deferred attention splits, merged in the O GEMV's prologue at a 2-way K split
+    for r in (g, c):
+        r.free_sequence(sids[id(r)])
+    rng = np.random.default_rng(9)
+    for n_keys in (200, 400):
+        toks = [1] + [int(x) for x in rng.integers(3, 500, n_keys - 1)]
+        sg, sc = g.new_sequence(), c.new_sequence()
+        g.prefill(sg, toks)
+        c.prefill(sc, toks + [77])
+        g.d_tokens[0] = 77
+        assert g.decode_splits(n_keys + 1) in (2, 4)
+        C().reset_launch_counts()
+        g.decode_step(sg, n_keys)
+        torch.cuda.synchronize()
+        n = C().launch_counts()
+        assert n["gemv_flight"] <= 1, n
+        assert rel(g.logits[0, :V].float().cpu(), c.logits[0, :V]) < 3e-2, n_keys
+        g.free_sequence(sg)
+        c.free_sequence(sc)
 
 
 @pytest.mark.parametrize("B", [1, 2])
