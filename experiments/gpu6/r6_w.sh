@@ -2,7 +2,7 @@
 # round 6 (w): rehearsal of the driver's round-end tiers on the current tree: full GPU suite, smoke(),
 # bench.py with no flags (headline line), 256-step bench
 set -o pipefail
-O=gpurun_out/r6_w
+O=gpurun_out/${OUT:-r6_w}
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1; rc=$?

@@ -84,6 +84,8 @@ def main():
         big.add_(1)
     torch.cuda.synchronize()
     del big
+    if os.environ.get("OMX_BENCH_BPC"):  # persistent-grid cap per CU: the J (tiles per block) rule of gemv8
+        C.set_gemv_tuning(int(os.environ["OMX_BENCH_BPC"]), 1, 0)
     if os.environ.get("OMX_BENCH_GEO"):
         C.set_gemv8_geo(*[int(v) for v in os.environ["OMX_BENCH_GEO"].split(",")])
     shapes = SHAPES + (ALIGN if os.environ.get("OMX_BENCH_ALIGN") else []) + \
@@ -141,7 +143,9 @@ def main():
         t = float(np.median(ts))
         geo = os.environ.get("OMX_BENCH_GEO")
         kbm = os.environ.get("OMX_GEMV8_KB")
+        bpc = os.environ.get("OMX_BENCH_BPC")
         tag = ("hot " if hot else "cold") + (f" geo {geo}" if geo else "") + (f" kb {kbm}" if kbm else "")
+        tag += f" bpc {bpc}" if bpc else ""
         tag += (" mem-only" if ops["dbg8"] else "") + (" no-emit" if emits and os.environ.get("OMX_BENCH_NOEMIT") else "")
         print(f"{name:9s} {tag} {t:7.2f} us/launch  {nbytes / t / 1e3:7.1f} GB/s  "
               f"({len(tups)} copies, {nbytes / 1e6:.1f} MB)", flush=True)
