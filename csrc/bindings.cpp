@@ -421,6 +421,7 @@ PYBIND11_MODULE(_C, m) {
       P.fb_bs = d["fb_bs"].cast<int>();
       P.fb_host_ring = Pp<int>(d.contains("fb_host_ring") ? d["fb_host_ring"].cast<uintptr_t>() : 0);
       P.fb_ring = d.contains("fb_ring") ? d["fb_ring"].cast<int>() : 0;
+      P.fb_sysfence = d.contains("fb_sysfence") ? d["fb_sysfence"].cast<int>() : 1;
       if (P.B > P.fb_ld || P.fb_bs <= 0 || P.fb_max_blocks <= 0) throw std::runtime_error("sample: bad feedback args");
       if (P.fb_host_ring && P.fb_ring <= 0) throw std::runtime_error("sample: bad feedback ring");
     }

@@ -6,13 +6,15 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+// sysfence: a system-scope fence after the host-ring store (0: the store alone; the host reads the ring
+// only after the step's event, whose completion signal is itself a system-scope release)
 __device__ __forceinline__ void decode_feedback_row(int* step, int ld, int b, int tok, int advance,
                                                     const int* block_table, int max_blocks, int bs,
-                                                    int* host_ring, int ring) {
+                                                    int* host_ring, int ring, int sysfence = 1) {
   step[5 * ld + b] = tok;
   if (host_ring && b == 0) {
     __hip_atomic_store(host_ring + step[0] % ring, tok, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __threadfence_system();
+    if (sysfence) __threadfence_system();
   }
   if (!advance) return;
   const int pos = step[b] + 1;

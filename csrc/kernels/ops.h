@@ -280,6 +280,8 @@ struct SampleParams {
   int fb_ld = 0, fb_max_blocks = 0, fb_bs = 0, fb_ring = 0;
   const int* fb_block_table = nullptr;
   int* fb_host_ring = nullptr;
+  int fb_sysfence = 1;           // system-scope fence after the host-ring store (feedback.h; the runner
+                                 // passes 0: its host reads a slot only after the step's event)
 };
 constexpr int SAMPLE_WS_FLOATS_PER_ROW(int V) { return ((V + 1023) / 1024) * 2 * 64; }
 void sample(const SampleParams& P, hipStream_t s);

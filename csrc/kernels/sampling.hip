@@ -297,7 +297,7 @@ __device__ __forceinline__ void finish_sample(const SampleParams& P, int b, int 
   P.hist_count[b] = seen + 1;
   P.step[b] += 1;
   if (P.fb_step) decode_feedback_row(P.fb_step, P.fb_ld, b, chosen, 1, P.fb_block_table, P.fb_max_blocks, P.fb_bs,
-                                     P.fb_host_ring, P.fb_ring);
+                                     P.fb_host_ring, P.fb_ring, P.fb_sysfence);
 }
 
 __global__ __launch_bounds__(SAMPLE_NT) void sample_kernel(SampleParams P) {

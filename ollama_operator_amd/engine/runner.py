@@ -298,6 +298,11 @@ class Runner:
         # OMX_GRAPH_PAIR=1 (A/B knob): batch-1 decode alternates between two captured instances of each
         # step graph, so a replay never re-launches the executable the previous replay is still running
         self.graph_pair = os.environ.get("OMX_GRAPH_PAIR", "0") == "1"
+        # system-scope fence after the sampler's host-ring store: off by default (OMX_RING_FENCE=1 restores
+        # it). The host reads a ring slot only after that step's event, whose completion is itself a
+        # system-scope release of every earlier write; the fence inside the graph cost 707 -> 724 tok/s on
+        # the 256-step headline (profiles/r6_decode/ring_fence)
+        self.ring_fence = 1 if os.environ.get("OMX_RING_FENCE", "0") == "1" else 0
         self.steps_issued = 0  # decode steps enqueued so far (batched steps count once): bench timing
         # past 8 x defer_kps keys, up to 8 x 512: 8 deferred splits of ceil(len / 8) keys (OMX_DEFER_LONG=1,
         # default: attention 14.4 -> 11.6 us at 2k keys, the O prologue's 8-slab merge 4.9 -> 7.1 us, net
@@ -611,7 +616,8 @@ class Runner:
             if feedback:
                 d.update(fb_step=p(self.d_step), fb_ld=self.d_step.shape[1], fb_block_table=p(self.d_block_table),
                          fb_max_blocks=self.max_blocks, fb_bs=self.block_size,
-                         fb_host_ring=self._host_ring_dev if B == 1 else 0, fb_ring=self._ring_n)
+                         fb_host_ring=self._host_ring_dev if B == 1 else 0, fb_ring=self._ring_n,
+                         fb_sysfence=self.ring_fence)
             native().sample(d, stream_handle())
         else:
             for b in range(B):
