@@ -291,9 +291,9 @@ class Runner:
         # merges them in its activation prologue (no in-launch ticket + re-read)
         self.defer_kps = int(os.environ.get("OMX_DEFER_KPS", "128"))
         # batch-1 generation: decode steps per graph replay (1 = one token per replay)
-        # (default 1: the A/B in profiles/r6_decode measured 4-step graphs 1.3 % slower per step -- the
-        # ~13 us boundary between two replays disappears inside a group, but the larger graph ran with
-        # more idle time between its kernels)
+        # (default 1: with the sampler's host-ring fence in every step, 4-step graphs measured 1.3 % slower;
+        # without it 0.5 % faster (profiles/r6_decode/group_ab_nofence.log) -- not worth streaming tokens
+        # in bursts and computing up to k - 1 steps past a stop)
         self.decode_group = max(1, int(os.environ.get("OMX_DECODE_GROUP", "1")))
         # OMX_GRAPH_PAIR=1 (A/B knob): batch-1 decode alternates between two captured instances of each
         # step graph, so a replay never re-launches the executable the previous replay is still running
